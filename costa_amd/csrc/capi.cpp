@@ -1,0 +1,357 @@
+// extern "C" boundary (include/costa_hip.h) and the C++ transform API
+// (include/costa/transform.hpp).  No exception crosses the C boundary.
+#include "engine.hpp"
+
+#include <costa/transform.hpp>
+
+#include <cctype>
+#include <complex>
+#include <cstring>
+#include <new>
+
+struct costa_layout_s {
+    costa::engine::elayout e;
+};
+struct costa_comm_s {
+    costa::engine::comm* c = nullptr;
+};
+
+namespace {
+thread_local std::string g_last_error;
+
+template <typename F>
+int guarded(F&& f) {
+    try {
+        f();
+        return COSTA_OK;
+    } catch (const costa::engine::error& e) {
+        g_last_error = e.what();
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        g_last_error = "out of host memory";
+        return COSTA_ERR_INTERNAL;
+    } catch (const std::exception& e) {
+        g_last_error = e.what();
+        return COSTA_ERR_ARG;
+    } catch (...) {
+        g_last_error = "unknown error";
+        return COSTA_ERR_INTERNAL;
+    }
+}
+
+using costa::engine::dtype_size;
+using costa::engine::elayout;
+using costa::engine::job;
+using costa::engine::scal;
+
+template <typename F>
+void with_type(costa_dtype_t t, F&& f) {
+    switch (t) {
+    case COSTA_FLOAT: f(float{}); return;
+    case COSTA_DOUBLE: f(double{}); return;
+    case COSTA_CFLOAT: f(std::complex<float>{}); return;
+    case COSTA_CDOUBLE: f(std::complex<double>{}); return;
+    case COSTA_INT32: f(int{}); return;
+    }
+    throw costa::engine::error(COSTA_ERR_ARG, "unknown dtype");
+}
+
+scal make_scal(costa_dtype_t t, const void* a, const void* b) {
+    scal s;
+    const size_t E = dtype_size(t);
+    std::memcpy(s.alpha.data(), a, E);
+    std::memcpy(s.beta.data(), b, E);
+    return s;
+}
+
+void check_handles(int n, const costa_layout_t* A, const costa_layout_t* C) {
+    if (n <= 0 || !A || !C) throw costa::engine::error(COSTA_ERR_ARG, "costa: empty batch");
+    for (int i = 0; i < n; ++i)
+        if (!A[i] || !C[i]) throw costa::engine::error(COSTA_ERR_ARG, "costa: null layout");
+}
+
+std::vector<job> make_jobs(int n, const costa_layout_t* A, const costa_layout_t* C,
+                           const char* trans, const void* alpha, const void* beta) {
+    check_handles(n, A, C);
+    const costa_dtype_t t = A[0]->e.dtype;
+    const size_t E = dtype_size(t);
+    std::vector<job> jobs(static_cast<size_t>(n));
+    for (int i = 0; i < n; ++i) {
+        jobs[size_t(i)].A = &A[i]->e;
+        jobs[size_t(i)].C = &C[i]->e;
+        jobs[size_t(i)].trans = trans ? trans[i] : 'N';
+        jobs[size_t(i)].s = make_scal(t, static_cast<const char*>(alpha) + size_t(i) * E,
+                                      static_cast<const char*>(beta) + size_t(i) * E);
+    }
+    return jobs;
+}
+}  // namespace
+
+extern "C" {
+
+const char* costa_hip_last_error(void) { return g_last_error.c_str(); }
+int costa_hip_version(void) { return 100; }
+
+int costa_hip_block_cyclic_layout(costa_dtype_t dtype, int m, int n, int block_m, int block_n,
+                                  int i, int j, int sub_m, int sub_n, int p_m, int p_n,
+                                  char rank_grid_ordering, int rsrc, int csrc, void* ptr, int lld,
+                                  char data_ordering, int rank, costa_layout_t* out) {
+    return guarded([&] {
+        if (!out) throw costa::engine::error(COSTA_ERR_ARG, "null output handle");
+        auto h = std::make_unique<costa_layout_s>();
+        with_type(dtype, [&](auto z) {
+            using T = decltype(z);
+            auto L = costa::block_cyclic_layout<T>(m, n, block_m, block_n, i, j, sub_m, sub_n, p_m,
+                                                   p_n, rank_grid_ordering, rsrc, csrc,
+                                                   static_cast<T*>(ptr), lld, data_ordering, rank);
+            h->e = costa::engine::erase(L);
+        });
+        *out = h.release();
+    });
+}
+
+int costa_hip_custom_layout(costa_dtype_t dtype, int rowblocks, int colblocks, const int* rowsplit,
+                            const int* colsplit, const int* owners, int nlocalblocks,
+                            const costa_block_t* localblocks, char ordering, costa_layout_t* out) {
+    static_assert(sizeof(costa_block_t) == sizeof(costa::block_t), "block_t layout");
+    return guarded([&] {
+        if (!out || !rowsplit || !colsplit || !owners || (nlocalblocks > 0 && !localblocks))
+            throw costa::engine::error(COSTA_ERR_ARG, "null argument");
+        auto h = std::make_unique<costa_layout_s>();
+        with_type(dtype, [&](auto z) {
+            using T = decltype(z);
+            auto L = costa::custom_layout<T>(rowblocks, colblocks, rowsplit, colsplit, owners,
+                                             nlocalblocks,
+                                             reinterpret_cast<const costa::block_t*>(localblocks),
+                                             ordering);
+            h->e = costa::engine::erase(L);
+        });
+        *out = h.release();
+    });
+}
+
+void costa_hip_layout_destroy(costa_layout_t layout) { delete layout; }
+
+int costa_hip_layout_num_blocks(costa_layout_t layout) {
+    return layout ? int(layout->e.blocks.size()) : -1;
+}
+
+int costa_hip_layout_block(costa_layout_t layout, int i, int* row_start, int* row_end,
+                           int* col_start, int* col_end, void** data, int* ld) {
+    return guarded([&] {
+        if (!layout || i < 0 || size_t(i) >= layout->e.blocks.size())
+            throw costa::engine::error(COSTA_ERR_ARG, "block index out of range");
+        const auto& b = layout->e.blocks[size_t(i)];
+        if (row_start) *row_start = b.rows.start;
+        if (row_end) *row_end = b.rows.end;
+        if (col_start) *col_start = b.cols.start;
+        if (col_end) *col_end = b.cols.end;
+        if (data) *data = b.data;
+        if (ld) *ld = b.ld;
+    });
+}
+
+int costa_hip_comm_self(int device, costa_comm_t* out) {
+    return guarded([&] {
+        if (!out) throw costa::engine::error(COSTA_ERR_ARG, "null output handle");
+        auto h = std::make_unique<costa_comm_s>();
+        h->c = costa::engine::comm_self(device);
+        *out = h.release();
+    });
+}
+
+int costa_hip_comm_unique_id(unsigned char id[128]) {
+    return guarded([&] { costa::engine::comm_unique_id(id); });
+}
+
+int costa_hip_comm_create(const unsigned char id[128], int nranks, int rank, int device,
+                          costa_comm_t* out) {
+    return guarded([&] {
+        if (!out || !id) throw costa::engine::error(COSTA_ERR_ARG, "null argument");
+        auto h = std::make_unique<costa_comm_s>();
+        h->c = costa::engine::comm_create(id, nranks, rank, device);
+        *out = h.release();
+    });
+}
+
+int costa_hip_comm_rank(costa_comm_t comm) { return comm ? costa::engine::comm_rank(comm->c) : -1; }
+int costa_hip_comm_size(costa_comm_t comm) { return comm ? costa::engine::comm_size(comm->c) : -1; }
+void costa_hip_comm_destroy(costa_comm_t comm) {
+    if (!comm) return;
+    costa::engine::comm_destroy(comm->c);
+    delete comm;
+}
+
+int costa_hip_transform(costa_layout_t A, costa_layout_t C, char trans, const void* alpha,
+                        const void* beta, costa_comm_t comm) {
+    return costa_hip_transform_batch(1, &A, &C, &trans, alpha, beta, comm);
+}
+
+int costa_hip_transform_batch(int n, const costa_layout_t* A, const costa_layout_t* C,
+                              const char* trans, const void* alpha, const void* beta,
+                              costa_comm_t comm) {
+    return guarded([&] {
+        if (!comm || !alpha || !beta) throw costa::engine::error(COSTA_ERR_ARG, "null argument");
+        auto jobs = make_jobs(n, A, C, trans, alpha, beta);
+        costa::engine::transform(jobs, comm->c);
+    });
+}
+
+int costa_hip_copy_and_transform(costa_dtype_t dtype, int n_rows, int n_cols, const void* src,
+                                 int src_stride, int src_col_major, void* dst, int dst_stride,
+                                 int dst_col_major, int transpose, int conjugate,
+                                 const void* alpha, const void* beta) {
+    return guarded([&] {
+        if (!alpha || !beta) throw costa::engine::error(COSTA_ERR_ARG, "null scalar");
+        costa::engine::copy_and_transform(dtype, n_rows, n_cols, src, src_stride, src_col_major != 0,
+                                          dst, dst_stride, dst_col_major != 0, transpose != 0,
+                                          conjugate != 0, alpha, beta);
+    });
+}
+
+int costa_hip_execute_tiles(costa_dtype_t dtype, const costa_tile_op_t* ops, int64_t n,
+                            const void* src_base, void* dst_base, const void* scalars,
+                            int n_slots, int device) {
+    return guarded([&] {
+        if (n < 0 || (n > 0 && (!ops || !scalars)))
+            throw costa::engine::error(COSTA_ERR_ARG, "null argument");
+        costa::engine::execute_tiles(dtype, ops, n, src_base, dst_base, scalars, n_slots, device);
+    });
+}
+
+int costa_hip_plan_export(int n, const costa_layout_t* A, const costa_layout_t* C,
+                          const char* trans, const void* alpha, const void* beta, int rank,
+                          int nranks, costa_plan_info_t* info, costa_tile_op_t* local_ops,
+                          costa_tile_op_t* pack_ops, costa_tile_op_t* unpack_ops,
+                          int64_t* send_counts, int64_t* send_displs, int64_t* recv_counts,
+                          int64_t* recv_displs, void* scalars) {
+    return guarded([&] {
+        if (!info || !alpha || !beta) throw costa::engine::error(COSTA_ERR_ARG, "null argument");
+        if (nranks < 1 || rank < 0 || rank >= nranks)
+            throw costa::engine::error(COSTA_ERR_ARG, "bad rank/size");
+        auto jobs = make_jobs(n, A, C, trans, alpha, beta);
+        auto p = costa::engine::make_plan(jobs, rank, nranks);
+        info->n_local = int64_t(p->local_ops.size());
+        info->n_pack = int64_t(p->pack_ops.size());
+        info->n_unpack = int64_t(p->unpack_ops.size());
+        info->send_elems = p->send_elems;
+        info->recv_elems = p->recv_elems;
+        info->local_elems = p->local_elems;
+        info->n_ranks = nranks;
+        info->n_slots = int32_t(p->slots.size());
+        auto cp = [](const auto& v, auto* dst) {
+            if (dst && !v.empty()) std::memcpy(dst, v.data(), v.size() * sizeof(v[0]));
+        };
+        cp(p->local_ops, local_ops);
+        cp(p->pack_ops, pack_ops);
+        cp(p->unpack_ops, unpack_ops);
+        cp(p->send_counts, send_counts);
+        cp(p->send_displs, send_displs);
+        cp(p->recv_counts, recv_counts);
+        cp(p->recv_displs, recv_displs);
+        if (scalars) {
+            const size_t E = dtype_size(p->dtype);
+            auto* out = static_cast<unsigned char*>(scalars);
+            for (size_t t = 0; t < p->slots.size(); ++t) {
+                std::memcpy(out + (2 * t) * E, p->slots[t].alpha.data(), E);
+                std::memcpy(out + (2 * t + 1) * E, p->slots[t].beta.data(), E);
+            }
+        }
+    });
+}
+
+int costa_hip_set_profiling(int on) {
+    costa::engine::set_profiling(on != 0);
+    return COSTA_OK;
+}
+
+int costa_hip_get_stats(costa_stats_t* out, int reset) {
+    return guarded([&] {
+        if (!out) throw costa::engine::error(COSTA_ERR_ARG, "null argument");
+        *out = costa::engine::stats();
+        if (reset) costa::engine::stats() = costa_stats_t{};
+    });
+}
+
+int costa_hip_release_caches(void) {
+    return guarded([&] { costa::engine::release_caches(); });
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- C++ API
+namespace costa {
+namespace {
+void raise(int rc) {
+    if (rc != COSTA_OK) throw hip_error(rc, g_last_error);
+}
+template <typename T>
+engine::scal scal_of(T a, T b) {
+    engine::scal s;
+    std::memcpy(s.alpha.data(), &a, sizeof(T));
+    std::memcpy(s.beta.data(), &b, sizeof(T));
+    return s;
+}
+template <typename T>
+void run(std::vector<layout_ref<T>>& from, std::vector<layout_ref<T>>& to, const char* trans,
+         const T* alpha, const T* beta, costa_comm_t comm) {
+    raise(guarded([&] {
+        if (from.size() != to.size())
+            throw engine::error(COSTA_ERR_ARG, "costa::transform: from/to sizes differ");
+        if (!comm) throw engine::error(COSTA_ERR_ARG, "costa::transform: null communicator");
+        std::vector<engine::elayout> es;
+        es.reserve(2 * from.size());
+        std::vector<engine::job> jobs(from.size());
+        for (size_t i = 0; i < from.size(); ++i) {
+            es.push_back(engine::erase(from[i].get()));
+            jobs[i].A = &es.back();
+            es.push_back(engine::erase(to[i].get()));
+            jobs[i].C = &es.back();
+            jobs[i].trans = trans ? trans[i] : 'N';
+            jobs[i].s = alpha ? scal_of(alpha[i], beta[i]) : scal_of(T{1}, T{0});
+        }
+        engine::transform(jobs, comm->c);
+    }));
+}
+}  // namespace
+
+template <typename T>
+void transform(grid_layout<T>& A, grid_layout<T>& C, costa_comm_t comm) {
+    std::vector<layout_ref<T>> f{A}, t{C};
+    run<T>(f, t, nullptr, nullptr, nullptr, comm);
+}
+
+template <typename T>
+void transform(grid_layout<T>& A, grid_layout<T>& C, char trans, T alpha, T beta,
+               costa_comm_t comm) {
+    std::vector<layout_ref<T>> f{A}, t{C};
+    run<T>(f, t, &trans, &alpha, &beta, comm);
+}
+
+template <typename T>
+void transform(std::vector<layout_ref<T>>& from, std::vector<layout_ref<T>>& to,
+               costa_comm_t comm) {
+    run<T>(from, to, nullptr, nullptr, nullptr, comm);
+}
+
+template <typename T>
+void transform(std::vector<layout_ref<T>>& from, std::vector<layout_ref<T>>& to, const char* trans,
+               const T* alpha, const T* beta, costa_comm_t comm) {
+    run<T>(from, to, trans, alpha, beta, comm);
+}
+
+#define COSTA_INSTANTIATE_TRANSFORM(T)                                                          \
+    template void transform<T>(grid_layout<T>&, grid_layout<T>&, costa_comm_t);                 \
+    template void transform<T>(grid_layout<T>&, grid_layout<T>&, char, T, T, costa_comm_t);     \
+    template void transform<T>(std::vector<layout_ref<T>>&, std::vector<layout_ref<T>>&,        \
+                               costa_comm_t);                                                   \
+    template void transform<T>(std::vector<layout_ref<T>>&, std::vector<layout_ref<T>>&,        \
+                               const char*, const T*, const T*, costa_comm_t);
+
+COSTA_INSTANTIATE_TRANSFORM(float)
+COSTA_INSTANTIATE_TRANSFORM(double)
+COSTA_INSTANTIATE_TRANSFORM(std::complex<float>)
+COSTA_INSTANTIATE_TRANSFORM(std::complex<double>)
+COSTA_INSTANTIATE_TRANSFORM(int)
+
+}  // namespace costa

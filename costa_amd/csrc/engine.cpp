@@ -1,0 +1,615 @@
+// Executor: device workspaces, plan cache, host staging, and the exchange.
+//
+// One transform = the reference's exchange_async (grid2grid/transform.cpp:46-128) re-laid
+// for one GPU per rank:
+//   main stream : [H2D of host-resident data] -> PACK kernel -> RCCL send/recv (all peers,
+//                 one group) -> UNPACK kernel -> [D2H]
+//   aux stream  : LOCAL kernel, overlapping pack + exchange (the reference overlaps its
+//                 local copy with the MPI messages in flight, transform.cpp:96-101)
+// Plans are cached by layout content (the reference re-plans every call).
+#include "engine.hpp"
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <list>
+#include <map>
+#include <mutex>
+#include <unordered_map>
+
+namespace costa {
+namespace engine {
+
+#define HIP_CHECK(x)                                                                   \
+    do {                                                                               \
+        hipError_t e_ = (x);                                                           \
+        if (e_ != hipSuccess)                                                          \
+            throw error(COSTA_ERR_HIP, std::string(#x " failed: ") + hipGetErrorString(e_)); \
+    } while (0)
+#define NCCL_CHECK(x)                                                                   \
+    do {                                                                                \
+        ncclResult_t r_ = (x);                                                          \
+        if (r_ != ncclSuccess)                                                          \
+            throw error(COSTA_ERR_NCCL, std::string(#x " failed: ") + ncclGetErrorString(r_)); \
+    } while (0)
+
+// ---------------------------------------------------------------- statistics
+namespace {
+costa_stats_t g_stats{};
+bool g_profiling = false;
+std::recursive_mutex g_mutex;  // transforms of one process are serialised (the reference's
+                               // per-type workspace singleton is not re-entrant either)
+}  // namespace
+costa_stats_t& stats() { return g_stats; }
+bool profiling() { return g_profiling; }
+void set_profiling(bool on) { g_profiling = on; }
+
+// ---------------------------------------------------------------- device memory
+struct dbuf {
+    void* p = nullptr;
+    size_t n = 0;
+    dbuf() = default;
+    dbuf(const dbuf&) = delete;
+    dbuf& operator=(const dbuf&) = delete;
+    ~dbuf() {
+        if (p) (void)hipFree(p);
+    }
+    void reserve(size_t bytes) {
+        if (bytes <= n) return;
+        if (p) HIP_CHECK(hipFree(p));
+        p = nullptr;
+        n = 0;
+        // round up to 2 MiB so growing workspaces do not reallocate every call
+        size_t want = (bytes + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
+        HIP_CHECK(hipMalloc(&p, want));
+        n = want;
+    }
+    template <typename X>
+    void upload(const std::vector<X>& v, hipStream_t s) {
+        if (v.empty()) return;
+        reserve(v.size() * sizeof(X));
+        HIP_CHECK(hipMemcpyAsync(p, v.data(), v.size() * sizeof(X), hipMemcpyHostToDevice, s));
+    }
+};
+
+// ---------------------------------------------------------------- per-device context
+struct device_ctx {
+    int device = 0;
+    hipStream_t main = nullptr, aux = nullptr;
+    hipEvent_t ev_ready = nullptr, ev_local = nullptr;
+    hipEvent_t t[8] = {};
+    dbuf send, recv;
+    explicit device_ctx(int dev) : device(dev) {
+        HIP_CHECK(hipSetDevice(dev));
+        // blocking streams: they order after work on the legacy default stream
+        HIP_CHECK(hipStreamCreate(&main));
+        HIP_CHECK(hipStreamCreate(&aux));
+        HIP_CHECK(hipEventCreateWithFlags(&ev_ready, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&ev_local, hipEventDisableTiming));
+        for (auto& e : t) HIP_CHECK(hipEventCreate(&e));
+    }
+    ~device_ctx() {
+        (void)hipSetDevice(device);
+        for (auto& e : t) (void)hipEventDestroy(e);
+        (void)hipEventDestroy(ev_ready);
+        (void)hipEventDestroy(ev_local);
+        (void)hipStreamDestroy(main);
+        (void)hipStreamDestroy(aux);
+    }
+};
+
+namespace {
+std::map<int, std::unique_ptr<device_ctx>>& ctx_map() {
+    static std::map<int, std::unique_ptr<device_ctx>> m;
+    return m;
+}
+device_ctx& ctx(int device) {
+    auto& m = ctx_map();
+    auto it = m.find(device);
+    if (it == m.end()) it = m.emplace(device, std::make_unique<device_ctx>(device)).first;
+    HIP_CHECK(hipSetDevice(device));
+    return *it->second;
+}
+}  // namespace
+
+// ---------------------------------------------------------------- communicator
+struct comm {
+    int rank = 0, size = 1, device = 0;
+    ncclComm_t nccl = nullptr;
+    ~comm() {
+        if (nccl) (void)ncclCommDestroy(nccl);
+    }
+};
+
+comm* comm_self(int device) {
+    int n = 0;
+    HIP_CHECK(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) throw error(COSTA_ERR_ARG, "costa: device index out of range");
+    auto* c = new comm;
+    c->device = device;
+    return c;
+}
+
+comm* comm_create(const unsigned char* id, int nranks, int rank, int device) {
+    if (nranks < 1 || rank < 0 || rank >= nranks) throw error(COSTA_ERR_ARG, "costa: bad rank/size");
+    auto* c = comm_self(device);
+    c->rank = rank;
+    c->size = nranks;
+    if (nranks > 1) {
+        HIP_CHECK(hipSetDevice(device));
+        ncclUniqueId uid;
+        std::memcpy(uid.internal, id, NCCL_UNIQUE_ID_BYTES);
+        ncclResult_t r = ncclCommInitRank(&c->nccl, nranks, uid, rank);
+        if (r != ncclSuccess) {
+            delete c;
+            throw error(COSTA_ERR_NCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+        }
+    }
+    return c;
+}
+
+int comm_rank(const comm* c) { return c->rank; }
+int comm_size(const comm* c) { return c->size; }
+void comm_destroy(comm* c) { delete c; }
+
+void comm_unique_id(unsigned char* out) {
+    ncclUniqueId uid;
+    NCCL_CHECK(ncclGetUniqueId(&uid));
+    std::memcpy(out, uid.internal, NCCL_UNIQUE_ID_BYTES);
+}
+
+// ---------------------------------------------------------------- work lists
+void build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops,
+                std::vector<uint64_t>& work) {
+    int bf = 0, bs = 0;
+    tile_shape(dtype, &bf, &bs);
+    work.clear();
+    for (size_t i = 0; i < ops.size(); ++i) {
+        const auto& op = ops[i];
+        if (op.nf <= 0 || op.ns <= 0) continue;
+        const uint64_t n = uint64_t((op.nf + bf - 1) / bf) * uint64_t((op.ns + bs - 1) / bs);
+        if (n > 0xFFFFFFFFull) throw error(COSTA_ERR_ARG, "costa: tile too large");
+        for (uint64_t k = 0; k < n; ++k) work.push_back((uint64_t(i) << 32) | k);
+    }
+}
+
+// ---------------------------------------------------------------- residency / staging
+namespace {
+
+// Byte ranges of host memory touched by a layout's blocks, merged; used to stage
+// host-resident matrices through HBM (the path starts and ends in host memory).
+struct hrange {
+    uintptr_t lo, hi;
+    size_t dev_off;
+};
+
+size_t block_extent_bytes(const eblock& b, char ordering, size_t E) {
+    const int64_t nr = b.rows.length(), nc = b.cols.length();
+    if (nr == 0 || nc == 0) return 0;
+    const int64_t fast = ordering == 'R' ? nc : nr, slow = ordering == 'R' ? nr : nc;
+    return size_t((slow - 1) * int64_t(b.ld) + fast) * E;
+}
+
+bool is_device_ptr(const void* p) {
+    hipPointerAttribute_t a;
+    hipError_t e = hipPointerGetAttributes(&a, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice;
+}
+
+// true if every block is in device memory; false if every block is host memory
+bool layout_on_device(const elayout& L) {
+    if (L.blocks.empty()) return true;
+    bool first = is_device_ptr(L.blocks.front().data);
+    // check block pointers that leave the current device allocation
+    uintptr_t lo = 0, hi = 0;
+    for (const auto& b : L.blocks) {
+        uintptr_t p = reinterpret_cast<uintptr_t>(b.data);
+        if (first && p >= lo && p < hi) continue;
+        bool d = is_device_ptr(b.data);
+        if (d != first)
+            throw error(COSTA_ERR_ARG, "costa: a layout mixes host and device blocks");
+        if (d) {
+            hipDeviceptr_t base = nullptr;
+            size_t sz = 0;
+            if (hipMemGetAddressRange(&base, &sz, const_cast<char*>(b.data)) == hipSuccess) {
+                lo = reinterpret_cast<uintptr_t>(base);
+                hi = lo + sz;
+            } else {
+                (void)hipGetLastError();
+            }
+        }
+    }
+    return first;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- plan cache
+namespace {
+
+struct hasher {
+    uint64_t h = 0x9E3779B97F4A7C15ull;
+    void mix(uint64_t v) {
+        v ^= v >> 33;
+        v *= 0xff51afd7ed558ccdull;
+        v ^= v >> 33;
+        h = (h ^ v) * 0xc4ceb9fe1a85ec53ull + 0x165667b19e3779f9ull;
+        h ^= h >> 29;
+    }
+    void mix_vec(const std::vector<int>& v) {
+        mix(v.size());
+        for (int x : v) mix(uint64_t(uint32_t(x)));
+    }
+    void mix_layout(const elayout& L) {
+        mix(uint64_t(L.dtype));
+        mix(uint64_t(uint8_t(L.ordering)));
+        mix(uint64_t(L.n_ranks));
+        mix_vec(L.rows_split);
+        mix_vec(L.cols_split);
+        mix_vec(L.owners);
+        mix(L.blocks.size());
+        for (const auto& b : L.blocks) {
+            mix(uint64_t(uint32_t(b.rows.start)) | (uint64_t(uint32_t(b.rows.end)) << 32));
+            mix(uint64_t(uint32_t(b.cols.start)) | (uint64_t(uint32_t(b.cols.end)) << 32));
+            mix(reinterpret_cast<uintptr_t>(b.data));
+            mix(uint64_t(uint32_t(b.ld)));
+        }
+    }
+};
+
+struct cached_plan {
+    std::unique_ptr<plan> p;
+    int device = 0;
+    // staging of host-resident layouts (empty when everything is in HBM)
+    bool staged = false;
+    std::vector<hrange> a_ranges, c_ranges;  // c_ranges also copied back
+    dbuf stage;
+    // device copies of the op lists and work lists
+    dbuf d_local, d_pack, d_unpack, w_local, w_pack, w_unpack, d_scal;
+    int64_t n_local = 0, n_pack = 0, n_unpack = 0;
+    std::vector<unsigned char> scal_host;
+};
+
+constexpr size_t kMaxPlans = 16;
+std::list<std::pair<uint64_t, std::unique_ptr<cached_plan>>> g_plans;  // MRU first
+
+// remap every block pointer of `L` that lies in a staged range to its device address
+elayout remap(const elayout& L, const std::vector<hrange>& ranges, char* dev) {
+    elayout out = L;
+    for (auto& b : out.blocks) {
+        uintptr_t p = reinterpret_cast<uintptr_t>(b.data);
+        auto it = std::upper_bound(ranges.begin(), ranges.end(), p,
+                                   [](uintptr_t v, const hrange& r) { return v < r.lo; });
+        if (it == ranges.begin()) throw error(COSTA_ERR_INTERNAL, "costa: staging map miss");
+        --it;
+        b.data = dev + it->dev_off + (p - it->lo);
+    }
+    return out;
+}
+
+std::vector<hrange> collect_ranges(const std::vector<const elayout*>& Ls) {
+    std::vector<hrange> r;
+    for (const elayout* L : Ls) {
+        const size_t E = dtype_size(L->dtype);
+        for (const auto& b : L->blocks) {
+            size_t ext = block_extent_bytes(b, L->ordering, E);
+            if (!ext) continue;
+            uintptr_t lo = reinterpret_cast<uintptr_t>(b.data);
+            r.push_back({lo, lo + ext, 0});
+        }
+    }
+    std::sort(r.begin(), r.end(), [](const hrange& x, const hrange& y) { return x.lo < y.lo; });
+    std::vector<hrange> m;
+    for (const auto& x : r) {
+        if (!m.empty() && x.lo <= m.back().hi)
+            m.back().hi = std::max(m.back().hi, x.hi);
+        else
+            m.push_back(x);
+    }
+    return m;
+}
+
+cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
+    hasher h;
+    h.mix(uint64_t(c->rank));
+    h.mix(uint64_t(c->size));
+    h.mix(uint64_t(c->device));
+    h.mix(jobs.size());
+    for (const auto& j : jobs) {
+        h.mix_layout(*j.A);
+        h.mix_layout(*j.C);
+        h.mix(uint64_t(uint8_t(std::toupper(static_cast<unsigned char>(j.trans)))));
+        // the scale kinds (not the values) are baked into the ops
+        for (bool cm : {true, false})
+            h.mix(scale_kind(j.A->dtype, j.s, cm, std::toupper(j.trans) == 'C'));
+    }
+    for (auto it = g_plans.begin(); it != g_plans.end(); ++it) {
+        if (it->first == h.h) {
+            g_plans.splice(g_plans.begin(), g_plans, it);
+            g_stats.plan_hits++;
+            return g_plans.front().second.get();
+        }
+    }
+    g_stats.plan_misses++;
+
+    auto cp = std::make_unique<cached_plan>();
+    cp->device = c->device;
+    // residency: all device, or stage the host-resident layouts
+    bool all_dev = true;
+    std::vector<const elayout*> host_layouts;
+    std::vector<bool> on_dev;
+    for (const auto& j : jobs)
+        for (const elayout* L : {j.A, j.C}) {
+            bool d = layout_on_device(*L);
+            on_dev.push_back(d);
+            all_dev = all_dev && d;
+        }
+    std::vector<elayout> remapped;
+    std::vector<job> pj = jobs;
+    if (!all_dev) {
+        cp->staged = true;
+        std::vector<const elayout*> As, Cs;
+        size_t k = 0;
+        for (const auto& j : jobs) {
+            if (!on_dev[k++]) As.push_back(j.A);
+            if (!on_dev[k++]) Cs.push_back(j.C);
+        }
+        std::vector<const elayout*> all = As;
+        all.insert(all.end(), Cs.begin(), Cs.end());
+        auto ranges = collect_ranges(all);
+        size_t off = 0;
+        for (auto& r : ranges) {
+            r.dev_off = off;
+            off += ((r.hi - r.lo) + 255) & ~size_t(255);
+        }
+        cp->stage.reserve(std::max<size_t>(off, 256));
+        auto in_set = [](const std::vector<const elayout*>& v, const elayout* L) {
+            return std::find(v.begin(), v.end(), L) != v.end();
+        };
+        // which merged ranges hold A data (H2D) and C data (H2D + D2H)
+        for (const auto& r : ranges) {
+            bool a = false, cc = false;
+            for (const elayout* L : all) {
+                const size_t E = dtype_size(L->dtype);
+                for (const auto& b : L->blocks) {
+                    uintptr_t lo = reinterpret_cast<uintptr_t>(b.data);
+                    if (lo >= r.lo && lo < r.hi && block_extent_bytes(b, L->ordering, E)) {
+                        if (in_set(As, L)) a = true;
+                        if (in_set(Cs, L)) cc = true;
+                    }
+                }
+                if (a && cc) break;
+            }
+            if (a || cc) cp->a_ranges.push_back(r);  // everything staged is uploaded
+            if (cc) cp->c_ranges.push_back(r);
+        }
+        remapped.reserve(jobs.size() * 2);
+        k = 0;
+        for (auto& j : pj) {
+            if (!on_dev[k++]) {
+                remapped.push_back(remap(*j.A, ranges, static_cast<char*>(cp->stage.p)));
+                j.A = &remapped.back();
+            }
+            if (!on_dev[k++]) {
+                remapped.push_back(remap(*j.C, ranges, static_cast<char*>(cp->stage.p)));
+                j.C = &remapped.back();
+            }
+        }
+    }
+    cp->p = make_plan(pj, c->rank, c->size);
+    const plan& p = *cp->p;
+    std::vector<uint64_t> w;
+    cp->d_local.upload(p.local_ops, dc.main);
+    build_work(p.dtype, p.local_ops, w);
+    cp->n_local = int64_t(w.size());
+    cp->w_local.upload(w, dc.main);
+    cp->d_pack.upload(p.pack_ops, dc.main);
+    build_work(p.dtype, p.pack_ops, w);
+    cp->n_pack = int64_t(w.size());
+    cp->w_pack.upload(w, dc.main);
+    cp->d_unpack.upload(p.unpack_ops, dc.main);
+    build_work(p.dtype, p.unpack_ops, w);
+    cp->n_unpack = int64_t(w.size());
+    cp->w_unpack.upload(w, dc.main);
+    HIP_CHECK(hipStreamSynchronize(dc.main));  // host vectors above are temporaries
+
+    g_plans.emplace_front(h.h, std::move(cp));
+    while (g_plans.size() > kMaxPlans) g_plans.pop_back();
+    return g_plans.front().second.get();
+}
+
+void upload_scalars(cached_plan& cp, const std::vector<job>& jobs, hipStream_t s) {
+    const size_t E = dtype_size(cp.p->dtype);
+    std::vector<unsigned char> host(jobs.size() * 2 * E);
+    for (size_t t = 0; t < jobs.size(); ++t) {
+        std::memcpy(&host[(2 * t) * E], jobs[t].s.alpha.data(), E);
+        std::memcpy(&host[(2 * t + 1) * E], jobs[t].s.beta.data(), E);
+    }
+    if (host != cp.scal_host || !cp.d_scal.p) {
+        cp.d_scal.reserve(host.size());
+        HIP_CHECK(hipMemcpy(cp.d_scal.p, host.data(), host.size(), hipMemcpyHostToDevice));
+        cp.scal_host = host;
+    }
+}
+
+float elapsed(hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&ms, a, b));
+    return ms;
+}
+
+}  // namespace
+
+void release_caches() {
+    std::lock_guard<std::recursive_mutex> lk(g_mutex);
+    g_plans.clear();
+    ctx_map().clear();
+}
+
+// ---------------------------------------------------------------- transform
+void transform(const std::vector<job>& jobs, comm* c) {
+    std::lock_guard<std::recursive_mutex> lk(g_mutex);
+    if (!c) throw error(COSTA_ERR_ARG, "costa: null communicator");
+    device_ctx& dc = ctx(c->device);
+    cached_plan& cp = *get_plan(jobs, c, dc);
+    const plan& p = *cp.p;
+    const size_t E = dtype_size(p.dtype);
+    upload_scalars(cp, jobs, dc.main);
+    const bool prof = g_profiling;
+
+    // H2D of host-resident data
+    if (cp.staged) {
+        if (prof) HIP_CHECK(hipEventRecord(dc.t[6], dc.main));
+        for (const auto& r : cp.a_ranges)
+            HIP_CHECK(hipMemcpyAsync(static_cast<char*>(cp.stage.p) + r.dev_off,
+                                     reinterpret_cast<void*>(r.lo), r.hi - r.lo,
+                                     hipMemcpyHostToDevice, dc.main));
+        if (prof) HIP_CHECK(hipEventRecord(dc.t[7], dc.main));
+    }
+    HIP_CHECK(hipEventRecord(dc.ev_ready, dc.main));
+
+    const bool exchange = c->size > 1 && (p.send_elems > 0 || p.recv_elems > 0);
+    // LOCAL on the aux stream (overlaps pack + exchange)
+    const bool local_on_aux = exchange;
+    hipStream_t ls = local_on_aux ? dc.aux : dc.main;
+    if (local_on_aux) HIP_CHECK(hipStreamWaitEvent(dc.aux, dc.ev_ready, 0));
+    if (cp.n_local) {
+        if (prof) HIP_CHECK(hipEventRecord(dc.t[0], ls));
+        launch_tiles(p.dtype,
+                     {static_cast<const costa_tile_op_t*>(cp.d_local.p),
+                      static_cast<const uint64_t*>(cp.w_local.p), cp.n_local, nullptr, nullptr,
+                      cp.d_scal.p},
+                     ls);
+        if (prof) HIP_CHECK(hipEventRecord(dc.t[1], ls));
+    }
+    if (local_on_aux) HIP_CHECK(hipEventRecord(dc.ev_local, dc.aux));
+
+    if (exchange) {
+        dc.send.reserve(size_t(p.send_elems) * E + 256);
+        dc.recv.reserve(size_t(p.recv_elems) * E + 256);
+        char* sb = static_cast<char*>(dc.send.p);
+        char* rb = static_cast<char*>(dc.recv.p);
+        if (cp.n_pack) {
+            if (prof) HIP_CHECK(hipEventRecord(dc.t[2], dc.main));
+            launch_tiles(p.dtype,
+                         {static_cast<const costa_tile_op_t*>(cp.d_pack.p),
+                          static_cast<const uint64_t*>(cp.w_pack.p), cp.n_pack, nullptr, sb,
+                          cp.d_scal.p},
+                         dc.main);
+            if (prof) HIP_CHECK(hipEventRecord(dc.t[3], dc.main));
+        }
+        NCCL_CHECK(ncclGroupStart());
+        for (int r = 0; r < c->size; ++r) {
+            if (p.send_counts[size_t(r)] > 0)
+                NCCL_CHECK(ncclSend(sb + size_t(p.send_displs[size_t(r)]) * E,
+                                    size_t(p.send_counts[size_t(r)]) * E, ncclUint8, r, c->nccl,
+                                    dc.main));
+            if (p.recv_counts[size_t(r)] > 0)
+                NCCL_CHECK(ncclRecv(rb + size_t(p.recv_displs[size_t(r)]) * E,
+                                    size_t(p.recv_counts[size_t(r)]) * E, ncclUint8, r, c->nccl,
+                                    dc.main));
+        }
+        NCCL_CHECK(ncclGroupEnd());
+        if (prof) HIP_CHECK(hipEventRecord(dc.t[4], dc.main));
+        if (cp.n_unpack)
+            launch_tiles(p.dtype,
+                         {static_cast<const costa_tile_op_t*>(cp.d_unpack.p),
+                          static_cast<const uint64_t*>(cp.w_unpack.p), cp.n_unpack, rb, nullptr,
+                          cp.d_scal.p},
+                         dc.main);
+        if (prof) HIP_CHECK(hipEventRecord(dc.t[5], dc.main));
+        HIP_CHECK(hipStreamWaitEvent(dc.main, dc.ev_local, 0));
+    }
+
+    // D2H of the target data
+    if (cp.staged) {
+        for (const auto& r : cp.c_ranges)
+            HIP_CHECK(hipMemcpyAsync(reinterpret_cast<void*>(r.lo),
+                                     static_cast<char*>(cp.stage.p) + r.dev_off, r.hi - r.lo,
+                                     hipMemcpyDeviceToHost, dc.main));
+    }
+    HIP_CHECK(hipStreamSynchronize(dc.main));
+    if (local_on_aux) HIP_CHECK(hipStreamSynchronize(dc.aux));
+
+    g_stats.transforms++;
+    if (cp.n_local) {
+        g_stats.local_launches++;
+        g_stats.local_bytes += p.local_bytes;
+    }
+    if (exchange && cp.n_pack) {
+        g_stats.pack_launches++;
+        g_stats.pack_bytes += p.pack_bytes;
+    }
+    if (exchange && cp.n_unpack) {
+        g_stats.unpack_launches++;
+        g_stats.unpack_bytes += p.unpack_bytes;
+    }
+    if (prof) {
+        if (cp.n_local) g_stats.local_ms += elapsed(dc.t[0], dc.t[1]);
+        if (exchange) {
+            if (cp.n_pack) g_stats.pack_ms += elapsed(dc.t[2], dc.t[3]);
+            g_stats.exchange_ms += elapsed(cp.n_pack ? dc.t[3] : dc.ev_ready, dc.t[4]);
+            g_stats.unpack_ms += elapsed(dc.t[4], dc.t[5]);
+        }
+        if (cp.staged) g_stats.h2d_ms += elapsed(dc.t[6], dc.t[7]);
+    }
+}
+
+// ---------------------------------------------------------------- direct tile calls
+void execute_tiles(costa_dtype_t dtype, const costa_tile_op_t* ops, int64_t n,
+                   const void* src_base, void* dst_base, const void* scalars, int n_slots,
+                   int device) {
+    std::lock_guard<std::recursive_mutex> lk(g_mutex);
+    device_ctx& dc = ctx(device);
+    std::vector<costa_tile_op_t> v(ops, ops + n);
+    for (const auto& op : v)
+        if ((op.flags >> COSTA_SLOT_SHIFT) >= uint32_t(std::max(n_slots, 0)))
+            throw error(COSTA_ERR_ARG, "costa_hip_execute_tiles: scalar slot out of range");
+    std::vector<uint64_t> w;
+    build_work(dtype, v, w);
+    dbuf d_ops, d_work, d_scal;
+    d_ops.upload(v, dc.main);
+    d_work.upload(w, dc.main);
+    const size_t E = dtype_size(dtype);
+    std::vector<unsigned char> sc(static_cast<const unsigned char*>(scalars),
+                                  static_cast<const unsigned char*>(scalars) + size_t(n_slots) * 2 * E);
+    d_scal.upload(sc, dc.main);
+    launch_tiles(dtype,
+                 {static_cast<const costa_tile_op_t*>(d_ops.p), static_cast<const uint64_t*>(d_work.p),
+                  int64_t(w.size()), static_cast<const char*>(src_base), static_cast<char*>(dst_base),
+                  d_scal.p},
+                 dc.main);
+    HIP_CHECK(hipStreamSynchronize(dc.main));
+}
+
+void copy_and_transform(costa_dtype_t dtype, int n_rows, int n_cols, const void* src,
+                        int src_stride, bool src_cm, void* dst, int dst_stride, bool dst_cm,
+                        bool trans, bool conj, const void* alpha, const void* beta) {
+    if (n_rows < 0 || n_cols < 0 || src_stride < 0 || dst_stride < 0)
+        throw error(COSTA_ERR_ARG, "costa_hip_copy_and_transform: negative size or stride");
+    if (size_t(n_rows) * size_t(n_cols) == 0) return;  // memory_utils.hpp:72-74
+    const size_t E = dtype_size(dtype);
+    scal s;
+    std::memcpy(s.alpha.data(), alpha, E);
+    std::memcpy(s.beta.data(), beta, E);
+    const bool cj = conj && dtype_is_complex(dtype);
+    const bool wt = (trans && src_cm == dst_cm) || (!trans && src_cm != dst_cm);
+    costa_tile_op_t op = make_tile_op(n_rows, n_cols, reinterpret_cast<uintptr_t>(src), src_stride,
+                                      src_cm, reinterpret_cast<uintptr_t>(dst), dst_stride, dst_cm,
+                                      trans, cj, scale_kind(dtype, s, !wt, cj), 0, E);
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    std::vector<unsigned char> sc(2 * E);
+    std::memcpy(sc.data(), alpha, E);
+    std::memcpy(sc.data() + E, beta, E);
+    execute_tiles(dtype, &op, 1, nullptr, nullptr, sc.data(), 1, dev);
+}
+
+}  // namespace engine
+}  // namespace costa

@@ -1,0 +1,133 @@
+// Internal engine interface: type-erased layouts, the tile planner and the executor.
+#pragma once
+
+#include <costa/layout.hpp>
+#include <costa_hip.h>
+
+#include <array>
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace costa {
+namespace engine {
+
+size_t dtype_size(costa_dtype_t t);
+bool dtype_is_complex(costa_dtype_t t);
+
+// One local block, element-type erased.  Intervals are in the layout's own (untransposed)
+// global coordinates; `data` points at its first element.
+struct eblock {
+    interval rows, cols;
+    char* data = nullptr;
+    int ld = 0;
+};
+
+// A grid_layout<T> with the element type erased (owners row-major, like the reference's
+// ranks[i][j]).  Plans are built from these.
+struct elayout {
+    costa_dtype_t dtype = COSTA_DOUBLE;
+    std::vector<int> rows_split, cols_split;
+    std::vector<int> owners;
+    int n_ranks = 1;
+    char ordering = 'C';
+    std::vector<eblock> blocks;
+
+    int nbr() const { return int(rows_split.size()) - 1; }
+    int nbc() const { return int(cols_split.size()) - 1; }
+};
+
+template <typename T>
+costa_dtype_t dtype_of();
+
+template <typename T>
+elayout erase(const grid_layout<T>& L);
+
+// scalars (alpha, beta) of one layout pair, stored as raw bytes of the dtype
+struct scal {
+    std::array<unsigned char, 16> alpha{};
+    std::array<unsigned char, 16> beta{};
+};
+
+// one (A -> C) pair of a transform
+struct job {
+    const elayout* A = nullptr;
+    const elayout* C = nullptr;
+    char trans = 'N';
+    scal s;
+};
+
+// The three tile-op lists of one rank plus the exchange geometry.  Addresses of pack
+// destinations and unpack sources are byte offsets into the send / receive buffers.
+struct plan {
+    costa_dtype_t dtype = COSTA_DOUBLE;
+    int rank = 0, n_ranks = 1;
+    std::vector<costa_tile_op_t> local_ops, pack_ops, unpack_ops;
+    std::vector<int64_t> send_counts, send_displs, recv_counts, recv_displs;  // elements
+    int64_t send_elems = 0, recv_elems = 0, local_elems = 0;
+    std::vector<scal> slots;
+    // algorithmic HBM bytes of each list (read + write (+ read of C when beta != 0))
+    int64_t local_bytes = 0, pack_bytes = 0, unpack_bytes = 0;
+};
+
+// Build the plan of `rank` (of `n_ranks`) for a batch of jobs (host only).
+std::unique_ptr<plan> make_plan(const std::vector<job>& jobs, int rank, int n_ranks);
+
+// normalise one copy_and_transform call (memory_utils.hpp:339-412) into a tile op
+costa_tile_op_t make_tile_op(int n_rows, int n_cols, uint64_t src, int src_stride, bool src_cm,
+                             uint64_t dst, int dst_stride, bool dst_cm, bool transpose, bool conj,
+                             uint32_t scale_kind, uint32_t slot, size_t elem);
+
+// scale kind of (alpha, beta) for `dtype` with the reference's branch rules
+uint32_t scale_kind(costa_dtype_t dtype, const scal& s, bool copy_mode, bool conj);
+
+// ---- executor (engine.cpp / tile_kernels.hip) ----
+struct comm;
+struct comm* comm_self(int device);
+struct comm* comm_create(const unsigned char* id, int nranks, int rank, int device);
+void comm_unique_id(unsigned char* out);
+int comm_rank(const struct comm* c);
+int comm_size(const struct comm* c);
+void comm_destroy(struct comm* c);
+
+void transform(const std::vector<job>& jobs, struct comm* c);
+
+void copy_and_transform(costa_dtype_t dtype, int n_rows, int n_cols, const void* src,
+                        int src_stride, bool src_cm, void* dst, int dst_stride, bool dst_cm,
+                        bool trans, bool conj, const void* alpha, const void* beta);
+
+void execute_tiles(costa_dtype_t dtype, const costa_tile_op_t* ops, int64_t n,
+                   const void* src_base, void* dst_base, const void* scalars, int n_slots,
+                   int device);
+
+// kernel launcher (tile_kernels.hip); `work` and `ops` are device arrays
+struct launch_args {
+    const costa_tile_op_t* ops;
+    const uint64_t* work;   // per workgroup: (op index << 32) | sub-tile index
+    int64_t n_work;
+    const char* src_base;
+    char* dst_base;
+    const void* scalars;    // device: n_slots x (alpha, beta) of the dtype
+};
+void launch_tiles(costa_dtype_t dtype, const launch_args& a, void* stream /* hipStream_t */);
+// sub-tile shape (elements along src fast dim, along src slow dim) used by the kernels
+void tile_shape(costa_dtype_t dtype, int* bf, int* bs);
+// build the per-workgroup work list of an op list
+void build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops,
+                std::vector<uint64_t>& work);
+
+// errors
+struct error : std::runtime_error {
+    int code;
+    error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+// statistics
+costa_stats_t& stats();
+bool profiling();
+void set_profiling(bool on);
+void release_caches();
+
+}  // namespace engine
+}  // namespace costa

@@ -1,0 +1,255 @@
+// TEST INFRASTRUCTURE ONLY — drives the REFERENCE COSTA library (compiled from
+// /root/reference sources into oracle/_ref/ by oracle/Makefile) to produce golden vectors.
+// Run by tests/golden/make_fixtures.py under `mpiexec -n P`; never shipped, never run on
+// the GPU box.
+//
+//   ref_harness kat <outdir>             the 4 copy_and_transform known-answer tests of
+//                                        tests/unit/test_utils.cpp, inputs + outputs dumped
+//   ref_harness case <spec> <outdir>     one transform case (spec written by
+//                                        make_fixtures.py); every rank dumps its C buffer
+#include <costa/layout.hpp>
+#include <costa/grid2grid/transform.hpp>
+#include <costa/grid2grid/transformer.hpp>
+#include <costa/grid2grid/memory_utils.hpp>
+#include <costa/grid2grid/workspace.hpp>
+#include <mpi.h>
+
+#include <complex>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <iostream>
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace {
+
+uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+// the synthetic-data generator shared with tests/golden/gen.py
+uint64_t draw(uint64_t seed, int rank, uint64_t k) {
+    return splitmix64(seed ^ (uint64_t(rank) << 48) ^ k);
+}
+double unif(uint64_t z) { return double(z >> 11) * 0x1.0p-52 - 1.0; }
+
+template <typename T> T gen(uint64_t seed, int rank, uint64_t k);
+template <> double gen<double>(uint64_t s, int r, uint64_t k) { return unif(draw(s, r, k)); }
+template <> float gen<float>(uint64_t s, int r, uint64_t k) { return float(unif(draw(s, r, k))); }
+template <> int gen<int>(uint64_t s, int r, uint64_t k) {
+    return int((draw(s, r, k) >> 33) % 2001) - 1000;
+}
+template <> std::complex<double> gen<std::complex<double>>(uint64_t s, int r, uint64_t k) {
+    return {unif(draw(s, r, 2 * k)), unif(draw(s, r, 2 * k + 1))};
+}
+template <> std::complex<float> gen<std::complex<float>>(uint64_t s, int r, uint64_t k) {
+    return {float(unif(draw(s, r, 2 * k))), float(unif(draw(s, r, 2 * k + 1)))};
+}
+
+template <typename T>
+void dump(const std::string& path, const std::vector<T>& v) {
+    std::ofstream f(path, std::ios::binary);
+    f.write(reinterpret_cast<const char*>(v.data()), std::streamsize(v.size() * sizeof(T)));
+}
+
+struct lspec {
+    std::string kind;
+    // bc
+    int m, n, mb, nb, ia, ja, subm, subn, pm, pn, rsrc, csrc, lld;
+    char order, ord;
+    long long buf_elems;
+    // custom
+    int nbr, nbc;
+    std::vector<int> rs, cs, owners;
+    std::vector<long long> bufs;                      // per rank
+    std::vector<std::vector<long long>> blocks;       // per rank: row col off ld ...
+};
+
+lspec read_layout(std::istream& in, int P) {
+    lspec L;
+    std::string tok;
+    in >> tok >> L.kind;  // "kind" <bc|custom>
+    if (L.kind == "bc") {
+        in >> L.m >> L.n >> L.mb >> L.nb >> L.ia >> L.ja >> L.subm >> L.subn >> L.pm >> L.pn >>
+            L.order >> L.rsrc >> L.csrc >> L.ord >> L.lld >> L.buf_elems;
+    } else {
+        in >> L.nbr >> L.nbc;
+        L.rs.resize(size_t(L.nbr + 1));
+        L.cs.resize(size_t(L.nbc + 1));
+        L.owners.resize(size_t(L.nbr) * size_t(L.nbc));
+        for (auto& x : L.rs) in >> x;
+        for (auto& x : L.cs) in >> x;
+        for (auto& x : L.owners) in >> x;
+        in >> L.ord;
+        L.bufs.resize(size_t(P));
+        for (auto& x : L.bufs) in >> x;
+        L.blocks.resize(size_t(P));
+        for (int r = 0; r < P; ++r) {
+            int nb;
+            in >> nb;
+            L.blocks[size_t(r)].resize(size_t(nb) * 4);
+            for (auto& x : L.blocks[size_t(r)]) in >> x;
+        }
+    }
+    return L;
+}
+
+template <typename T>
+costa::grid_layout<T> build(const lspec& L, std::vector<T>& buf, int rank) {
+    if (L.kind == "bc") {
+        return costa::block_cyclic_layout<T>(L.m, L.n, L.mb, L.nb, L.ia, L.ja, L.subm, L.subn, L.pm,
+                                             L.pn, L.order, L.rsrc, L.csrc, buf.data(), L.lld,
+                                             L.ord, rank);
+    }
+    const auto& bl = L.blocks[size_t(rank)];
+    std::vector<costa::block_t> loc;
+    for (size_t k = 0; k + 3 < bl.size(); k += 4) {
+        costa::block_t b;
+        b.row = int(bl[k]);
+        b.col = int(bl[k + 1]);
+        b.data = buf.data() + bl[k + 2];
+        b.ld = int(bl[k + 3]);
+        loc.push_back(b);
+    }
+    return costa::custom_layout<T>(L.nbr, L.nbc, L.rs.data(), L.cs.data(), L.owners.data(),
+                                   int(loc.size()), loc.data(), L.ord);
+}
+
+long long buf_size(const lspec& L, int rank) {
+    long long n = L.kind == "bc" ? L.buf_elems : L.bufs[size_t(rank)];
+    return n > 0 ? n : 1;
+}
+
+template <typename T>
+int run_case(std::istream& in, const std::string& out, int rank, int P) {
+    int npairs;
+    std::string tok;
+    in >> tok >> npairs;
+    const size_t np = size_t(npairs);
+    std::vector<char> trans(np);
+    std::vector<T> alpha(np), beta(np);
+    std::vector<int> noscale(np);
+    std::vector<uint64_t> seedA(np), seedC(np);
+    std::vector<lspec> A, C;
+    for (int p = 0; p < npairs; ++p) {
+        double ar, ai, br, bi;
+        in >> tok >> trans[size_t(p)] >> tok >> ar >> ai >> tok >> br >> bi >> tok >>
+            noscale[size_t(p)] >> tok >> seedA[size_t(p)] >> tok >> seedC[size_t(p)];
+        if constexpr (std::is_same<T, std::complex<double>>::value ||
+                      std::is_same<T, std::complex<float>>::value) {
+            alpha[size_t(p)] = T(ar, ai);
+            beta[size_t(p)] = T(br, bi);
+        } else {
+            alpha[size_t(p)] = T(ar);
+            beta[size_t(p)] = T(br);
+        }
+        A.push_back(read_layout(in, P));
+        C.push_back(read_layout(in, P));
+    }
+    std::vector<std::vector<T>> abuf(np), cbuf(np);
+    std::vector<costa::grid_layout<T>> la, lc;
+    la.reserve(np);
+    lc.reserve(np);
+    for (int p = 0; p < npairs; ++p) {
+        auto& a = abuf[size_t(p)];
+        auto& c = cbuf[size_t(p)];
+        a.resize(size_t(buf_size(A[size_t(p)], rank)));
+        c.resize(size_t(buf_size(C[size_t(p)], rank)));
+        for (size_t k = 0; k < a.size(); ++k) a[k] = gen<T>(seedA[size_t(p)], rank, k);
+        for (size_t k = 0; k < c.size(); ++k) c[k] = gen<T>(seedC[size_t(p)], rank, k);
+        la.push_back(build<T>(A[size_t(p)], a, rank));
+        lc.push_back(build<T>(C[size_t(p)], c, rank));
+    }
+    if (npairs == 1) {
+        if (noscale[0])
+            costa::transform<T>(la[0], lc[0], MPI_COMM_WORLD);
+        else
+            costa::transform<T>(la[0], lc[0], trans[0], alpha[0], beta[0], MPI_COMM_WORLD);
+    } else {
+        costa::transformer<T> tf(MPI_COMM_WORLD);
+        for (int p = 0; p < npairs; ++p) {
+            if (noscale[0])
+                tf.schedule(la[size_t(p)], lc[size_t(p)]);
+            else
+                tf.schedule(la[size_t(p)], lc[size_t(p)], trans[size_t(p)], alpha[size_t(p)],
+                            beta[size_t(p)]);
+        }
+        tf.transform();
+    }
+    for (int p = 0; p < npairs; ++p)
+        dump(out + "/C" + std::to_string(p) + "_rank" + std::to_string(rank) + ".bin",
+             cbuf[size_t(p)]);
+    return 0;
+}
+
+// the four known-answer tests of the reference (tests/unit/test_utils.cpp:7, 75, 143, 208)
+int run_kat(const std::string& out) {
+    auto& ws = *costa::memory::get_costa_context_instance<int>();
+    std::vector<int> in8x4 = {9, 1, 1, -1, 7, 3, 4, -1, 5, 5, 1, -1, 9, 2, 3, -1,
+                              7, 6, 5, -1, 2, 2, 4, -1, 3, 7, 4, -1, 3, 8, 1, -1};
+    {  // copy2D.row_major
+        std::vector<int> o(40);
+        costa::memory::copy_and_transform(8, 3, in8x4.data(), 4, false, o.data(), 5, false, false,
+                                          false, 1, 0, ws);
+        dump(out + "/kat_copy2D_row_major_out.bin", o);
+    }
+    {  // copy2D.col_major: in 3x8 col-major, ld 4 -> ld 5
+        std::vector<int> o(40);
+        costa::memory::copy_and_transform(3, 8, in8x4.data(), 4, true, o.data(), 5, true, false,
+                                          false, 1, 0, ws);
+        dump(out + "/kat_copy2D_col_major_out.bin", o);
+    }
+    {  // transpose.row_to_col_major
+        std::vector<int> o(30);
+        costa::memory::copy_and_transform(8, 3, in8x4.data(), 4, false, o.data(), 10, true, false,
+                                          false, 1, 0, ws);
+        dump(out + "/kat_row_to_col_major_out.bin", o);
+    }
+    {  // transpose.col_to_row_major with srand(100), in[i] = i + rand()
+        srand(100);
+        const int n_rows = 1000, n_cols = 500, in_stride = 1100, out_stride = 501;
+        std::vector<int> in(size_t(n_cols) * in_stride);
+        for (size_t i = 0; i < in.size(); ++i) in[i] = int(i) + rand();
+        std::vector<int> o(size_t(n_rows) * out_stride);
+        costa::memory::copy_and_transform(n_rows, n_cols, in.data(), in_stride, true, o.data(),
+                                          out_stride, false, false, false, 1, 0, ws);
+        dump(out + "/kat_col_to_row_major_in.bin", in);
+        dump(out + "/kat_col_to_row_major_out.bin", o);
+    }
+    dump(out + "/kat_in8x4.bin", in8x4);
+    return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    MPI_Init(&argc, &argv);
+    int rank = 0, P = 1;
+    MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+    MPI_Comm_size(MPI_COMM_WORLD, &P);
+    int rc = 1;
+    if (argc >= 3 && std::string(argv[1]) == "kat") {
+        rc = rank == 0 ? run_kat(argv[2]) : 0;
+    } else if (argc >= 4 && std::string(argv[1]) == "case") {
+        std::ifstream in(argv[2]);
+        std::string tok;
+        int dtype;
+        in >> tok >> dtype;
+        switch (dtype) {
+        case 0: rc = run_case<float>(in, argv[3], rank, P); break;
+        case 1: rc = run_case<double>(in, argv[3], rank, P); break;
+        case 2: rc = run_case<std::complex<float>>(in, argv[3], rank, P); break;
+        case 3: rc = run_case<std::complex<double>>(in, argv[3], rank, P); break;
+        default: break;  // the reference instantiates transform for the 4 FP types only
+        }
+    } else {
+        if (rank == 0) std::cerr << "usage: ref_harness kat <out> | case <spec> <out>\n";
+    }
+    MPI_Finalize();
+    return rc;
+}
