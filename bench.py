@@ -1,0 +1,235 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident tile pack + transpose + unpack (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Workload (one "step" = one costa::transform over all local tiles, data already in HBM):
+  N = 1   BASELINE configs[1]: pxtran fp64 16384 x 16384, 256 x 256 blocks, op 'T',
+          alpha = 1, beta = 0, 1 x 1 grid -> 4096 local 256^2 transposes per step.
+  N > 1   the same per rank (weak scaling): global (16384*pm) x (16384*pn) fp64 on a pm x pn
+          rank grid, C = A^T on the transposed grid; remote tiles go pack -> RCCL -> unpack,
+          local tiles are transposed in place (overlapping the exchange).
+Timing: W untimed steps; then barrier + device sync, K steps, device sync + barrier; max over
+ranks.  value = algorithmic bytes of all ranks / that time (read + write of every
+element moved, + read of C when beta != 0).  Rank 0 prints ONE JSON line.
+
+roofline: the dominant kernel's algorithmic bytes per launch / its average duration from
+HIP events recorded on the stream it runs on (costa_hip_get_stats), against 8 TB/s.
+cpu_baseline: the oracle's restatement of the reference's OpenMP tile loop (256x256-blocked
+transpose, OpenMP over tiles) on a bounded sample of the same tiles, rank 0 at N = 1.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def grid_for(n: int):
+    pm = int(math.isqrt(n))
+    while n % pm:
+        pm -= 1
+    return pm, n // pm
+
+
+def cpu_baseline(n=16384, b=256, slab_cols=2048, target_s=10.0):
+    """Oracle restatement of the reference tile loop on a 16384 x 2048 column slab of A
+    (512 tiles of 256^2 fp64, 256 MiB in / 256 MiB out), repeated for ~target_s seconds."""
+    import numpy as np
+    import oracle
+    threads = min(16, os.cpu_count() or 1)
+    a = np.random.default_rng(1).standard_normal(n * slab_cols)  # col-major, ld n
+    c = np.zeros(slab_cols * n)                                  # col-major, ld slab_cols
+    tiles = []
+    for j in range(slab_cols // b):
+        for i in range(n // b):
+            # A tile (i, j) -> C tile (j, i): (src_off, lds, dst_off, ldd, F, S)
+            tiles.append((i * b + j * b * n, n, j * b + i * b * slab_cols, slab_cols, b, b))
+    tiles = np.array(tiles, np.int64)
+    oracle.transform_tiles(1, 1, 0, 1.0, 0.0, a, c, tiles, threads)  # warm-up, first touch
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        oracle.transform_tiles(1, 1, 0, 1.0, 0.0, a, c, tiles, threads)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= target_s or reps >= 1000:
+            break
+    ok = np.array_equal(c.reshape(n, slab_cols).T, a.reshape(slab_cols, n))
+    bytes_per = 2 * a.nbytes
+    return {"value": round(bytes_per * reps / el / 1e9, 3), "unit": "GB/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{len(tiles)} tiles of 256x256 fp64 ('T', alpha=1, beta=0; a 16384x2048 "
+                      f"slab of cfg 2), {reps} passes in {el:.1f} s, oracle/costa_oracle.c "
+                      f"oracle_transform_tiles, OpenMP {threads} threads, verified={ok}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=16384, help="local matrix edge per rank")
+    ap.add_argument("--block", type=int, default=256)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    import costa_amd as costa
+
+    costa.lib()
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def max_over_ranks(x: float) -> float:
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    # ---- communicator: RCCL unique id from rank 0, broadcast over the control plane
+    if world > 1:
+        uid = torch.zeros(128, dtype=torch.uint8)
+        if rank == 0:
+            uid = torch.frombuffer(bytearray(costa.Comm.unique_id()), dtype=torch.uint8).clone()
+        dist.broadcast(uid, 0)
+        comm = costa.Comm.create(bytes(uid.numpy().tobytes()), world, rank, local_rank)
+    else:
+        comm = costa.Comm.self(local_rank)
+
+    # ---- workload
+    n, b = args.n, args.block
+    pm, pn = grid_for(world)
+    M, N = n * pm, n * pn  # A: M x N on pm x pn; C = A^T: N x M on the same rank grid
+    lr_a, lc_a = M // pm, N // pn
+    lr_c, lc_c = N // pm, M // pn
+    g = torch.Generator(device="cuda")
+    g.manual_seed(1234 + rank)
+    A = torch.rand(lr_a * lc_a, dtype=torch.float64, device="cuda", generator=g)
+    Cm = torch.zeros(lr_c * lc_c, dtype=torch.float64, device="cuda")
+    LA = costa.block_cyclic_layout(M, N, b, b, 1, 1, M, N, pm, pn, "R", 0, 0, A.data_ptr(), lr_a,
+                                   "C", rank)
+    LC = costa.block_cyclic_layout(N, M, b, b, 1, 1, N, M, pm, pn, "R", 0, 0, Cm.data_ptr(), lr_c,
+                                   "C", rank)
+    torch.cuda.synchronize()
+
+    def step():
+        costa.transform(LA, LC, comm, "T", 1.0, 0.0)
+
+    for _ in range(args.warmup):
+        step()
+    if world == 1:  # correctness of what we time: C == A^T
+        assert torch.equal(Cm.view(n, n), A.view(n, n).t()), "transpose result wrong"
+
+    costa.set_profiling(True)
+    costa.get_stats(reset=True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    el = max_over_ranks(time.perf_counter() - t0)
+    st = costa.get_stats(reset=True)
+    costa.set_profiling(False)
+
+    alg_bytes = st["local_bytes"] + st["pack_bytes"] + st["unpack_bytes"]  # this rank, K steps
+    total_bytes = alg_bytes
+    if world > 1:
+        t = torch.tensor([float(alg_bytes)], dtype=torch.float64)
+        dist.all_reduce(t)
+        total_bytes = t.item()
+    value = total_bytes / el / 1e9
+
+    # dominant kernel: the launch list moving the most bytes on this rank
+    kern = max([("local", st["local_bytes"], st["local_ms"], st["local_launches"]),
+                ("pack", st["pack_bytes"], st["pack_ms"], st["pack_launches"]),
+                ("unpack", st["unpack_bytes"], st["unpack_ms"], st["unpack_launches"])],
+               key=lambda x: x[1])
+    name, kbytes, kms, kl = kern
+    per_launch = kbytes / max(kl, 1)
+    avg_ms = kms / max(kl, 1)
+    achieved = per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+            "kernel": f"tile_kernel<double> ({name} list)", "bytes_per_launch": int(per_launch),
+            "avg_launch_ms": round(avg_ms, 4)}
+
+    # end-to-end from host memory (H2D + kernels + D2H), reported, never `value`
+    e2e = None
+    if not args.no_e2e and world == 1:
+        import numpy as np
+        ha = A.cpu().numpy()
+        hc = np.zeros_like(ha)
+        HA = costa.block_cyclic_layout(M, N, b, b, 1, 1, M, N, pm, pn, "R", 0, 0, ha, lr_a, "C", rank)
+        HC = costa.block_cyclic_layout(N, M, b, b, 1, 1, N, M, pm, pn, "R", 0, 0, hc, lr_c, "C", rank)
+        costa.transform(HA, HC, comm, "T", 1.0, 0.0)  # plan + staging allocation
+        reps, t1 = 3, time.perf_counter()
+        for _ in range(reps):
+            costa.transform(HA, HC, comm, "T", 1.0, 0.0)
+        te = (time.perf_counter() - t1) / reps
+        e2e = {"GBps_algorithmic": round(2 * ha.nbytes / te / 1e9, 2), "ms_per_call": round(te * 1e3, 2),
+               "note": "pageable host A and C; H2D of A and C ranges + kernel + D2H of C"}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(n=n, b=b)
+
+    if rank == 0:
+        line = {
+            "metric": "GB/s device-resident tile pack+transpose+unpack (fp64), % HBM peak",
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "pct_hbm_peak": round(100 * value / (HBM_PEAK_GBPS * world), 2),
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (uniform random fp64, device-resident)",
+            "config": {
+                "workload": ("pxtran fp64 16384x16384, 256x256 blocks, op T, alpha=1 beta=0, "
+                             "1x1 grid (BASELINE configs[1])") if world == 1 else
+                            (f"pxtran fp64 weak-scaled: {M}x{N} on a {pm}x{pn} rank grid "
+                             f"(16384^2 per rank), 256x256 blocks, op T, alpha=1 beta=0"),
+                "m": M, "n": N, "block": b, "grid": f"{pm}x{pn}", "op": "T",
+                "parallelism": f"{world} rank(s), one per GPU, RCCL send/recv exchange",
+                "bytes_per_step": int(total_bytes / args.steps),
+            },
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "e2e_host": e2e,
+            "phase_ms_per_step": {k: round(st[k + "_ms"] / args.steps, 4)
+                                  for k in ("pack", "local", "unpack", "exchange")},
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -105,6 +105,27 @@ def copy_and_transform(code, n_rows, n_cols, src: np.ndarray, src_stride, src_cm
                                     scalar(code, beta))
 
 
+def exec_tile_ops(code, ops: np.ndarray, scalars: np.ndarray, src_base: int = 0,
+                  dst_base: int = 0) -> None:
+    """Execute a costa_tile_op_t list on host memory, op by op, with the oracle's
+    copy_and_transform (the test-side model of one batched kernel launch)."""
+    L = lib()
+    sc = np.ascontiguousarray(scalars, NP[code]).reshape(-1)
+    one, zero = scalar(code, 1), scalar(code, 0)
+    for op in ops:
+        flags = int(op["flags"])
+        kind = (flags >> 4) & 3
+        slot = flags >> 16
+        if kind == 0:  # BITCOPY ops (pack) ignore the slot scalars
+            a, b = one, zero
+        else:
+            a, b = sc[2 * slot: 2 * slot + 1].tobytes(), sc[2 * slot + 1: 2 * slot + 2].tobytes()
+        L.oracle_copy_and_transform(code, int(op["nf"]), int(op["ns"]),
+                                    C.c_void_p(src_base + int(op["src"])), int(op["lds"]), 1,
+                                    C.c_void_p(dst_base + int(op["dst"])), int(op["ldd"]), 1,
+                                    int(flags & 1), int((flags >> 1) & 1), a, b)
+
+
 def numroc(n, nb, iproc, isrc, nprocs) -> int:
     return lib().oracle_numroc(n, nb, iproc, isrc, nprocs)
 

@@ -1,0 +1,228 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the reference's golden vectors and
+the CPU oracle.  Bit-exact for every case (copies and fp arithmetic alike: contraction is off
+on both sides); the fp tolerance is therefore 0 ulp.
+
+Multi-rank golden cases run on ONE GPU: each rank's plan is executed by the real kernels
+(pack / local / unpack launches via costa_hip_execute_tiles) and the exchange is emulated with
+device-to-device copies of exactly the segments ncclSend/ncclRecv would move.  The RCCL path
+itself runs in bench.py on multi-GPU nodes.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+import oracle
+from cases import BC, Case, Pair, all_cases
+from golden_io import first_mismatch, load, matches
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def dev(arr: np.ndarray):
+    """device copy of a numpy buffer (raw bytes, any dtype)"""
+    return torch.from_numpy(np.ascontiguousarray(arr).view(np.uint8).copy()).cuda()
+
+
+def host(t, dtype) -> np.ndarray:
+    return t.cpu().numpy().view(dtype)
+
+
+@pytest.fixture(scope="module")
+def gpu(costa):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return costa
+
+
+# ------------------------------------------------------------------ known answers
+IN8x4 = np.array([9, 1, 1, -1, 7, 3, 4, -1, 5, 5, 1, -1, 9, 2, 3, -1,
+                  7, 6, 5, -1, 2, 2, 4, -1, 3, 7, 4, -1, 3, 8, 1, -1], np.int32)
+
+
+@pytest.mark.parametrize("name,args,size", [
+    ("copy2D_row_major_out", (8, 3, 4, False, 5, False), 40),
+    ("copy2D_col_major_out", (3, 8, 4, True, 5, True), 40),
+    ("row_to_col_major_out", (8, 3, 4, False, 10, True), 30),
+])
+def test_kat_small(gpu, name, args, size):
+    nr, nc, ls, scm, ld, dcm = args
+    src = dev(IN8x4)
+    dst = dev(np.zeros(size, np.int32))
+    gpu.copy_and_transform(gpu.INT32, nr, nc, src.data_ptr(), ls, scm, dst.data_ptr(), ld, dcm)
+    torch.cuda.synchronize()
+    assert (host(dst, np.int32) == load("kat")[name]).all()
+
+
+def test_kat_col_to_row_major(gpu):
+    from test_oracle_golden import kat_inputs_col_to_row
+    inp = kat_inputs_col_to_row()
+    src = dev(inp)
+    dst = dev(np.zeros(1000 * 501, np.int32))
+    gpu.copy_and_transform(gpu.INT32, 1000, 500, src.data_ptr(), 1100, True, dst.data_ptr(), 501,
+                           False)
+    out = host(dst, np.int32)
+    assert (out.reshape(1000, 501)[:, :500] == inp.reshape(500, 1100)[:, :1000].T).all()
+    assert hashlib.sha256(out.tobytes()).digest() == bytes(load("kat")["sha_col_to_row_major_out"])
+
+
+# ------------------------------------------------------------------ golden cases
+def _run_single_rank(costa, case, on_device=True):
+    bufs = [case.inputs(k, 0) for k in range(len(case.pairs))]
+    dbufs = [(dev(a), dev(c)) for a, c in bufs] if on_device else bufs
+    As, Cs = [], []
+    for k, p in enumerate(case.pairs):
+        a, c = dbufs[k]
+        pa = a.data_ptr() if on_device else a.ctypes.data
+        pc = c.data_ptr() if on_device else c.ctypes.data
+        As.append(p.A.make_layout(0, pa, 1, case.dtype))
+        Cs.append(p.C.make_layout(0, pc, 1, case.dtype))
+    eff = [case.effective(k) for k in range(len(case.pairs))]
+    comm = costa.Comm.self(0)
+    costa.transform_batch(As, Cs, comm, [e[0] for e in eff], [e[1] for e in eff],
+                          [e[2] for e in eff])
+    out = []
+    for k in range(len(case.pairs)):
+        c = dbufs[k][1]
+        out.append(host(c, oracle.NP[case.dtype]) if on_device else c)
+    return out
+
+
+def _run_emulated_ranks(costa, case):
+    P, dt = case.P, oracle.NP[case.dtype]
+    bufs = [[tuple(dev(x) for x in case.inputs(k, r)) for k in range(len(case.pairs))]
+            for r in range(P)]
+    eff = [case.effective(k) for k in range(len(case.pairs))]
+    plans, keep = [], []
+    for r in range(P):
+        As = [p.A.make_layout(r, bufs[r][k][0].data_ptr(), P, case.dtype)
+              for k, p in enumerate(case.pairs)]
+        Cs = [p.C.make_layout(r, bufs[r][k][1].data_ptr(), P, case.dtype)
+              for k, p in enumerate(case.pairs)]
+        keep.append((As, Cs))
+        plans.append(costa.plan_export(As, Cs, r, P, [e[0] for e in eff], [e[1] for e in eff],
+                                       [e[2] for e in eff]))
+    E = np.dtype(dt).itemsize
+    send = [torch.zeros(max(1, p.send_elems) * E, dtype=torch.uint8, device="cuda") for p in plans]
+    recv = [torch.zeros(max(1, p.recv_elems) * E, dtype=torch.uint8, device="cuda") for p in plans]
+    for r, p in enumerate(plans):
+        if p.pack_ops.size:
+            costa.execute_tiles(case.dtype, p.pack_ops, p.scalars, 0, send[r].data_ptr())
+    for r in range(P):
+        for q in range(P):
+            n = int(plans[r].recv_counts[q]) * E
+            d, s = int(plans[r].recv_displs[q]) * E, int(plans[q].send_displs[r]) * E
+            if n:
+                recv[r][d:d + n].copy_(send[q][s:s + n])
+    torch.cuda.synchronize()
+    for r, p in enumerate(plans):
+        if p.unpack_ops.size:
+            costa.execute_tiles(case.dtype, p.unpack_ops, p.scalars, recv[r].data_ptr(), 0)
+        if p.local_ops.size:
+            costa.execute_tiles(case.dtype, p.local_ops, p.scalars, 0, 0)
+    return [[host(bufs[r][k][1], dt) for k in range(len(case.pairs))] for r in range(P)]
+
+
+@pytest.mark.parametrize("case", all_cases(), ids=lambda c: c.name)
+def test_golden_on_gpu(gpu, case):
+    fx = load(case.name)
+    if case.P == 1:
+        got = [_run_single_rank(gpu, case)]
+    else:
+        got = _run_emulated_ranks(gpu, case)
+    for r in range(case.P):
+        for k in range(len(case.pairs)):
+            key = f"C{k}_r{r}"
+            assert matches(fx, key, got[r][k]), f"{case.name} {key}: " + first_mismatch(
+                fx, key, got[r][k])
+
+
+@pytest.mark.parametrize("case", [c for c in all_cases() if c.P == 1][:8], ids=lambda c: c.name)
+def test_golden_host_staged(gpu, case):
+    """host-resident matrices (the reference's own situation): staged through HBM"""
+    fx = load(case.name)
+    got = _run_single_rank(gpu, case, on_device=False)
+    for k in range(len(case.pairs)):
+        assert matches(fx, f"C{k}_r0", got[k])
+
+
+# ------------------------------------------------------------------ edge cases vs oracle
+SPECIAL = np.array([0.0, -0.0, 1.0, -1.0, 1e-310, -1e-310, 1e308, -1e308, 3.5, -2.25],
+                   np.float64)
+
+
+@pytest.mark.parametrize("dtype", [0, 1, 2, 3])
+@pytest.mark.parametrize("trans", ["N", "T", "C"])
+@pytest.mark.parametrize("ab", [(1, 0), (0, 0), (0.5, 0), (1, 1), (-1.5, 0.25)])
+@pytest.mark.parametrize("ords", [("C", "C"), ("R", "C"), ("C", "R")])
+def test_special_values_vs_oracle(gpu, dtype, trans, ab, ords):
+    """signed zeros, denormals, huge values; the complex alpha = 1 'copy' fast path vs the
+    transposing path (signed-zero sensitive); beta = 0 must not read C (C holds NaN)."""
+    m, n = 37, 29
+    rng = np.random.default_rng(7)
+    a_case = BC(n if trans != "N" else m, m if trans != "N" else n, 8, 5, ord=ords[0])
+    c_case = BC(m, n, 6, 7, ord=ords[1])
+    npd = oracle.NP[dtype]
+    na, nc = a_case.buf_elems(0, 1), c_case.buf_elems(0, 1)
+    if dtype in (2, 3):
+        a = (rng.choice(SPECIAL, na) + 1j * rng.choice(SPECIAL, na)).astype(npd)
+    else:
+        a = rng.choice(SPECIAL, na).astype(npd)
+    beta = ab[1]
+    c = np.full(nc, np.nan, npd) if beta == 0 else rng.choice(SPECIAL, nc).astype(npd)
+    alpha = ab[0] if dtype < 2 else complex(ab[0], 0.5 if ab[0] not in (0, 1) else 0)
+    expected = c.copy()
+    oracle.transform(dtype, trans, alpha, beta, a_case.geom(1), [a], c_case.geom(1), [expected])
+    da, dc = dev(a), dev(c)
+    A = a_case.make_layout(0, da.data_ptr(), 1, dtype)
+    Cl = c_case.make_layout(0, dc.data_ptr(), 1, dtype)
+    gpu.transform(A, Cl, gpu.Comm.self(0), trans, alpha, beta)
+    got = host(dc, npd)
+    assert got.tobytes() == expected.tobytes()
+    if beta == 0:
+        assert not np.isnan(got[:m]).any()  # first column of C written
+
+
+# ------------------------------------------------------------------ full-size properties
+def test_cfg2_full_size_transpose(gpu):
+    """BASELINE cfg 2 at full size: pxtran fp64 16384^2, 256^2 blocks, alpha=1, beta=0.
+    Property: C == A^T exactly (bit copy through alpha*x with alpha = 1)."""
+    n, b = 16384, 256
+    A = torch.randn(n, n, dtype=torch.float64, device="cuda")
+    Cm = torch.full((n, n), float("nan"), dtype=torch.float64, device="cuda")
+    # column-major local storage: element (i, j) at i + j*n  ==  tensor[j, i]
+    LA = gpu.block_cyclic_layout(n, n, b, b, 1, 1, n, n, 1, 1, "R", 0, 0, A.data_ptr(), n, "C", 0)
+    LC = gpu.block_cyclic_layout(n, n, b, b, 1, 1, n, n, 1, 1, "R", 0, 0, Cm.data_ptr(), n, "C", 0)
+    gpu.transform(LA, LC, gpu.Comm.self(0), "T", 1.0, 0.0)
+    torch.cuda.synchronize()
+    assert torch.equal(Cm, A.t())
+
+
+def test_full_size_axpby_checksum(gpu):
+    """8192^2 fp64 'T' with alpha, beta != 0 against numpy's separately rounded
+    beta*C + alpha*A^T (no fma), compared bit for bit."""
+    n, b = 8192, 256
+    rng = np.random.default_rng(11)
+    a = rng.standard_normal(n * n)
+    c = rng.standard_normal(n * n)
+    alpha, beta = 0.75, -1.25
+    expected = (beta * c.reshape(n, n)) + (alpha * a.reshape(n, n).T)
+    da, dc = dev(a), dev(c)
+    LA = gpu.block_cyclic_layout(n, n, b, b, 1, 1, n, n, 1, 1, "R", 0, 0, da.data_ptr(), n, "C", 0)
+    LC = gpu.block_cyclic_layout(n, n, b, b, 1, 1, n, n, 1, 1, "R", 0, 0, dc.data_ptr(), n, "C", 0)
+    gpu.transform(LA, LC, gpu.Comm.self(0), "T", alpha, beta)
+    got = host(dc, np.float64).reshape(n, n)
+    assert got.tobytes() == np.ascontiguousarray(expected).tobytes()
+
+
+def test_plan_cache_reuse(gpu):
+    """the second identical call hits the plan cache and gives the same result"""
+    case = [c for c in all_cases() if c.name == "block_cyclic"][0]
+    gpu.get_stats(reset=True)
+    r1 = _run_single_rank(gpu, case)
+    r2 = _run_single_rank(gpu, case)
+    assert r1[0].tobytes() == r2[0].tobytes()
+    s = gpu.get_stats()
+    assert s["transforms"] == 2
