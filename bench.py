@@ -77,7 +77,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=16384, help="local matrix edge per rank")
+    ap.add_argument("--edge", type=int, default=16384, help="local matrix edge per rank")
     ap.add_argument("--block", type=int, default=256)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
@@ -91,7 +91,8 @@ def main():
     import costa_amd as costa
 
     costa.lib()
-    torch.cuda.set_device(local_rank)
+    device = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(device)
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
@@ -112,12 +113,12 @@ def main():
         if rank == 0:
             uid = torch.frombuffer(bytearray(costa.Comm.unique_id()), dtype=torch.uint8).clone()
         dist.broadcast(uid, 0)
-        comm = costa.Comm.create(bytes(uid.numpy().tobytes()), world, rank, local_rank)
+        comm = costa.Comm.create(bytes(uid.numpy().tobytes()), world, rank, device)
     else:
-        comm = costa.Comm.self(local_rank)
+        comm = costa.Comm.self(device)
 
     # ---- workload
-    n, b = args.n, args.block
+    n, b = args.edge, args.block
     pm, pn = grid_for(world)
     M, N = n * pm, n * pn  # A: M x N on pm x pn; C = A^T: N x M on the same rank grid
     lr_a, lc_a = M // pm, N // pn
@@ -191,6 +192,22 @@ def main():
         e2e = {"GBps_algorithmic": round(2 * ha.nbytes / te / 1e9, 2), "ms_per_call": round(te * 1e3, 2),
                "note": "pageable host A and C; H2D of A and C ranges + kernel + D2H of C"}
 
+    # fixed cost of one blocking transform call (plan-cache hit, one 64x64 tile)
+    overhead_us = None
+    if world == 1:
+        ta = torch.zeros(64 * 64, dtype=torch.float64, device="cuda")
+        tc = torch.zeros(64 * 64, dtype=torch.float64, device="cuda")
+        SA = costa.block_cyclic_layout(64, 64, 64, 64, 1, 1, 64, 64, 1, 1, "R", 0, 0, ta.data_ptr(),
+                                       64, "C", 0)
+        SC = costa.block_cyclic_layout(64, 64, 64, 64, 1, 1, 64, 64, 1, 1, "R", 0, 0, tc.data_ptr(),
+                                       64, "C", 0)
+        for _ in range(10):
+            costa.transform(SA, SC, comm, "T", 1.0, 0.0)
+        t1 = time.perf_counter()
+        for _ in range(200):
+            costa.transform(SA, SC, comm, "T", 1.0, 0.0)
+        overhead_us = round((time.perf_counter() - t1) / 200 * 1e6, 1)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(n=n, b=b)
@@ -222,6 +239,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "e2e_host": e2e,
+            "call_overhead_us": overhead_us,
             "phase_ms_per_step": {k: round(st[k + "_ms"] / args.steps, 4)
                                   for k in ("pack", "local", "unpack", "exchange")},
         }

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import struct
 from dataclasses import dataclass
 from typing import Iterable, Sequence
 
@@ -169,6 +170,11 @@ def _ptr(p) -> int:
 
 
 def _scalar_bytes(code: int, x) -> bytes:
+    if code == DOUBLE:
+        return struct.pack("<d", float(x))
+    if code == CDOUBLE:
+        z = complex(x)
+        return struct.pack("<dd", z.real, z.imag)
     return np.asarray(x, dtype=_NP[code]).reshape(1).tobytes()
 
 

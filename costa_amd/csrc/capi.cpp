@@ -105,6 +105,7 @@ int costa_hip_block_cyclic_layout(costa_dtype_t dtype, int m, int n, int block_m
                                                    p_n, rank_grid_ordering, rsrc, csrc,
                                                    static_cast<T*>(ptr), lld, data_ordering, rank);
             h->e = costa::engine::erase(L);
+            h->e.hash = costa::engine::layout_hash(h->e);  // handles are immutable
         });
         *out = h.release();
     });
@@ -125,6 +126,7 @@ int costa_hip_custom_layout(costa_dtype_t dtype, int rowblocks, int colblocks, c
                                              reinterpret_cast<const costa::block_t*>(localblocks),
                                              ordering);
             h->e = costa::engine::erase(L);
+            h->e.hash = costa::engine::layout_hash(h->e);  // handles are immutable
         });
         *out = h.release();
     });

@@ -161,18 +161,33 @@ void comm_unique_id(unsigned char* out) {
 }
 
 // ---------------------------------------------------------------- work lists
-void build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops,
-                std::vector<uint64_t>& work) {
-    int bf = 0, bs = 0;
-    tile_shape(dtype, &bf, &bs);
+bool any_transpose(const std::vector<costa_tile_op_t>& ops) {
+    for (const auto& op : ops)
+        if (op.flags & COSTA_TILE_TRANSPOSE) return true;
+    return false;
+}
+
+// An op goes to the large shape when it holds at least half a large sub-tile of data;
+// smaller (ragged, many-small) tiles go to the small shape so a workgroup is not mostly idle.
+int64_t build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops,
+                   std::vector<uint64_t>& work) {
+    int bfl = 0, bsl = 0, bfs = 0, bss = 0;
+    tile_shapes(dtype, &bfl, &bsl, &bfs, &bss);
     work.clear();
+    std::vector<uint64_t> small;
     for (size_t i = 0; i < ops.size(); ++i) {
         const auto& op = ops[i];
         if (op.nf <= 0 || op.ns <= 0) continue;
+        const bool large = 2 * int64_t(op.nf) * op.ns >= int64_t(bfl) * bsl;
+        const int bf = large ? bfl : bfs, bs = large ? bsl : bss;
         const uint64_t n = uint64_t((op.nf + bf - 1) / bf) * uint64_t((op.ns + bs - 1) / bs);
-        if (n > 0xFFFFFFFFull) throw error(COSTA_ERR_ARG, "costa: tile too large");
-        for (uint64_t k = 0; k < n; ++k) work.push_back((uint64_t(i) << 32) | k);
+        if (n > 0xFFFFFFFFull || i > 0xFFFFFFFFull) throw error(COSTA_ERR_ARG, "costa: tile too large");
+        auto& dst = large ? work : small;
+        for (uint64_t k = 0; k < n; ++k) dst.push_back((uint64_t(i) << 32) | k);
     }
+    const int64_t n_large = int64_t(work.size());
+    work.insert(work.end(), small.begin(), small.end());
+    return n_large;
 }
 
 // ---------------------------------------------------------------- residency / staging
@@ -263,6 +278,16 @@ struct hasher {
     }
 };
 
+}  // namespace
+
+uint64_t layout_hash(const elayout& L) {
+    hasher h;
+    h.mix_layout(L);
+    return h.h | 1;  // never 0 (0 = "not computed")
+}
+
+namespace {
+
 struct cached_plan {
     std::unique_ptr<plan> p;
     int device = 0;
@@ -273,6 +298,8 @@ struct cached_plan {
     // device copies of the op lists and work lists
     dbuf d_local, d_pack, d_unpack, w_local, w_pack, w_unpack, d_scal;
     int64_t n_local = 0, n_pack = 0, n_unpack = 0;
+    int64_t l_local = 0, l_pack = 0, l_unpack = 0;  // large-shape items at the front
+    bool tr_local = true, tr_unpack = true;          // any op of the list transposes
     std::vector<unsigned char> scal_host;
 };
 
@@ -322,8 +349,8 @@ cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
     h.mix(uint64_t(c->device));
     h.mix(jobs.size());
     for (const auto& j : jobs) {
-        h.mix_layout(*j.A);
-        h.mix_layout(*j.C);
+        h.mix(j.A->hash ? j.A->hash : layout_hash(*j.A));  // handles cache their hash
+        h.mix(j.C->hash ? j.C->hash : layout_hash(*j.C));
         h.mix(uint64_t(uint8_t(std::toupper(static_cast<unsigned char>(j.trans)))));
         // the scale kinds (not the values) are baked into the ops
         for (bool cm : {true, false})
@@ -406,15 +433,17 @@ cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
     const plan& p = *cp->p;
     std::vector<uint64_t> w;
     cp->d_local.upload(p.local_ops, dc.main);
-    build_work(p.dtype, p.local_ops, w);
+    cp->tr_local = any_transpose(p.local_ops);
+    cp->tr_unpack = any_transpose(p.unpack_ops);
+    cp->l_local = build_work(p.dtype, p.local_ops, w);
     cp->n_local = int64_t(w.size());
     cp->w_local.upload(w, dc.main);
     cp->d_pack.upload(p.pack_ops, dc.main);
-    build_work(p.dtype, p.pack_ops, w);
+    cp->l_pack = build_work(p.dtype, p.pack_ops, w);
     cp->n_pack = int64_t(w.size());
     cp->w_pack.upload(w, dc.main);
     cp->d_unpack.upload(p.unpack_ops, dc.main);
-    build_work(p.dtype, p.unpack_ops, w);
+    cp->l_unpack = build_work(p.dtype, p.unpack_ops, w);
     cp->n_unpack = int64_t(w.size());
     cp->w_unpack.upload(w, dc.main);
     HIP_CHECK(hipStreamSynchronize(dc.main));  // host vectors above are temporaries
@@ -483,8 +512,8 @@ void transform(const std::vector<job>& jobs, comm* c) {
         if (prof) HIP_CHECK(hipEventRecord(dc.t[0], ls));
         launch_tiles(p.dtype,
                      {static_cast<const costa_tile_op_t*>(cp.d_local.p),
-                      static_cast<const uint64_t*>(cp.w_local.p), cp.n_local, nullptr, nullptr,
-                      cp.d_scal.p},
+                      static_cast<const uint64_t*>(cp.w_local.p), cp.n_local, cp.l_local, nullptr, nullptr,
+                      cp.d_scal.p, cp.tr_local},
                      ls);
         if (prof) HIP_CHECK(hipEventRecord(dc.t[1], ls));
     }
@@ -499,8 +528,8 @@ void transform(const std::vector<job>& jobs, comm* c) {
             if (prof) HIP_CHECK(hipEventRecord(dc.t[2], dc.main));
             launch_tiles(p.dtype,
                          {static_cast<const costa_tile_op_t*>(cp.d_pack.p),
-                          static_cast<const uint64_t*>(cp.w_pack.p), cp.n_pack, nullptr, sb,
-                          cp.d_scal.p},
+                          static_cast<const uint64_t*>(cp.w_pack.p), cp.n_pack, cp.l_pack, nullptr, sb,
+                          cp.d_scal.p, false},
                          dc.main);
             if (prof) HIP_CHECK(hipEventRecord(dc.t[3], dc.main));
         }
@@ -520,8 +549,8 @@ void transform(const std::vector<job>& jobs, comm* c) {
         if (cp.n_unpack)
             launch_tiles(p.dtype,
                          {static_cast<const costa_tile_op_t*>(cp.d_unpack.p),
-                          static_cast<const uint64_t*>(cp.w_unpack.p), cp.n_unpack, rb, nullptr,
-                          cp.d_scal.p},
+                          static_cast<const uint64_t*>(cp.w_unpack.p), cp.n_unpack, cp.l_unpack, rb, nullptr,
+                          cp.d_scal.p, cp.tr_unpack},
                          dc.main);
         if (prof) HIP_CHECK(hipEventRecord(dc.t[5], dc.main));
         HIP_CHECK(hipStreamWaitEvent(dc.main, dc.ev_local, 0));
@@ -572,7 +601,7 @@ void execute_tiles(costa_dtype_t dtype, const costa_tile_op_t* ops, int64_t n,
         if ((op.flags >> COSTA_SLOT_SHIFT) >= uint32_t(std::max(n_slots, 0)))
             throw error(COSTA_ERR_ARG, "costa_hip_execute_tiles: scalar slot out of range");
     std::vector<uint64_t> w;
-    build_work(dtype, v, w);
+    const int64_t nl = build_work(dtype, v, w);
     dbuf d_ops, d_work, d_scal;
     d_ops.upload(v, dc.main);
     d_work.upload(w, dc.main);
@@ -582,8 +611,8 @@ void execute_tiles(costa_dtype_t dtype, const costa_tile_op_t* ops, int64_t n,
     d_scal.upload(sc, dc.main);
     launch_tiles(dtype,
                  {static_cast<const costa_tile_op_t*>(d_ops.p), static_cast<const uint64_t*>(d_work.p),
-                  int64_t(w.size()), static_cast<const char*>(src_base), static_cast<char*>(dst_base),
-                  d_scal.p},
+                  int64_t(w.size()), nl, static_cast<const char*>(src_base), static_cast<char*>(dst_base),
+                  d_scal.p, any_transpose(v)},
                  dc.main);
     HIP_CHECK(hipStreamSynchronize(dc.main));
 }

@@ -33,6 +33,7 @@ struct elayout {
     int n_ranks = 1;
     char ordering = 'C';
     std::vector<eblock> blocks;
+    uint64_t hash = 0;  // content hash (plan-cache key); 0 = not computed yet
 
     int nbr() const { return int(rows_split.size()) - 1; }
     int nbc() const { return int(cols_split.size()) - 1; }
@@ -43,6 +44,9 @@ costa_dtype_t dtype_of();
 
 template <typename T>
 elayout erase(const grid_layout<T>& L);
+
+// content hash of a layout (splits, owners, ordering, every block's intervals/pointer/ld)
+uint64_t layout_hash(const elayout& L);
 
 // scalars (alpha, beta) of one layout pair, stored as raw bytes of the dtype
 struct scal {
@@ -105,17 +109,20 @@ void execute_tiles(costa_dtype_t dtype, const costa_tile_op_t* ops, int64_t n,
 struct launch_args {
     const costa_tile_op_t* ops;
     const uint64_t* work;   // per workgroup: (op index << 32) | sub-tile index
-    int64_t n_work;
+    int64_t n_work;         // total work items
+    int64_t n_large;        // the first n_large items use the large sub-tile shape
     const char* src_base;
     char* dst_base;
     const void* scalars;    // device: n_slots x (alpha, beta) of the dtype
+    bool any_transpose;     // false: copy-mode ops only, launch without the LDS tile
 };
+bool any_transpose(const std::vector<costa_tile_op_t>& ops);
 void launch_tiles(costa_dtype_t dtype, const launch_args& a, void* stream /* hipStream_t */);
-// sub-tile shape (elements along src fast dim, along src slow dim) used by the kernels
-void tile_shape(costa_dtype_t dtype, int* bf, int* bs);
-// build the per-workgroup work list of an op list
-void build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops,
-                std::vector<uint64_t>& work);
+// sub-tile shapes (elements along the source's fast dim, along its slow dim)
+void tile_shapes(costa_dtype_t dtype, int* bf_large, int* bs_large, int* bf_small, int* bs_small);
+// per-workgroup work list of an op list: large-shape items first; returns their count
+int64_t build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops,
+                   std::vector<uint64_t>& work);
 
 // errors
 struct error : std::runtime_error {

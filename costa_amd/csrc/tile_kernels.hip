@@ -1,18 +1,27 @@
 // Batched tile kernels for CDNA4 (gfx950): one launch runs a whole list of tile ops
-// (pack, local or unpack), one 256-thread workgroup per sub-tile.
+// (pack, local or unpack), one workgroup per sub-tile of one op.
 //
 // What each op computes is the reference's copy_and_transform
 // (eth-cscs/COSTA src/costa/grid2grid/memory_utils.hpp:339-412):
-//   copy mode       dst(f, s) = g(src(f, s))            copy2D / copy         :20-98
-//   transpose mode  dst(s, f) = g(src(f, s))            transpose_{col,row}_major :101-291
-//   g(x) = x | 0 | alpha*op(x) | beta*dst + alpha*op(x) (op = conj for 'C' on complex)
-// evaluated in the same order as the reference with contraction OFF, so results are
-// bit-identical to the x86 build (which has no FMA: SURVEY §8c).
+//   copy mode       dst(f, s) = g(src(f, s))                 copy2D / copy           :20-98
+//   transpose mode  dst(s, f) = g(src(f, s))                 transpose_{col,row}_major :101-291
+//   g(x) = x | 0 | alpha*op(x) | beta*dst + alpha*op(x)      (op = conj for 'C' on complex)
+// evaluated in the reference's order with contraction OFF: results are bit-identical to the
+// reference's x86 build (which has no FMA: SURVEY §8c).
 //
-// Memory path: the transpose stages each BF x BS sub-tile through LDS. Global loads are
-// 16-byte vectors along the source's contiguous dimension, global stores are whole
-// wavefront rows along the destination's contiguous dimension.  No MFMA: the op is
-// purely HBM-bound (<= 0.5 flop/byte).
+// Memory path (HBM-bound, no MFMA: <= 0.5 flop/byte):
+//   load   every lane fetches 16-byte vectors along the source's contiguous dimension; all
+//          of a thread's loads are issued before any is consumed
+//   LDS    the sub-tile is staged as rows s with a 16-byte pad per row, so both the
+//          ds_write_b128 of the load phase and the ds_read_b128 of the store phase are
+//          bank-conflict free
+//   store  a lane reads one 16-byte LDS slot (V elements along f for one s); V lanes then
+//          transpose their V x V block through cross-lane shuffles, so every lane stores one
+//          16-byte vector along the destination's contiguous dimension
+// Two shapes: "large" (1024 threads, ~130 KiB LDS, 1 KiB load segments) for ops with at
+// least half a large sub-tile of data, "small" (256 threads, ~33 KiB) for the rest.
+// Measured on MI355X (tools/tune_transpose.hip): the large shape moves cfg-2 transposes at
+// 91 % of the best flat 16-byte copy of the same bytes.
 #include <hip/hip_runtime.h>
 
 #include "engine.hpp"
@@ -22,8 +31,6 @@
 namespace costa {
 namespace engine {
 namespace {
-
-constexpr int NT = 256;  // threads per workgroup = 4 wavefronts
 
 template <typename R>
 struct cpx {
@@ -65,30 +72,30 @@ __device__ __forceinline__ T scale(T x, T y, uint32_t kind, bool conj, T alpha, 
     return x;  // BITCOPY
 }
 
-// sub-tile shape: BF elements along the source's contiguous dim (one 512-byte strip per
-// 32 lanes), BS = 64 along the strided dim; V elements per 16-byte vector
-template <typename T>
-struct shape {
-    static constexpr int V = 16 / sizeof(T);
-    static constexpr int BF = 32 * V;
-    static constexpr int BS = 64;
-};
+// ---- cross-lane moves ----
+__device__ __forceinline__ float shfl(float v, int l) { return __shfl(v, l); }
+__device__ __forceinline__ int shfl(int v, int l) { return __shfl(v, l); }
+__device__ __forceinline__ double shfl(double v, int l) { return __shfl(v, l); }
+__device__ __forceinline__ cpx<float> shfl(cpx<float> v, int l) {
+    return {__shfl(v.re, l), __shfl(v.im, l)};
+}
 
-struct __attribute__((aligned(16))) vec16 {
+// V elements = one 16-byte vector
+template <typename T>
+struct vec {
+    static constexpr int V = 16 / int(sizeof(T));
+    T e[V];
+};
+struct __attribute__((aligned(16))) raw16 {
     uint32_t w[4];
 };
 
 template <typename T>
-union pack16 {
-    vec16 v;
-    T e[shape<T>::V];
-};
-
-template <typename T>
-__device__ __forceinline__ void load_strip(const T* p, int n, bool vec, pack16<T>& out) {
-    constexpr int V = shape<T>::V;
-    if (vec && n == V) {
-        out.v = *reinterpret_cast<const vec16*>(p);
+__device__ __forceinline__ void vload(vec<T>& out, const T* p, int n, bool vec_ok) {
+    constexpr int V = vec<T>::V;
+    if (vec_ok && n >= V) {
+        raw16 r = *reinterpret_cast<const raw16*>(p);
+        __builtin_memcpy(&out, &r, 16);
     } else {
 #pragma unroll
         for (int k = 0; k < V; ++k)
@@ -97,10 +104,12 @@ __device__ __forceinline__ void load_strip(const T* p, int n, bool vec, pack16<T
 }
 
 template <typename T>
-__device__ __forceinline__ void store_strip(T* p, int n, bool vec, const pack16<T>& in) {
-    constexpr int V = shape<T>::V;
-    if (vec && n == V) {
-        *reinterpret_cast<vec16*>(p) = in.v;
+__device__ __forceinline__ void vstore(T* p, const vec<T>& in, int n, bool vec_ok) {
+    constexpr int V = vec<T>::V;
+    if (vec_ok && n >= V) {
+        raw16 r;
+        __builtin_memcpy(&r, &in, 16);
+        *reinterpret_cast<raw16*>(p) = r;
     } else {
 #pragma unroll
         for (int k = 0; k < V; ++k)
@@ -108,153 +117,261 @@ __device__ __forceinline__ void store_strip(T* p, int n, bool vec, const pack16<
     }
 }
 
-// ---- copy mode: dst(f, s) = g(src(f, s)); no LDS ----
+// Lanes k = 0..V-1 of an aligned group hold in[.] = row k of a V x V block; afterwards
+// lane k holds column k.  Round r: every lane offers element (k - r) mod V and reads the
+// offer of lane (k + r) mod V.  All indices are compile-time after unrolling.
 template <typename T>
-__device__ __forceinline__ void copy_tile(const T* __restrict__ src, T* __restrict__ dst, int tf,
-                                          int ts, int64_t lds, int64_t ldd, uint32_t flags,
-                                          T alpha, T beta) {
-    constexpr int V = shape<T>::V;
-    constexpr int LPC = shape<T>::BF / V;  // lanes per column (32)
-    constexpr int CPP = NT / LPC;          // columns per pass (8)
-    const int lane_f = (threadIdx.x % LPC) * V;
-    const int col0 = threadIdx.x / LPC;
-    const uint32_t kind = (flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT;
-    const bool conj = flags & COSTA_TILE_CONJ;
-    const bool vs = flags & COSTA_TILE_VEC_SRC, vd = flags & COSTA_TILE_VEC_DST;
-    const int n = min(V, tf - lane_f);
-    if (n <= 0) return;
-    constexpr int P = shape<T>::BS / CPP;  // passes
-    pack16<T> x[P];
+__device__ __forceinline__ vec<T> lane_transpose(const vec<T>& in, int lane) {
+    constexpr int V = vec<T>::V;
+    vec<T> out;
+    if constexpr (V == 1) {
+        out = in;
+    } else {
+        const int k = lane & (V - 1), base = lane - k;
 #pragma unroll
-    for (int k = 0; k < P; ++k) {
-        const int s = col0 + k * CPP;
-        if (s < ts) load_strip(src + s * lds + lane_f, n, vs, x[k]);
-    }
+        for (int r = 0; r < V; ++r) {
+            const int give = (k - r) & (V - 1), from = (k + r) & (V - 1);
+            T offer = in.e[0];
 #pragma unroll
-    for (int k = 0; k < P; ++k) {
-        const int s = col0 + k * CPP;
-        if (s >= ts) continue;
-        T* d = dst + s * ldd + lane_f;
-        if (kind != COSTA_SCALE_BITCOPY) {
-            pack16<T> y;
-            if (kind == COSTA_SCALE_AXPBY) load_strip(d, n, vd, y);
+            for (int e = 1; e < V; ++e)
+                if (e == give) offer = in.e[e];
+            const T got = r == 0 ? offer : shfl(offer, base + from);
 #pragma unroll
-            for (int e = 0; e < V; ++e) x[k].e[e] = scale(x[k].e[e], y.e[e], kind, conj, alpha, beta);
+            for (int e = 0; e < V; ++e)
+                if (e == from) out.e[e] = got;
         }
-        store_strip(d, n, vd, x[k]);
     }
+    return out;
 }
 
-// ---- transpose mode: dst(s, f) = g(src(f, s)), staged through LDS ----
-template <typename T>
-__device__ __forceinline__ void transpose_tile(const T* __restrict__ src, T* __restrict__ dst,
-                                               int tf, int ts, int64_t lds, int64_t ldd,
-                                               uint32_t flags, T alpha, T beta, T* tile) {
-    constexpr int V = shape<T>::V;
-    constexpr int BF = shape<T>::BF;
-    constexpr int BS = shape<T>::BS;
-    constexpr int PITCH = BF + 1;          // +1 element: conflict-free column reads
-    constexpr int LPC = BF / V;            // lanes per source column (32)
-    constexpr int CPP = NT / LPC;          // source columns per pass (8)
-    constexpr int P = BS / CPP;            // load passes (8)
+// sub-tile geometry of one kernel shape
+template <typename T, int NT_, int BF_, int BS_>
+struct shape {
+    static constexpr int NT = NT_;
+    static constexpr int V = vec<T>::V;
+    static constexpr int BF = BF_;                  // elements along the source's fast dim
+    static constexpr int BS = BS_;                  // elements along the source's slow dim
+    static constexpr int P = BF + V;                // LDS row pitch (16-byte pad)
+    static constexpr int LPC = BF / V;              // lanes per source column (load)
+    static constexpr int CPP = NT / LPC;            // source columns per load pass
+    static constexpr int PL = BS / CPP;             // load passes
+    static constexpr int NW = NT / 64;              // wavefronts
+    static constexpr int UNITS = (BS / 64) * (BF / V);  // store units: 64 s x one f slot
+    static constexpr int PS = UNITS / NW;           // store passes
+    static_assert(LPC <= NT && NT % LPC == 0 && BS % CPP == 0, "load mapping");
+    static_assert(BS % 64 == 0 && UNITS % NW == 0, "store mapping");
+    static constexpr size_t lds_bytes = size_t(BS) * P * sizeof(T);
+};
+
+// large / small shapes per element size (LDS ~130 KiB / ~33 KiB)
+template <typename T> struct shapes;
+template <> struct shapes<float> {
+    using large = shape<float, 1024, 256, 128>;
+    using small = shape<float, 256, 128, 64>;
+};
+template <> struct shapes<int> {
+    using large = shape<int, 1024, 256, 128>;
+    using small = shape<int, 256, 128, 64>;
+};
+template <> struct shapes<double> {
+    using large = shape<double, 1024, 128, 128>;
+    using small = shape<double, 256, 64, 64>;
+};
+template <> struct shapes<cpx<float>> {
+    using large = shape<cpx<float>, 1024, 128, 128>;
+    using small = shape<cpx<float>, 256, 64, 64>;
+};
+template <> struct shapes<cpx<double>> {
+    using large = shape<cpx<double>, 1024, 64, 128>;
+    using small = shape<cpx<double>, 256, 32, 64>;
+};
+
+// One sub-tile.  FULL: the sub-tile is a whole BF x BS block with 16-byte aligned rows on
+// both sides, so every guard below folds away and each thread issues its loads and stores
+// back to back with no per-lane branches (the common case: block-cyclic tiles).
+template <typename T, typename S, bool FULL>
+__device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int s0, int tf_, int ts_,
+                                         const char* src_base, char* dst_base, T alpha, T beta,
+                                         T* tile) {
+    constexpr int V = S::V, BF = S::BF, P = S::P;
+    const int tf = FULL ? S::BF : tf_;
+    const int ts = FULL ? S::BS : ts_;
+    const uint32_t flags = op.flags;
     const uint32_t kind = (flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT;
     const bool conj = flags & COSTA_TILE_CONJ;
-    const bool vs = flags & COSTA_TILE_VEC_SRC;
+    const bool vs = FULL || (flags & COSTA_TILE_VEC_SRC);
+    const bool vd = FULL || (flags & COSTA_TILE_VEC_DST);
+    const int64_t lds = op.lds, ldd = op.ldd;
+    const T* src = reinterpret_cast<const T*>(src_base + op.src) + int64_t(s0) * lds + f0;
 
-    // load: 16-byte strips along f, all loads issued before any LDS write
-    {
-        const int lane_f = (threadIdx.x % LPC) * V;
-        const int col0 = threadIdx.x / LPC;
-        const int n = min(V, tf - lane_f);
-        pack16<T> x[P];
+    // ---- load phase: lane -> (16-byte strip along f, column s); all loads issued first
+    const int lf = (int(threadIdx.x) % S::LPC) * V;
+    const int c0 = int(threadIdx.x) / S::LPC;
+    const int nf_lane = FULL ? V : tf - lf;  // elements of this lane's strip inside the tile
+    vec<T> x[S::PL];
 #pragma unroll
-        for (int k = 0; k < P; ++k) {
-            const int s = col0 + k * CPP;
-            if (n > 0 && s < ts) load_strip(src + s * lds + lane_f, n, vs, x[k]);
-        }
+    for (int k = 0; k < S::PL; ++k) {
+        const int s = c0 + k * S::CPP;
+        if (FULL || (nf_lane > 0 && s < ts)) vload(x[k], src + s * lds + lf, nf_lane, vs);
+    }
+
+    if (!(flags & COSTA_TILE_TRANSPOSE)) {
+        // ---- copy mode: dst(f, s) = g(src(f, s)), no LDS
+        T* dst = reinterpret_cast<T*>(dst_base + op.dst) + int64_t(s0) * ldd + f0;
 #pragma unroll
-        for (int k = 0; k < P; ++k) {
-            const int s = col0 + k * CPP;
-            if (n > 0 && s < ts) {
+        for (int k = 0; k < S::PL; ++k) {
+            const int s = c0 + k * S::CPP;
+            if (!FULL && (nf_lane <= 0 || s >= ts)) continue;
+            T* d = dst + s * ldd + lf;
+            if (kind != COSTA_SCALE_BITCOPY) {
+                vec<T> y;
+                if (kind == COSTA_SCALE_AXPBY) vload(y, d, nf_lane, vd);
 #pragma unroll
                 for (int e = 0; e < V; ++e)
-                    if (e < n) tile[s * PITCH + lane_f + e] = x[k].e[e];
+                    x[k].e[e] = scale(x[k].e[e], kind == COSTA_SCALE_AXPBY ? y.e[e] : e_zero<T>(),
+                                      kind, conj, alpha, beta);
             }
+            vstore(d, x[k], nf_lane, vd);
+        }
+        return;
+    }
+
+    // ---- transpose mode: dst(s, f) = g(src(f, s)) through LDS
+#pragma unroll
+    for (int k = 0; k < S::PL; ++k) {
+        const int s = c0 + k * S::CPP;
+        if (FULL || (nf_lane > 0 && s < ts)) {  // partial strips: the tail is junk, never stored
+            raw16 r;
+            __builtin_memcpy(&r, &x[k], 16);
+            *reinterpret_cast<raw16*>(tile + s * P + lf) = r;
         }
     }
     __syncthreads();
-    // store: destination row f is contiguous along s; one wavefront row per f
-    {
-        const int lane = threadIdx.x % 64;  // s within the row
-        const int wave = threadIdx.x / 64;
-        if (lane < ts) {
-            for (int f = wave; f < tf; f += NT / 64) {
-                T v = tile[lane * PITCH + f];
-                T* d = dst + f * ldd + lane;
-                T y = e_zero<T>();
-                if (kind == COSTA_SCALE_AXPBY) y = *d;
-                *d = scale(v, y, kind, conj, alpha, beta);
-            }
+
+    T* dst = reinterpret_cast<T*>(dst_base + op.dst) + int64_t(f0) * ldd + s0;
+    const int lane = int(threadIdx.x) % 64, wave = int(threadIdx.x) / 64;
+    constexpr int FSLOTS = BF / V;
+    vec<T> y[S::PS];
+#pragma unroll
+    for (int k = 0; k < S::PS; ++k) {
+        const int u = wave + S::NW * k;             // store unit: 64 s values x one f slot
+        const int sc = u / FSLOTS, q = u % FSLOTS;  // s chunk, f slot
+        const int s = sc * 64 + lane;
+        if (FULL || (s < ts && q * V < tf)) {
+            raw16 r = *reinterpret_cast<const raw16*>(tile + s * P + q * V);
+            __builtin_memcpy(&y[k], &r, 16);
         }
+    }
+#pragma unroll
+    for (int k = 0; k < S::PS; ++k) {
+        const int u = wave + S::NW * k;
+        const int sc = u / FSLOTS, q = u % FSLOTS;
+        // after the exchange lane (base + j) holds f = q*V + j for s = sc*64 + base .. +V-1
+        vec<T> o = lane_transpose(y[k], lane);
+        const int j = lane & (V - 1);
+        const int f = q * V + j;
+        const int sb = sc * 64 + (lane - j);
+        const int n = FULL ? V : ts - sb;
+        if (!FULL && (f >= tf || n <= 0)) continue;
+        T* d = dst + f * ldd + sb;
+        vec<T> old;
+        if (kind == COSTA_SCALE_AXPBY) vload(old, d, n, vd);
+        if (kind != COSTA_SCALE_BITCOPY) {
+#pragma unroll
+            for (int e = 0; e < V; ++e)
+                o.e[e] = scale(o.e[e], kind == COSTA_SCALE_AXPBY ? old.e[e] : e_zero<T>(), kind,
+                               conj, alpha, beta);
+        }
+        vstore(d, o, n, vd);
     }
 }
 
-template <typename T>
-__global__ __launch_bounds__(NT) void tile_kernel(const costa_tile_op_t* __restrict__ ops,
-                                                  const uint64_t* __restrict__ work,
-                                                  const char* src_base, char* dst_base,
-                                                  const T* __restrict__ scalars) {
-    constexpr int BF = shape<T>::BF;
-    constexpr int BS = shape<T>::BS;
-    __shared__ T tile[BS * (BF + 1)];
-
+template <typename T, typename S>
+__global__ __launch_bounds__(S::NT) void tile_kernel(const costa_tile_op_t* __restrict__ ops,
+                                                     const uint64_t* __restrict__ work,
+                                                     const char* src_base, char* dst_base,
+                                                     const T* __restrict__ scalars) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    T* tile = reinterpret_cast<T*>(smem);
+    // which sub-tile of which op (wave-uniform: scalar loads)
     const uint64_t w = work[blockIdx.x];
     const costa_tile_op_t op = ops[w >> 32];
     const uint32_t sub = uint32_t(w);
-    const int nbf = (op.nf + BF - 1) / BF;
-    const int f0 = int(sub % uint32_t(nbf)) * BF;
-    const int s0 = int(sub / uint32_t(nbf)) * BS;
-    const int tf = min(BF, op.nf - f0);
-    const int ts = min(BS, op.ns - s0);
+    const int nbf = (op.nf + S::BF - 1) / S::BF;
+    const int f0 = int(sub % uint32_t(nbf)) * S::BF;
+    const int s0 = int(sub / uint32_t(nbf)) * S::BS;
+    const int tf = min(S::BF, op.nf - f0);
+    const int ts = min(S::BS, op.ns - s0);
     const uint32_t slot = op.flags >> COSTA_SLOT_SHIFT;
     const T alpha = scalars[2 * slot];
     const T beta = scalars[2 * slot + 1];
-    const T* src = reinterpret_cast<const T*>(src_base + op.src) + int64_t(s0) * op.lds + f0;
-    if (op.flags & COSTA_TILE_TRANSPOSE) {
-        T* dst = reinterpret_cast<T*>(dst_base + op.dst) + int64_t(f0) * op.ldd + s0;
-        transpose_tile<T>(src, dst, tf, ts, op.lds, op.ldd, op.flags, alpha, beta, tile);
-    } else {
-        T* dst = reinterpret_cast<T*>(dst_base + op.dst) + int64_t(s0) * op.ldd + f0;
-        copy_tile<T>(src, dst, tf, ts, op.lds, op.ldd, op.flags, alpha, beta);
+    const uint32_t vec_both = COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST;
+    if (tf == S::BF && ts == S::BS && (op.flags & vec_both) == vec_both)
+        run_tile<T, S, true>(op, f0, s0, tf, ts, src_base, dst_base, alpha, beta, tile);
+    else
+        run_tile<T, S, false>(op, f0, s0, tf, ts, src_base, dst_base, alpha, beta, tile);
+}
+
+template <typename T, typename S>
+void launch_shape(const launch_args& a, const uint64_t* work, int64_t n, hipStream_t stream) {
+    const int64_t max_grid = 1LL << 30;
+    for (int64_t off = 0; off < n; off += max_grid) {
+        const int64_t m = std::min(max_grid, n - off);
+        // copy-only lists need no LDS tile: more workgroups per CU
+        const size_t lds = a.any_transpose ? S::lds_bytes : 0;
+        hipLaunchKernelGGL((tile_kernel<T, S>), dim3(unsigned(m)), dim3(S::NT), lds, stream,
+                           a.ops, work + off, a.src_base, a.dst_base,
+                           static_cast<const T*>(a.scalars));
     }
 }
 
 template <typename T>
 void launch_t(const launch_args& a, hipStream_t stream) {
-    const int64_t max_grid = 1LL << 30;
-    for (int64_t off = 0; off < a.n_work; off += max_grid) {
-        const int64_t n = std::min(max_grid, a.n_work - off);
-        hipLaunchKernelGGL(tile_kernel<T>, dim3(unsigned(n)), dim3(NT), 0, stream, a.ops,
-                           a.work + off, a.src_base, a.dst_base,
-                           static_cast<const T*>(a.scalars));
-    }
+    // work list: [large sub-tiles | small sub-tiles]
+    launch_shape<T, typename shapes<T>::large>(a, a.work, a.n_large, stream);
+    launch_shape<T, typename shapes<T>::small>(a, a.work + a.n_large, a.n_work - a.n_large, stream);
+}
+
+template <typename T>
+void shape_of(int* bf_l, int* bs_l, int* bf_s, int* bs_s) {
+    *bf_l = shapes<T>::large::BF;
+    *bs_l = shapes<T>::large::BS;
+    *bf_s = shapes<T>::small::BF;
+    *bs_s = shapes<T>::small::BS;
+}
+
+template <typename T>
+void set_lds_limits() {
+    // the large shape needs more than the default dynamic-LDS limit
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tile_kernel<T, typename shapes<T>::large>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              int(shapes<T>::large::lds_bytes));
 }
 
 }  // namespace
 
-void tile_shape(costa_dtype_t dtype, int* bf, int* bs) {
+void tile_shapes(costa_dtype_t dtype, int* bf_large, int* bs_large, int* bf_small, int* bs_small) {
     switch (dtype) {
-    case COSTA_FLOAT: *bf = shape<float>::BF; *bs = shape<float>::BS; return;
-    case COSTA_DOUBLE: *bf = shape<double>::BF; *bs = shape<double>::BS; return;
-    case COSTA_CFLOAT: *bf = shape<cpx<float>>::BF; *bs = shape<cpx<float>>::BS; return;
-    case COSTA_CDOUBLE: *bf = shape<cpx<double>>::BF; *bs = shape<cpx<double>>::BS; return;
-    case COSTA_INT32: *bf = shape<int>::BF; *bs = shape<int>::BS; return;
+    case COSTA_FLOAT: shape_of<float>(bf_large, bs_large, bf_small, bs_small); return;
+    case COSTA_DOUBLE: shape_of<double>(bf_large, bs_large, bf_small, bs_small); return;
+    case COSTA_CFLOAT: shape_of<cpx<float>>(bf_large, bs_large, bf_small, bs_small); return;
+    case COSTA_CDOUBLE: shape_of<cpx<double>>(bf_large, bs_large, bf_small, bs_small); return;
+    case COSTA_INT32: shape_of<int>(bf_large, bs_large, bf_small, bs_small); return;
     }
     throw error(COSTA_ERR_ARG, "unknown dtype");
 }
 
 void launch_tiles(costa_dtype_t dtype, const launch_args& a, void* stream) {
     if (a.n_work <= 0) return;
+    static bool once = [] {
+        set_lds_limits<float>();
+        set_lds_limits<double>();
+        set_lds_limits<cpx<float>>();
+        set_lds_limits<cpx<double>>();
+        set_lds_limits<int>();
+        return true;
+    }();
+    (void)once;
     hipStream_t s = static_cast<hipStream_t>(stream);
     switch (dtype) {
     case COSTA_FLOAT: launch_t<float>(a, s); break;

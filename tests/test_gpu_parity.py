@@ -192,9 +192,9 @@ def test_special_values_vs_oracle(gpu, dtype, trans, ab, ords):
     Cl = c_case.make_layout(0, dc.data_ptr(), 1, dtype)
     gpu.transform(A, Cl, gpu.Comm.self(0), trans, alpha, beta)
     got = host(dc, npd)
+    # C was pre-filled with NaN when beta == 0: any read of C would leave NaN where the
+    # oracle (which never reads C then) has a number
     assert_bits_equal_or_both_nan(got, expected)
-    if beta == 0:
-        assert not np.isnan(got[:m]).any()  # first column of C written
 
 
 # ------------------------------------------------------------------ full-size properties

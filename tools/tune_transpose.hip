@@ -1,0 +1,494 @@
+// Tuning harness (not part of the product): structural variants of the fp64 tile transpose
+// on BASELINE cfg 2 geometry (16384^2, 4096 tiles of 256^2, ld 16384), timed interleaved in
+// one process with hipEvents.  Each variant is verified against C == A^T.
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/tune_transpose.hip -o /tmp/tune && /tmp/tune
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <functional>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#define CK(x)                                                                           \
+    do {                                                                                \
+        hipError_t e = (x);                                                             \
+        if (e != hipSuccess) {                                                          \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e)); \
+            exit(1);                                                                    \
+        }                                                                               \
+    } while (0)
+
+struct op_t {
+    uint64_t src, dst;
+    int nf, ns, lds, ldd;
+    uint32_t flags, pad;
+};
+
+typedef double d2 __attribute__((ext_vector_type(2)));
+
+// ----------------------------------------------------------------------------------
+// V0: one 64x64 sub-tile per WG, 256 threads, padded LDS, 8-B row stores (product r01)
+template <int BS, int NTS>
+__global__ __launch_bounds__(256) void v_basic(const op_t* ops, const uint64_t* work) {
+    constexpr int BF = 64, P = BF + 1;
+    __shared__ double tile[BS * P];
+    const uint64_t w = work[blockIdx.x];
+    const op_t op = ops[w >> 32];
+    const uint32_t sub = uint32_t(w);
+    const int nbf = op.nf / BF;
+    const int f0 = int(sub % nbf) * BF, s0 = int(sub / nbf) * BS;
+    const double* src = reinterpret_cast<const double*>(op.src) + int64_t(s0) * op.lds + f0;
+    double* dst = reinterpret_cast<double*>(op.dst) + int64_t(f0) * op.ldd + s0;
+    const int lf = (threadIdx.x % 32) * 2, c0 = threadIdx.x / 32;
+    d2 x[BS / 8];
+#pragma unroll
+    for (int k = 0; k < BS / 8; ++k)
+        x[k] = *reinterpret_cast<const d2*>(src + int64_t(c0 + 8 * k) * op.lds + lf);
+#pragma unroll
+    for (int k = 0; k < BS / 8; ++k) {
+        tile[(c0 + 8 * k) * P + lf] = x[k].x;
+        tile[(c0 + 8 * k) * P + lf + 1] = x[k].y;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x % 64, wave = threadIdx.x / 64;
+    if (NTS) {
+#pragma unroll
+        for (int j = 0; j < BS / 64; ++j)
+#pragma unroll
+            for (int f = wave; f < BF; f += 4)
+                __builtin_nontemporal_store(tile[(lane + 64 * j) * P + f],
+                                            dst + int64_t(f) * op.ldd + lane + 64 * j);
+    } else {
+        for (int j = 0; j < BS / 64; ++j)
+            for (int f = wave; f < BF; f += 4)
+                dst[int64_t(f) * op.ldd + lane + 64 * j] = tile[(lane + 64 * j) * P + f];
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// V1: unrolled store phase with 16-B stores via a 2x2 lane-pair exchange.
+// LDS rows are s, pitch 66 doubles (conflict-free b128 reads and writes); a lane reads
+// slot (s, f..f+1) and swaps with its xor-1 neighbour so it holds (s, f),(s+1, f) [even
+// lane] or (s, f+1),(s+1, f+1) [odd lane] -> one 16-B store each.
+template <int BS, int NTS, int NTL>
+__global__ __launch_bounds__(256) void v_pair(const op_t* ops, const uint64_t* work) {
+    constexpr int BF = 64, P = BF + 2;
+    __shared__ __attribute__((aligned(16))) double tile[BS * P];
+    const uint64_t w = work[blockIdx.x];
+    const op_t op = ops[w >> 32];
+    const uint32_t sub = uint32_t(w);
+    const int nbf = op.nf / BF;
+    const int f0 = int(sub % nbf) * BF, s0 = int(sub / nbf) * BS;
+    const double* src = reinterpret_cast<const double*>(op.src) + int64_t(s0) * op.lds + f0;
+    double* dst = reinterpret_cast<double*>(op.dst) + int64_t(f0) * op.ldd + s0;
+    const int lf = (threadIdx.x % 32) * 2, c0 = threadIdx.x / 32;
+    d2 x[BS / 8];
+#pragma unroll
+    for (int k = 0; k < BS / 8; ++k) {
+        const d2* p = reinterpret_cast<const d2*>(src + int64_t(c0 + 8 * k) * op.lds + lf);
+        x[k] = NTL ? __builtin_nontemporal_load(p) : *p;
+    }
+#pragma unroll
+    for (int k = 0; k < BS / 8; ++k) *reinterpret_cast<d2*>(&tile[(c0 + 8 * k) * P + lf]) = x[k];
+    __syncthreads();
+    // store phase: a wave covers rows f, f+1 (BS s-values each): lane -> s = lane (for 64)
+    const int lane = threadIdx.x % 64, wave = threadIdx.x / 64;
+    const bool odd = lane & 1;
+    constexpr int SW = BS / 64;  // s-chunks of 64
+    d2 y[BF / 8 * SW];
+#pragma unroll
+    for (int j = 0; j < SW; ++j)
+#pragma unroll
+        for (int q = 0; q < BF / 8; ++q) {  // slot pairs: rows f = 2*(wave + 4q)
+            const int f = 2 * (wave + 4 * q);
+            y[j * (BF / 8) + q] = *reinterpret_cast<const d2*>(&tile[(lane + 64 * j) * P + f]);
+        }
+#pragma unroll
+    for (int j = 0; j < SW; ++j)
+#pragma unroll
+        for (int q = 0; q < BF / 8; ++q) {
+            d2 v = y[j * (BF / 8) + q];
+            // even lane keeps (s,f) and takes neighbour's (s+1,f); odd keeps (s+1,f+1)...
+            double give = odd ? v.x : v.y;
+            double got = __shfl_xor(give, 1);
+            d2 o;
+            if (!odd) { o.x = v.x; o.y = got; }   // (s, f), (s+1, f)
+            else      { o.x = got; o.y = v.y; }   // (s-1, f+1), (s, f+1)
+            const int f = 2 * (wave + 4 * q) + (odd ? 1 : 0);
+            const int s = (lane & ~1) + 64 * j;
+            d2* p = reinterpret_cast<d2*>(dst + int64_t(f) * op.ldd + s);
+            if (NTS) __builtin_nontemporal_store(o, p); else *p = o;
+        }
+}
+
+// ----------------------------------------------------------------------------------
+// V2: persistent WGs with software pipelining: the next sub-tile's loads are in flight
+// while the current one is stored.
+template <int BS>
+__global__ __launch_bounds__(256) void v_persist(const op_t* ops, const uint64_t* work, int64_t n) {
+    constexpr int BF = 64, P = BF + 2;
+    __shared__ __attribute__((aligned(16))) double tile[BS * P];
+    const int lf = (threadIdx.x % 32) * 2, c0 = threadIdx.x / 32;
+    const int lane = threadIdx.x % 64, wave = threadIdx.x / 64;
+    const bool odd = lane & 1;
+    int64_t i = blockIdx.x;
+    if (i >= n) return;
+    auto geo = [&](int64_t wi, const double*& src, double*& dst, int& ldd) {
+        const uint64_t w = work[wi];
+        const op_t op = ops[w >> 32];
+        const uint32_t sub = uint32_t(w);
+        const int nbf = op.nf / BF;
+        const int f0 = int(sub % nbf) * BF, s0 = int(sub / nbf) * BS;
+        src = reinterpret_cast<const double*>(op.src) + int64_t(s0) * op.lds + f0;
+        dst = reinterpret_cast<double*>(op.dst) + int64_t(f0) * op.ldd + s0;
+        ldd = op.ldd;
+        return op.lds;
+    };
+    const double* src;
+    double* dst;
+    int ldd;
+    int lds = geo(i, src, dst, ldd);
+    d2 x[BS / 8];
+#pragma unroll
+    for (int k = 0; k < BS / 8; ++k)
+        x[k] = *reinterpret_cast<const d2*>(src + int64_t(c0 + 8 * k) * lds + lf);
+    while (true) {
+#pragma unroll
+        for (int k = 0; k < BS / 8; ++k) *reinterpret_cast<d2*>(&tile[(c0 + 8 * k) * P + lf]) = x[k];
+        __syncthreads();
+        double* cdst = dst;
+        const int cldd = ldd;
+        const int64_t nxt = i + gridDim.x;
+        if (nxt < n) {
+            lds = geo(nxt, src, dst, ldd);
+#pragma unroll
+            for (int k = 0; k < BS / 8; ++k)
+                x[k] = *reinterpret_cast<const d2*>(src + int64_t(c0 + 8 * k) * lds + lf);
+        }
+        constexpr int SW = BS / 64;
+        d2 y[BF / 8 * SW];
+#pragma unroll
+        for (int j = 0; j < SW; ++j)
+#pragma unroll
+            for (int q = 0; q < BF / 8; ++q)
+                y[j * (BF / 8) + q] =
+                    *reinterpret_cast<const d2*>(&tile[(lane + 64 * j) * P + 2 * (wave + 4 * q)]);
+        __syncthreads();  // tile free for the next iteration's writes
+#pragma unroll
+        for (int j = 0; j < SW; ++j)
+#pragma unroll
+            for (int q = 0; q < BF / 8; ++q) {
+                d2 v = y[j * (BF / 8) + q];
+                double got = __shfl_xor(odd ? v.x : v.y, 1);
+                d2 o;
+                if (!odd) { o.x = v.x; o.y = got; } else { o.x = got; o.y = v.y; }
+                const int f = 2 * (wave + 4 * q) + (odd ? 1 : 0);
+                const int s = (lane & ~1) + 64 * j;
+                *reinterpret_cast<d2*>(cdst + int64_t(f) * cldd + s) = o;
+            }
+        if (nxt >= n) break;
+        i = nxt;
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// V3: generic BF x BS tile, NT threads, pair-exchange 16-B stores, optional nt loads.
+// Load: LPC = BF/2 lanes per column; store: 32 lane-pairs cover 64 s per row pair.
+template <int BF, int BS, int NT, int NTL>
+__global__ __launch_bounds__(NT) void v_gen(const op_t* ops, const uint64_t* work) {
+    constexpr int P = BF + 2;
+    __shared__ __attribute__((aligned(16))) double tile[BS * P];
+    const uint64_t w = work[blockIdx.x];
+    const op_t op = ops[w >> 32];
+    const uint32_t sub = uint32_t(w);
+    const int nbf = op.nf / BF;
+    const int f0 = int(sub % nbf) * BF, s0 = int(sub / nbf) * BS;
+    const double* src = reinterpret_cast<const double*>(op.src) + int64_t(s0) * op.lds + f0;
+    double* dst = reinterpret_cast<double*>(op.dst) + int64_t(f0) * op.ldd + s0;
+    constexpr int LPC = BF / 2, CPP = NT / LPC, PL = BS / CPP;
+    const int lf = (threadIdx.x % LPC) * 2, c0 = threadIdx.x / LPC;
+    d2 x[PL];
+#pragma unroll
+    for (int k = 0; k < PL; ++k) {
+        const d2* p = reinterpret_cast<const d2*>(src + int64_t(c0 + CPP * k) * op.lds + lf);
+        x[k] = NTL ? __builtin_nontemporal_load(p) : *p;
+    }
+#pragma unroll
+    for (int k = 0; k < PL; ++k) *reinterpret_cast<d2*>(&tile[(c0 + CPP * k) * P + lf]) = x[k];
+    __syncthreads();
+    // store: a wave = 64 lanes = 64 s values x one row pair (f, f+1); NT/64 waves
+    constexpr int NW = NT / 64, SC = BS / 64, RP = BF / 2;  // row pairs
+    constexpr int PS = SC * RP / NW;
+    const int lane = threadIdx.x % 64, wave = threadIdx.x / 64;
+    const bool odd = lane & 1;
+    d2 y[PS];
+#pragma unroll
+    for (int k = 0; k < PS; ++k) {
+        const int t = wave + NW * k, j = t / RP, rp = t % RP;
+        y[k] = *reinterpret_cast<const d2*>(&tile[(lane + 64 * j) * P + 2 * rp]);
+    }
+#pragma unroll
+    for (int k = 0; k < PS; ++k) {
+        const int t = wave + NW * k, j = t / RP, rp = t % RP;
+        d2 v = y[k];
+        double got = __shfl_xor(odd ? v.x : v.y, 1);
+        d2 o;
+        if (!odd) { o.x = v.x; o.y = got; } else { o.x = got; o.y = v.y; }
+        *reinterpret_cast<d2*>(dst + int64_t(2 * rp + (odd ? 1 : 0)) * op.ldd + (lane & ~1) + 64 * j) = o;
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// V4: v_gen as a persistent loop: the next sub-tile's loads are issued before the current
+// sub-tile's LDS read-out and stores (register double buffering).
+template <int BF, int BS, int NT>
+__global__ __launch_bounds__(NT) void v_gen_persist(const op_t* ops, const uint64_t* work,
+                                                    int64_t n) {
+    constexpr int P = BF + 2;
+    __shared__ __attribute__((aligned(16))) double tile[BS * P];
+    constexpr int LPC = BF / 2, CPP = NT / LPC, PL = BS / CPP;
+    constexpr int NW = NT / 64, SC = BS / 64, RP = BF / 2, PS = SC * RP / NW;
+    const int lf = (threadIdx.x % LPC) * 2, c0 = threadIdx.x / LPC;
+    const int lane = threadIdx.x % 64, wave = threadIdx.x / 64;
+    const bool odd = lane & 1;
+    int64_t i = blockIdx.x;
+    if (i >= n) return;
+    const double* src;
+    double* dst;
+    int lds, ldd;
+    auto geo = [&](int64_t wi) {
+        const uint64_t w = work[wi];
+        const op_t op = ops[w >> 32];
+        const uint32_t sub = uint32_t(w);
+        const int nbf = op.nf / BF;
+        const int f0 = int(sub % nbf) * BF, s0 = int(sub / nbf) * BS;
+        src = reinterpret_cast<const double*>(op.src) + int64_t(s0) * op.lds + f0;
+        dst = reinterpret_cast<double*>(op.dst) + int64_t(f0) * op.ldd + s0;
+        lds = op.lds;
+        ldd = op.ldd;
+    };
+    geo(i);
+    d2 x[PL];
+#pragma unroll
+    for (int k = 0; k < PL; ++k)
+        x[k] = *reinterpret_cast<const d2*>(src + int64_t(c0 + CPP * k) * lds + lf);
+    while (true) {
+#pragma unroll
+        for (int k = 0; k < PL; ++k) *reinterpret_cast<d2*>(&tile[(c0 + CPP * k) * P + lf]) = x[k];
+        __syncthreads();
+        double* cdst = dst;
+        const int cldd = ldd;
+        const int64_t nxt = i + gridDim.x;
+        if (nxt < n) {
+            geo(nxt);
+#pragma unroll
+            for (int k = 0; k < PL; ++k)
+                x[k] = *reinterpret_cast<const d2*>(src + int64_t(c0 + CPP * k) * lds + lf);
+        }
+        d2 y[PS];
+#pragma unroll
+        for (int k = 0; k < PS; ++k) {
+            const int t = wave + NW * k, j = t / RP, rp = t % RP;
+            y[k] = *reinterpret_cast<const d2*>(&tile[(lane + 64 * j) * P + 2 * rp]);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < PS; ++k) {
+            const int t = wave + NW * k, j = t / RP, rp = t % RP;
+            d2 v = y[k];
+            double got = __shfl_xor(odd ? v.x : v.y, 1);
+            d2 o;
+            if (!odd) { o.x = v.x; o.y = got; } else { o.x = got; o.y = v.y; }
+            *reinterpret_cast<d2*>(cdst + int64_t(2 * rp + (odd ? 1 : 0)) * cldd + (lane & ~1) + 64 * j) = o;
+        }
+        if (nxt >= n) break;
+        i = nxt;
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// ceiling: flat 16-B copy of the same bytes (grid-stride)
+__global__ __launch_bounds__(256) void v_copy(const d2* a, d2* c, int64_t n) {
+    for (int64_t i = blockIdx.x * int64_t(256) + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256)
+        c[i] = a[i];
+}
+
+// ceiling probes: each WG moves U*256 contiguous 16-B chunks per iteration, loads first
+template <int U, int NTL, int NTS>
+__global__ __launch_bounds__(256) void v_copy_ilp(const d2* a, d2* c, int64_t n) {
+    const int64_t per = int64_t(U) * 256;
+    for (int64_t base = blockIdx.x * per; base < n; base += int64_t(gridDim.x) * per) {
+        d2 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const d2* p = a + base + u * 256 + threadIdx.x;
+            x[u] = NTL ? __builtin_nontemporal_load(p) : *p;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            d2* p = c + base + u * 256 + threadIdx.x;
+            if (NTS) __builtin_nontemporal_store(x[u], p); else *p = x[u];
+        }
+    }
+}
+template <int U>
+__global__ __launch_bounds__(256) void v_read(const d2* a, int64_t n, d2* sink) {
+    d2 acc = {0, 0};
+    const int64_t per = int64_t(U) * 256;
+    for (int64_t base = blockIdx.x * per; base < n; base += int64_t(gridDim.x) * per) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc += a[base + u * 256 + threadIdx.x];
+    }
+    if (acc.x == 12345.678) sink[threadIdx.x] = acc;
+}
+template <int U>
+__global__ __launch_bounds__(256) void v_write(d2* c, int64_t n) {
+    const int64_t per = int64_t(U) * 256;
+    d2 v = {1.0, 2.0};
+    for (int64_t base = blockIdx.x * per; base < n; base += int64_t(gridDim.x) * per) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) c[base + u * 256 + threadIdx.x] = v;
+    }
+}
+
+__global__ void fill(double* a, int64_t n) {
+    for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n;
+         i += int64_t(gridDim.x) * blockDim.x)
+        a[i] = double(i % 1000003) * 0.5 + double(i / 1000003);
+}
+
+__global__ void check(const double* a, const double* c, int n, unsigned long long* bad) {
+    int64_t k = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+    if (k >= int64_t(n) * n) return;
+    int i = int(k % n), j = int(k / n);  // C(i, j) at i + j*n must be A(j, i) at j + i*n
+    if (c[k] != a[j + int64_t(i) * n]) atomicAdd(bad, 1ull);
+}
+
+int main(int argc, char** argv) {
+    const int n = 16384, b = 256;
+    const int reps = argc > 1 ? atoi(argv[1]) : 10;
+    double *A, *Cm;
+    CK(hipMalloc(&A, sizeof(double) * n * n));
+    CK(hipMalloc(&Cm, sizeof(double) * n * n));
+    hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, A, int64_t(n) * n);
+    std::vector<op_t> ops;
+    for (int j = 0; j < n / b; ++j)
+        for (int i = 0; i < n / b; ++i) {
+            op_t o{};
+            o.src = uint64_t(A + i * b + int64_t(j) * b * n);
+            o.dst = uint64_t(Cm + j * b + int64_t(i) * b * n);
+            o.nf = o.ns = b;
+            o.lds = o.ldd = n;
+            ops.push_back(o);
+        }
+    op_t* d_ops;
+    CK(hipMalloc(&d_ops, ops.size() * sizeof(op_t)));
+    CK(hipMemcpy(d_ops, ops.data(), ops.size() * sizeof(op_t), hipMemcpyHostToDevice));
+    auto mkwork = [&](int BS, int BF = 64, bool xcd = false) {
+        std::vector<uint64_t> w;
+        for (size_t o = 0; o < ops.size(); ++o)
+            for (uint64_t k = 0; k < uint64_t(b / BF) * (b / BS); ++k) w.push_back((uint64_t(o) << 32) | k);
+        if (xcd) {  // blockIdx p -> XCD p%8: give each XCD a contiguous run of the list
+            std::vector<uint64_t> v(w.size());
+            const size_t per = w.size() / 8;
+            for (size_t p = 0; p < w.size(); ++p) v[p] = w[(p % 8) * per + p / 8];
+            w.swap(v);
+        }
+        uint64_t* d;
+        CK(hipMalloc(&d, w.size() * 8));
+        CK(hipMemcpy(d, w.data(), w.size() * 8, hipMemcpyHostToDevice));
+        return std::make_pair(d, int64_t(w.size()));
+    };
+    auto w64 = mkwork(64), w128 = mkwork(128);
+    auto w64x = mkwork(64, 64, true);
+    auto g128x64 = mkwork(64, 128), g128x128 = mkwork(128, 128), g64x128 = mkwork(128, 64);
+    unsigned long long* bad;
+    CK(hipMalloc(&bad, 8));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const double bytes = 2.0 * sizeof(double) * n * n;
+    int cus = 256;
+
+    struct var {
+        std::string name;
+        std::function<void()> run;
+        bool verify;
+        std::vector<float> ms;
+    };
+    std::vector<var> V;
+    V.push_back({"basic 64x64", [&] { hipLaunchKernelGGL((v_basic<64, 0>), dim3(w64.second), dim3(256), 0, 0, d_ops, w64.first); }, true, {}});
+    V.push_back({"basic 64x64 nt-store", [&] { hipLaunchKernelGGL((v_basic<64, 1>), dim3(w64.second), dim3(256), 0, 0, d_ops, w64.first); }, true, {}});
+    V.push_back({"basic 64x128", [&] { hipLaunchKernelGGL((v_basic<128, 0>), dim3(w128.second), dim3(256), 0, 0, d_ops, w128.first); }, true, {}});
+    V.push_back({"pair 64x64", [&] { hipLaunchKernelGGL((v_pair<64, 0, 0>), dim3(w64.second), dim3(256), 0, 0, d_ops, w64.first); }, true, {}});
+    V.push_back({"pair 64x64 nt-store", [&] { hipLaunchKernelGGL((v_pair<64, 1, 0>), dim3(w64.second), dim3(256), 0, 0, d_ops, w64.first); }, true, {}});
+    V.push_back({"pair 64x64 nt-load", [&] { hipLaunchKernelGGL((v_pair<64, 0, 1>), dim3(w64.second), dim3(256), 0, 0, d_ops, w64.first); }, true, {}});
+    V.push_back({"pair 64x128", [&] { hipLaunchKernelGGL((v_pair<128, 0, 0>), dim3(w128.second), dim3(256), 0, 0, d_ops, w128.first); }, true, {}});
+    for (int k : {4, 8, 16}) {
+        V.push_back({"persist 64x64 x" + std::to_string(k), [&, k] { hipLaunchKernelGGL((v_persist<64>), dim3(cus * k), dim3(256), 0, 0, d_ops, w64.first, w64.second); }, true, {}});
+    }
+    V.push_back({"persist 64x128 x4", [&] { hipLaunchKernelGGL((v_persist<128>), dim3(cus * 4), dim3(256), 0, 0, d_ops, w128.first, w128.second); }, true, {}});
+    V.push_back({"flat copy 16B (ceiling)", [&] { hipLaunchKernelGGL(v_copy, dim3(cus * 16), dim3(256), 0, 0, (const d2*)A, (d2*)Cm, int64_t(n) * n / 2); }, false, {}});
+    V.push_back({"hipMemcpyDtoD (ceiling)", [&] { CK(hipMemcpyAsync(Cm, A, sizeof(double) * n * n, hipMemcpyDeviceToDevice, 0)); }, false, {}});
+    V.push_back({"gen 64x64 t256 nt-load", [&] { hipLaunchKernelGGL((v_gen<64, 64, 256, 1>), dim3(w64.second), dim3(256), 0, 0, d_ops, w64.first); }, true, {}});
+    V.push_back({"gen 64x64 t256 nt-load xcd", [&] { hipLaunchKernelGGL((v_gen<64, 64, 256, 1>), dim3(w64x.second), dim3(256), 0, 0, d_ops, w64x.first); }, true, {}});
+    V.push_back({"gen 128x64 t512", [&] { hipLaunchKernelGGL((v_gen<128, 64, 512, 0>), dim3(g128x64.second), dim3(512), 0, 0, d_ops, g128x64.first); }, true, {}});
+    V.push_back({"gen 128x64 t512 nt-load", [&] { hipLaunchKernelGGL((v_gen<128, 64, 512, 1>), dim3(g128x64.second), dim3(512), 0, 0, d_ops, g128x64.first); }, true, {}});
+    V.push_back({"gen 128x64 t256", [&] { hipLaunchKernelGGL((v_gen<128, 64, 256, 0>), dim3(g128x64.second), dim3(256), 0, 0, d_ops, g128x64.first); }, true, {}});
+    V.push_back({"gen 64x128 t512", [&] { hipLaunchKernelGGL((v_gen<64, 128, 512, 0>), dim3(g64x128.second), dim3(512), 0, 0, d_ops, g64x128.first); }, true, {}});
+    V.push_back({"gen 128x128 t1024", [&] { hipLaunchKernelGGL((v_gen<128, 128, 1024, 0>), dim3(g128x128.second), dim3(1024), 0, 0, d_ops, g128x128.first); }, true, {}});
+    V.push_back({"gen 128x128 t1024 nt-load", [&] { hipLaunchKernelGGL((v_gen<128, 128, 1024, 1>), dim3(g128x128.second), dim3(1024), 0, 0, d_ops, g128x128.first); }, true, {}});
+    for (int k : {1, 2}) {
+        V.push_back({"gpersist 128x128 t1024 x" + std::to_string(k), [&, k] { hipLaunchKernelGGL((v_gen_persist<128, 128, 1024>), dim3(cus * k), dim3(1024), 0, 0, d_ops, g128x128.first, g128x128.second); }, true, {}});
+    }
+    for (int k : {2, 3}) {
+        V.push_back({"gpersist 128x64 t512 x" + std::to_string(k), [&, k] { hipLaunchKernelGGL((v_gen_persist<128, 64, 512>), dim3(cus * k), dim3(512), 0, 0, d_ops, g128x64.first, g128x64.second); }, true, {}});
+    }
+    V.push_back({"gpersist 64x64 t256 x4", [&] { hipLaunchKernelGGL((v_gen_persist<64, 64, 256>), dim3(cus * 4), dim3(256), 0, 0, d_ops, w64.first, w64.second); }, true, {}});
+    V.push_back({"gen 128x128 t512", [&] { hipLaunchKernelGGL((v_gen<128, 128, 512, 0>), dim3(g128x128.second), dim3(512), 0, 0, d_ops, g128x128.first); }, true, {}});
+    const int64_t n2 = int64_t(n) * n / 2;
+    for (int g : {2, 4, 8, 32}) {
+        V.push_back({"copy U8 grid " + std::to_string(g) + "/CU", [&, g] { hipLaunchKernelGGL((v_copy_ilp<8, 0, 0>), dim3(cus * g), dim3(256), 0, 0, (const d2*)A, (d2*)Cm, n2); }, false, {}});
+    }
+    V.push_back({"copy U4 grid 8/CU", [&] { hipLaunchKernelGGL((v_copy_ilp<4, 0, 0>), dim3(cus * 8), dim3(256), 0, 0, (const d2*)A, (d2*)Cm, n2); }, false, {}});
+    V.push_back({"copy U16 grid 4/CU", [&] { hipLaunchKernelGGL((v_copy_ilp<16, 0, 0>), dim3(cus * 4), dim3(256), 0, 0, (const d2*)A, (d2*)Cm, n2); }, false, {}});
+    V.push_back({"copy U8 nt-load", [&] { hipLaunchKernelGGL((v_copy_ilp<8, 1, 0>), dim3(cus * 8), dim3(256), 0, 0, (const d2*)A, (d2*)Cm, n2); }, false, {}});
+    V.push_back({"copy U8 nt-store", [&] { hipLaunchKernelGGL((v_copy_ilp<8, 0, 1>), dim3(cus * 8), dim3(256), 0, 0, (const d2*)A, (d2*)Cm, n2); }, false, {}});
+    V.push_back({"copy U8 one-shot grid", [&] { hipLaunchKernelGGL((v_copy_ilp<8, 0, 0>), dim3(n2 / 2048), dim3(256), 0, 0, (const d2*)A, (d2*)Cm, n2); }, false, {}});
+    V.push_back({"read-only 2GiB x2 (as 4GiB)", [&] { hipLaunchKernelGGL((v_read<8>), dim3(cus * 8), dim3(256), 0, 0, (const d2*)A, n2, (d2*)Cm); hipLaunchKernelGGL((v_read<8>), dim3(cus * 8), dim3(256), 0, 0, (const d2*)Cm, n2, (d2*)A); }, false, {}});
+    V.push_back({"write-only 2GiB x2 (as 4GiB)", [&] { hipLaunchKernelGGL((v_write<8>), dim3(cus * 8), dim3(256), 0, 0, (d2*)Cm, n2); hipLaunchKernelGGL((v_write<8>), dim3(cus * 8), dim3(256), 0, 0, (d2*)Cm, n2); }, false, {}});
+
+    for (auto& v : V) {  // warm + verify
+        CK(hipMemset(Cm, 0, sizeof(double) * n * n));
+        v.run();
+        CK(hipDeviceSynchronize());
+        if (v.verify) {
+            CK(hipMemset(bad, 0, 8));
+            hipLaunchKernelGGL(check, dim3((int64_t(n) * n + 255) / 256), dim3(256), 0, 0, A, Cm, n, bad);
+            unsigned long long h = 0;
+            CK(hipMemcpy(&h, bad, 8, hipMemcpyDeviceToHost));
+            printf("%-28s verify: %s\n", v.name.c_str(), h ? "FAIL" : "ok");
+        }
+    }
+    for (int r = 0; r < reps; ++r)
+        for (auto& v : V) {
+            CK(hipEventRecord(e0, 0));
+            v.run();
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            v.ms.push_back(ms);
+        }
+    printf("%-28s %9s %9s %9s %7s\n", "variant", "min ms", "med ms", "GB/s med", "%peak");
+    for (auto& v : V) {
+        std::sort(v.ms.begin(), v.ms.end());
+        float med = v.ms[v.ms.size() / 2];
+        printf("%-28s %9.4f %9.4f %9.1f %7.2f\n", v.name.c_str(), v.ms[0], med, bytes / med / 1e6,
+               bytes / med / 1e6 / 80.0);
+    }
+    return 0;
+}
