@@ -41,6 +41,23 @@ def grid_for(n: int):
     return pm, n // pm
 
 
+def measured_traffic(alg_bytes: int):
+    """HBM bytes per launch of this workload's dominant kernel, from the newest committed
+    rocprofv3 PMC pass of this same bench command (profiles/<tag>/pmc_tile_kernel.json,
+    written by tools/save_profiles.py with the gfx950 FETCH_SIZE correction).  PMC counters
+    cannot be read from inside this process, so they come from that separate pass."""
+    import glob
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_tile_kernel.json"))):
+        try:
+            d = json.load(open(p))
+        except Exception:
+            continue
+        if d.get("bytes_per_launch_alg") == alg_bytes and d.get("hbm_bytes_per_launch_corrected"):
+            best = (d["hbm_bytes_per_launch_corrected"], os.path.relpath(p, ROOT))
+    return best if best else (None, None)
+
+
 def cpu_baseline(n=16384, b=256, slab_cols=2048, target_s=10.0):
     """Oracle restatement of the reference tile loop on a 16384 x 2048 column slab of A
     (512 tiles of 256^2 fp64, 256 MiB in / 256 MiB out), repeated for ~target_s seconds."""
@@ -171,8 +188,10 @@ def main():
     per_launch = kbytes / max(kl, 1)
     avg_ms = kms / max(kl, 1)
     achieved = per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    traffic, traffic_src = measured_traffic(int(per_launch))
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+            "traffic_source": traffic_src,
             "kernel": f"tile_kernel<double> ({name} list)", "bytes_per_launch": int(per_launch),
             "avg_launch_ms": round(avg_ms, 4)}
 
