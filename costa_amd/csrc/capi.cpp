@@ -92,6 +92,13 @@ extern "C" {
 const char* costa_hip_last_error(void) { return g_last_error.c_str(); }
 int costa_hip_version(void) { return 100; }
 
+int costa_hip_device_count(int* count) {
+    return guarded([&] {
+        if (!count) throw costa::engine::error(COSTA_ERR_ARG, "null argument");
+        *count = costa::engine::device_count();
+    });
+}
+
 int costa_hip_block_cyclic_layout(costa_dtype_t dtype, int m, int n, int block_m, int block_n,
                                   int i, int j, int sub_m, int sub_n, int p_m, int p_n,
                                   char rank_grid_ordering, int rsrc, int csrc, void* ptr, int lld,

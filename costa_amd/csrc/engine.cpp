@@ -123,9 +123,14 @@ struct comm {
     }
 };
 
-comm* comm_self(int device) {
+int device_count() {
     int n = 0;
     HIP_CHECK(hipGetDeviceCount(&n));
+    return n;
+}
+
+comm* comm_self(int device) {
+    const int n = device_count();
     if (device < 0 || device >= n) throw error(COSTA_ERR_ARG, "costa: device index out of range");
     auto* c = new comm;
     c->device = device;

@@ -87,6 +87,7 @@ costa_tile_op_t make_tile_op(int n_rows, int n_cols, uint64_t src, int src_strid
 uint32_t scale_kind(costa_dtype_t dtype, const scal& s, bool copy_mode, bool conj);
 
 // ---- executor (engine.cpp / tile_kernels.hip) ----
+int device_count();
 struct comm;
 struct comm* comm_self(int device);
 struct comm* comm_create(const unsigned char* id, int nranks, int rank, int device);

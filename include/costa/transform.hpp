@@ -65,6 +65,11 @@ struct transformer {
         transpose.push_back(trans);
         schedule(f, t);
     }
+#ifdef MPI_VERSION
+    // reference constructor: transformer(MPI_Comm) (transformer.hpp:24-27)
+    explicit transformer(MPI_Comm c);
+#endif
+
     void transform() {
         if (alpha.size() != beta.size() || alpha.size() != transpose.size())
             throw std::runtime_error("costa::transformer: inconsistent scheduling");
@@ -85,5 +90,79 @@ struct transformer {
         transpose.clear();
     }
 };
+
+#ifdef MPI_VERSION
+// ---- MPI_Comm signatures of the reference (header-only: works with the application's MPI).
+// Every MPI communicator gets ONE costa communicator (RCCL over the same ranks, one GPU per
+// rank: node-local rank modulo the visible devices), cached as an MPI attribute and
+// destroyed with the MPI communicator.  Collective over `comm` on first use.
+namespace detail {
+inline int mpi_comm_delete(MPI_Comm, int, void* attr, void*) {
+    costa_hip_comm_destroy(static_cast<costa_comm_t>(attr));
+    return MPI_SUCCESS;
+}
+inline int& mpi_keyval() {
+    static int k = MPI_KEYVAL_INVALID;
+    return k;
+}
+}  // namespace detail
+
+inline costa_comm_t comm_from_mpi(MPI_Comm comm, int device = -1) {
+    int& key = detail::mpi_keyval();
+    if (key == MPI_KEYVAL_INVALID)
+        MPI_Comm_create_keyval(MPI_COMM_NULL_COPY_FN, detail::mpi_comm_delete, &key, nullptr);
+    void* val = nullptr;
+    int flag = 0;
+    MPI_Comm_get_attr(comm, key, &val, &flag);
+    if (flag) return static_cast<costa_comm_t>(val);
+    int rank = 0, size = 1;
+    MPI_Comm_rank(comm, &rank);
+    MPI_Comm_size(comm, &size);
+    if (device < 0) {
+        MPI_Comm node;
+        MPI_Comm_split_type(comm, MPI_COMM_TYPE_SHARED, rank, MPI_INFO_NULL, &node);
+        int local = 0, ndev = 1;
+        MPI_Comm_rank(node, &local);
+        MPI_Comm_free(&node);
+        if (costa_hip_device_count(&ndev) != COSTA_OK || ndev < 1)
+            throw hip_error(COSTA_ERR_HIP, costa_hip_last_error());
+        device = local % ndev;
+    }
+    unsigned char id[128] = {0};
+    int rc = COSTA_OK;
+    if (size > 1 && rank == 0) rc = costa_hip_comm_unique_id(id);
+    if (size > 1) {
+        MPI_Bcast(&rc, 1, MPI_INT, 0, comm);
+        if (rc != COSTA_OK) throw hip_error(rc, "costa: RCCL unique id failed on rank 0");
+        MPI_Bcast(id, 128, MPI_UNSIGNED_CHAR, 0, comm);
+    }
+    costa_comm_t c = nullptr;
+    rc = costa_hip_comm_create(id, size, rank, device, &c);
+    if (rc != COSTA_OK) throw hip_error(rc, costa_hip_last_error());
+    MPI_Comm_set_attr(comm, key, c);
+    return c;
+}
+
+template <typename T>
+transformer<T>::transformer(MPI_Comm c) : comm(comm_from_mpi(c)) {}
+
+template <typename T>
+void transform(grid_layout<T>& A, grid_layout<T>& C, MPI_Comm comm) {
+    transform<T>(A, C, comm_from_mpi(comm));
+}
+template <typename T>
+void transform(grid_layout<T>& A, grid_layout<T>& C, char trans, T alpha, T beta, MPI_Comm comm) {
+    transform<T>(A, C, trans, alpha, beta, comm_from_mpi(comm));
+}
+template <typename T>
+void transform(std::vector<layout_ref<T>>& A, std::vector<layout_ref<T>>& C, MPI_Comm comm) {
+    transform<T>(A, C, comm_from_mpi(comm));
+}
+template <typename T>
+void transform(std::vector<layout_ref<T>>& A, std::vector<layout_ref<T>>& C, const char* trans,
+               const T* alpha, const T* beta, MPI_Comm comm) {
+    transform<T>(A, C, trans, alpha, beta, comm_from_mpi(comm));
+}
+#endif  // MPI_VERSION
 
 }  // namespace costa

@@ -105,6 +105,7 @@ typedef struct {
 /* ---- library ---- */
 const char* costa_hip_last_error(void);
 int costa_hip_version(void); /* major*10000 + minor*100 + patch */
+int costa_hip_device_count(int* count); /* visible GPUs (COSTA_ERR_HIP without a GPU) */
 
 /* ---- layouts (pointers may be host or device memory; never dereferenced
  *      until a transform runs) ---- */
