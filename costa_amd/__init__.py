@@ -29,7 +29,7 @@ import numpy as np
 __all__ = [
     "CostaError", "lib", "FLOAT", "DOUBLE", "CFLOAT", "CDOUBLE", "INT32", "dtype_code",
     "np_dtype", "Layout", "block_cyclic_layout", "custom_layout", "Comm", "transform",
-    "transform_batch", "transformer", "copy_and_transform", "execute_tiles", "TileOp",
+    "transform_batch", "transform_async", "transform_batch_async", "synchronize", "transformer", "copy_and_transform", "execute_tiles", "TileOp",
     "plan_export", "set_profiling", "get_stats", "release_caches", "TILE_OP_DTYPE",
 ]
 
@@ -135,6 +135,11 @@ def lib():
         "costa_hip_transform": (i, [vp, vp, c, vp, vp, vp]),
         "costa_hip_transform_batch": (i, [i, C.POINTER(vp), C.POINTER(vp), C.c_char_p, vp, vp,
                                           vp]),
+        "costa_hip_transform_async": (i, [vp, vp, c, vp, vp, vp, vp]),
+        "costa_hip_transform_batch_async": (i, [i, C.POINTER(vp), C.POINTER(vp), C.c_char_p, vp,
+                                                vp, vp, vp]),
+        "costa_hip_synchronize": (i, [vp]),
+        "costa_hip_device_count": (i, [C.POINTER(i)]),
         "costa_hip_copy_and_transform": (i, [i, i, i, vp, i, i, vp, i, i, i, i, vp, vp]),
         "costa_hip_execute_tiles": (i, [i, C.POINTER(TileOp), i64, vp, vp, vp, i, i]),
         "costa_hip_plan_export": (i, [i, C.POINTER(vp), C.POINTER(vp), C.c_char_p, vp, vp, i, i,
@@ -332,6 +337,33 @@ def transform_batch(As: Sequence[Layout], Cs: Sequence[Layout], comm: Comm,
     ab = b"".join(_scalar_bytes(code, x) for x in alpha)
     bb = b"".join(_scalar_bytes(code, x) for x in beta)
     _check(lib().costa_hip_transform_batch(n, a, c, "".join(trans).encode(), ab, bb, comm.handle))
+
+
+def transform_async(A: Layout, Cl: Layout, comm: Comm, trans: str = "N", alpha=1, beta=0,
+                    stream=None):
+    """Stream-ordered transform (device-resident layouts).  `stream`: a torch stream, a raw
+    hipStream_t address, or None; it waits for the result.  See costa_hip_transform_async."""
+    transform_batch_async([A], [Cl], comm, [trans], [alpha], [beta], stream)
+
+
+def transform_batch_async(As, Cs, comm: Comm, trans=None, alpha=None, beta=None, stream=None):
+    n = len(As)
+    code = As[0].dtype
+    trans = list(trans) if trans is not None else ["N"] * n
+    alpha = list(alpha) if alpha is not None else [1] * n
+    beta = list(beta) if beta is not None else [0] * n
+    a = (C.c_void_p * n)(*[x.handle.value for x in As])
+    c = (C.c_void_p * n)(*[x.handle.value for x in Cs])
+    ab = b"".join(_scalar_bytes(code, x) for x in alpha)
+    bb = b"".join(_scalar_bytes(code, x) for x in beta)
+    s = getattr(stream, "cuda_stream", stream) or 0
+    _check(lib().costa_hip_transform_batch_async(n, a, c, "".join(trans).encode(), ab, bb,
+                                                 comm.handle, C.c_void_p(s)))
+
+
+def synchronize(comm: Comm):
+    """Wait for every transform queued on the communicator's device."""
+    _check(lib().costa_hip_synchronize(comm.handle))
 
 
 class transformer:

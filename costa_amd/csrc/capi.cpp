@@ -206,6 +206,28 @@ int costa_hip_transform_batch(int n, const costa_layout_t* A, const costa_layout
     });
 }
 
+int costa_hip_transform_async(costa_layout_t A, costa_layout_t C, char trans, const void* alpha,
+                              const void* beta, costa_comm_t comm, void* stream) {
+    return costa_hip_transform_batch_async(1, &A, &C, &trans, alpha, beta, comm, stream);
+}
+
+int costa_hip_transform_batch_async(int n, const costa_layout_t* A, const costa_layout_t* C,
+                                    const char* trans, const void* alpha, const void* beta,
+                                    costa_comm_t comm, void* stream) {
+    return guarded([&] {
+        if (!comm || !alpha || !beta) throw costa::engine::error(COSTA_ERR_ARG, "null argument");
+        auto jobs = make_jobs(n, A, C, trans, alpha, beta);
+        costa::engine::transform(jobs, comm->c, stream, true);
+    });
+}
+
+int costa_hip_synchronize(costa_comm_t comm) {
+    return guarded([&] {
+        if (!comm) throw costa::engine::error(COSTA_ERR_ARG, "null communicator");
+        costa::engine::synchronize(comm->c);
+    });
+}
+
 int costa_hip_copy_and_transform(costa_dtype_t dtype, int n_rows, int n_cols, const void* src,
                                  int src_stride, int src_col_major, void* dst, int dst_stride,
                                  int dst_col_major, int transpose, int conjugate,
@@ -277,6 +299,7 @@ int costa_hip_set_profiling(int on) {
 int costa_hip_get_stats(costa_stats_t* out, int reset) {
     return guarded([&] {
         if (!out) throw costa::engine::error(COSTA_ERR_ARG, "null argument");
+        costa::engine::resolve_pending();  // timings of asynchronous transforms
         *out = costa::engine::stats();
         if (reset) costa::engine::stats() = costa_stats_t{};
     });

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <deque>
 #include <list>
 #include <map>
 #include <mutex>
@@ -76,28 +77,39 @@ struct dbuf {
 
 // ---------------------------------------------------------------- per-device context
 struct device_ctx {
+    struct timed {
+        int phase;
+        hipEvent_t a, b;
+    };
     int device = 0;
     hipStream_t main = nullptr, aux = nullptr;
-    hipEvent_t ev_ready = nullptr, ev_local = nullptr;
-    hipEvent_t t[8] = {};
+    hipEvent_t ev_ready = nullptr, ev_local = nullptr, ev_user = nullptr, ev_done = nullptr;
+    std::vector<hipEvent_t> free_events;  // timing events ready for reuse
+    std::deque<timed> pending;            // recorded phase brackets not yet read
     dbuf send, recv;
     explicit device_ctx(int dev) : device(dev) {
         HIP_CHECK(hipSetDevice(dev));
         // blocking streams: they order after work on the legacy default stream
         HIP_CHECK(hipStreamCreate(&main));
         HIP_CHECK(hipStreamCreate(&aux));
-        HIP_CHECK(hipEventCreateWithFlags(&ev_ready, hipEventDisableTiming));
-        HIP_CHECK(hipEventCreateWithFlags(&ev_local, hipEventDisableTiming));
-        for (auto& e : t) HIP_CHECK(hipEventCreate(&e));
+        for (hipEvent_t* e : {&ev_ready, &ev_local, &ev_user, &ev_done})
+            HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
     ~device_ctx() {
         (void)hipSetDevice(device);
-        for (auto& e : t) (void)hipEventDestroy(e);
-        (void)hipEventDestroy(ev_ready);
-        (void)hipEventDestroy(ev_local);
+        (void)hipStreamSynchronize(main);
+        (void)hipStreamSynchronize(aux);
+        for (auto& t : pending) {
+            (void)hipEventDestroy(t.a);
+            (void)hipEventDestroy(t.b);
+        }
+        for (auto e : free_events) (void)hipEventDestroy(e);
+        for (hipEvent_t e : {ev_ready, ev_local, ev_user, ev_done}) (void)hipEventDestroy(e);
         (void)hipStreamDestroy(main);
         (void)hipStreamDestroy(aux);
     }
+    hipEvent_t take_event();
+    void resolve(size_t max_n = size_t(-1));  // read finished brackets into the statistics
 };
 
 namespace {
@@ -466,16 +478,13 @@ void upload_scalars(cached_plan& cp, const std::vector<job>& jobs, hipStream_t s
         std::memcpy(&host[(2 * t + 1) * E], jobs[t].s.beta.data(), E);
     }
     if (host != cp.scal_host || !cp.d_scal.p) {
+        // stream-ordered behind earlier (possibly asynchronous) transforms that still read the
+        // old values; pageable source -> the runtime stages it before returning
         cp.d_scal.reserve(host.size());
-        HIP_CHECK(hipMemcpy(cp.d_scal.p, host.data(), host.size(), hipMemcpyHostToDevice));
         cp.scal_host = host;
+        HIP_CHECK(hipMemcpyAsync(cp.d_scal.p, cp.scal_host.data(), host.size(),
+                                 hipMemcpyHostToDevice, s));
     }
-}
-
-float elapsed(hipEvent_t a, hipEvent_t b) {
-    float ms = 0.f;
-    HIP_CHECK(hipEventElapsedTime(&ms, a, b));
-    return ms;
 }
 
 }  // namespace
@@ -487,57 +496,146 @@ void release_caches() {
 }
 
 // ---------------------------------------------------------------- transform
-void transform(const std::vector<job>& jobs, comm* c) {
+// Phases are bracketed by pooled event pairs on the stream they run on; the pairs are
+// resolved (elapsed time added to the statistics) at the next synchronisation point, so
+// asynchronous transforms are timed too.
+namespace {
+enum phase { PH_LOCAL, PH_PACK, PH_EXCHANGE, PH_UNPACK, PH_H2D, PH_D2H };
+
+struct phase_timer {
+    device_ctx& dc;
+    bool on;
+    int ph = 0;
+    hipEvent_t a = nullptr;
+    hipStream_t s = nullptr;
+    phase_timer(device_ctx& d, bool prof) : dc(d), on(prof) {}
+    void start(int p, hipStream_t st) {
+        if (!on) return;
+        ph = p;
+        s = st;
+        a = dc.take_event();
+        HIP_CHECK(hipEventRecord(a, s));
+    }
+    void stop() {
+        if (!on || !a) return;
+        hipEvent_t b = dc.take_event();
+        HIP_CHECK(hipEventRecord(b, s));
+        dc.pending.push_back({ph, a, b});
+        a = nullptr;
+        if (dc.pending.size() > 1024) dc.resolve(64);
+    }
+};
+}  // namespace
+
+void device_ctx::resolve(size_t max_n) {
+    size_t n = 0;
+    while (!pending.empty() && n < max_n) {
+        timed t = pending.front();
+        pending.pop_front();
+        float ms = 0.f;
+        HIP_CHECK(hipEventSynchronize(t.b));
+        HIP_CHECK(hipEventElapsedTime(&ms, t.a, t.b));
+        double* acc[] = {&g_stats.local_ms, &g_stats.pack_ms, &g_stats.exchange_ms,
+                         &g_stats.unpack_ms, &g_stats.h2d_ms, &g_stats.d2h_ms};
+        *acc[t.phase] += ms;
+        free_events.push_back(t.a);
+        free_events.push_back(t.b);
+        ++n;
+    }
+}
+
+hipEvent_t device_ctx::take_event() {
+    if (free_events.empty()) {
+        hipEvent_t e;
+        HIP_CHECK(hipEventCreate(&e));
+        return e;
+    }
+    hipEvent_t e = free_events.back();
+    free_events.pop_back();
+    return e;
+}
+
+void resolve_pending() {
+    std::lock_guard<std::recursive_mutex> lk(g_mutex);
+    for (auto& kv : ctx_map()) {
+        HIP_CHECK(hipSetDevice(kv.first));
+        kv.second->resolve();
+    }
+}
+
+void synchronize(comm* c) {
+    std::lock_guard<std::recursive_mutex> lk(g_mutex);
+    if (!c) throw error(COSTA_ERR_ARG, "costa: null communicator");
+    device_ctx& dc = ctx(c->device);
+    HIP_CHECK(hipStreamSynchronize(dc.main));
+    HIP_CHECK(hipStreamSynchronize(dc.aux));
+    dc.resolve();
+}
+
+void transform(const std::vector<job>& jobs, comm* c, void* user_stream, bool async) {
     std::lock_guard<std::recursive_mutex> lk(g_mutex);
     if (!c) throw error(COSTA_ERR_ARG, "costa: null communicator");
     device_ctx& dc = ctx(c->device);
     cached_plan& cp = *get_plan(jobs, c, dc);
     const plan& p = *cp.p;
     const size_t E = dtype_size(p.dtype);
+    if (async && cp.staged)
+        throw error(COSTA_ERR_ARG,
+                    "costa: asynchronous transforms need device-resident layouts (host data is "
+                    "staged synchronously)");
+    hipStream_t user = static_cast<hipStream_t>(user_stream);
+    // everything runs on the context's streams, in call order (they own the workspaces);
+    // a caller stream is joined at entry and made to wait for the result at exit
+    if (user) {
+        HIP_CHECK(hipEventRecord(dc.ev_user, user));
+        HIP_CHECK(hipStreamWaitEvent(dc.main, dc.ev_user, 0));
+    }
     upload_scalars(cp, jobs, dc.main);
-    const bool prof = g_profiling;
+    phase_timer tm(dc, g_profiling);
 
     // H2D of host-resident data
     if (cp.staged) {
-        if (prof) HIP_CHECK(hipEventRecord(dc.t[6], dc.main));
+        tm.start(PH_H2D, dc.main);
         for (const auto& r : cp.a_ranges)
             HIP_CHECK(hipMemcpyAsync(static_cast<char*>(cp.stage.p) + r.dev_off,
                                      reinterpret_cast<void*>(r.lo), r.hi - r.lo,
                                      hipMemcpyHostToDevice, dc.main));
-        if (prof) HIP_CHECK(hipEventRecord(dc.t[7], dc.main));
+        tm.stop();
     }
-    HIP_CHECK(hipEventRecord(dc.ev_ready, dc.main));
 
     const bool exchange = c->size > 1 && (p.send_elems > 0 || p.recv_elems > 0);
-    // LOCAL on the aux stream (overlaps pack + exchange)
-    const bool local_on_aux = exchange;
-    hipStream_t ls = local_on_aux ? dc.aux : dc.main;
-    if (local_on_aux) HIP_CHECK(hipStreamWaitEvent(dc.aux, dc.ev_ready, 0));
+    // LOCAL on the aux stream when there is an exchange to overlap, else on main
+    hipStream_t ls = exchange ? dc.aux : dc.main;
+    if (exchange) {
+        HIP_CHECK(hipEventRecord(dc.ev_ready, dc.main));
+        HIP_CHECK(hipStreamWaitEvent(dc.aux, dc.ev_ready, 0));
+    }
     if (cp.n_local) {
-        if (prof) HIP_CHECK(hipEventRecord(dc.t[0], ls));
+        tm.start(PH_LOCAL, ls);
         launch_tiles(p.dtype,
                      {static_cast<const costa_tile_op_t*>(cp.d_local.p),
-                      static_cast<const uint64_t*>(cp.w_local.p), cp.n_local, cp.l_local, nullptr, nullptr,
-                      cp.d_scal.p, cp.tr_local},
+                      static_cast<const uint64_t*>(cp.w_local.p), cp.n_local, cp.l_local, nullptr,
+                      nullptr, cp.d_scal.p, cp.tr_local},
                      ls);
-        if (prof) HIP_CHECK(hipEventRecord(dc.t[1], ls));
+        tm.stop();
     }
-    if (local_on_aux) HIP_CHECK(hipEventRecord(dc.ev_local, dc.aux));
 
     if (exchange) {
+        HIP_CHECK(hipEventRecord(dc.ev_local, dc.aux));
         dc.send.reserve(size_t(p.send_elems) * E + 256);
         dc.recv.reserve(size_t(p.recv_elems) * E + 256);
         char* sb = static_cast<char*>(dc.send.p);
         char* rb = static_cast<char*>(dc.recv.p);
         if (cp.n_pack) {
-            if (prof) HIP_CHECK(hipEventRecord(dc.t[2], dc.main));
+            tm.start(PH_PACK, dc.main);
             launch_tiles(p.dtype,
                          {static_cast<const costa_tile_op_t*>(cp.d_pack.p),
-                          static_cast<const uint64_t*>(cp.w_pack.p), cp.n_pack, cp.l_pack, nullptr, sb,
-                          cp.d_scal.p, false},
+                          static_cast<const uint64_t*>(cp.w_pack.p), cp.n_pack, cp.l_pack, nullptr,
+                          sb, cp.d_scal.p, false},
                          dc.main);
-            if (prof) HIP_CHECK(hipEventRecord(dc.t[3], dc.main));
+            tm.stop();
         }
+        tm.start(PH_EXCHANGE, dc.main);
         NCCL_CHECK(ncclGroupStart());
         for (int r = 0; r < c->size; ++r) {
             if (p.send_counts[size_t(r)] > 0)
@@ -550,26 +648,28 @@ void transform(const std::vector<job>& jobs, comm* c) {
                                     dc.main));
         }
         NCCL_CHECK(ncclGroupEnd());
-        if (prof) HIP_CHECK(hipEventRecord(dc.t[4], dc.main));
-        if (cp.n_unpack)
+        tm.stop();
+        if (cp.n_unpack) {
+            tm.start(PH_UNPACK, dc.main);
             launch_tiles(p.dtype,
                          {static_cast<const costa_tile_op_t*>(cp.d_unpack.p),
-                          static_cast<const uint64_t*>(cp.w_unpack.p), cp.n_unpack, cp.l_unpack, rb, nullptr,
-                          cp.d_scal.p, cp.tr_unpack},
+                          static_cast<const uint64_t*>(cp.w_unpack.p), cp.n_unpack, cp.l_unpack,
+                          rb, nullptr, cp.d_scal.p, cp.tr_unpack},
                          dc.main);
-        if (prof) HIP_CHECK(hipEventRecord(dc.t[5], dc.main));
+            tm.stop();
+        }
         HIP_CHECK(hipStreamWaitEvent(dc.main, dc.ev_local, 0));
     }
 
     // D2H of the target data
     if (cp.staged) {
+        tm.start(PH_D2H, dc.main);
         for (const auto& r : cp.c_ranges)
             HIP_CHECK(hipMemcpyAsync(reinterpret_cast<void*>(r.lo),
                                      static_cast<char*>(cp.stage.p) + r.dev_off, r.hi - r.lo,
                                      hipMemcpyDeviceToHost, dc.main));
+        tm.stop();
     }
-    HIP_CHECK(hipStreamSynchronize(dc.main));
-    if (local_on_aux) HIP_CHECK(hipStreamSynchronize(dc.aux));
 
     g_stats.transforms++;
     if (cp.n_local) {
@@ -584,16 +684,16 @@ void transform(const std::vector<job>& jobs, comm* c) {
         g_stats.unpack_launches++;
         g_stats.unpack_bytes += p.unpack_bytes;
     }
-    if (prof) {
-        if (cp.n_local) g_stats.local_ms += elapsed(dc.t[0], dc.t[1]);
-        if (exchange) {
-            if (cp.n_pack) g_stats.pack_ms += elapsed(dc.t[2], dc.t[3]);
-            g_stats.exchange_ms += elapsed(cp.n_pack ? dc.t[3] : dc.ev_ready, dc.t[4]);
-            g_stats.unpack_ms += elapsed(dc.t[4], dc.t[5]);
-        }
-        if (cp.staged) g_stats.h2d_ms += elapsed(dc.t[6], dc.t[7]);
+
+    if (async) {
+        HIP_CHECK(hipEventRecord(dc.ev_done, dc.main));
+        if (user) HIP_CHECK(hipStreamWaitEvent(user, dc.ev_done, 0));
+        return;
     }
+    HIP_CHECK(hipStreamSynchronize(dc.main));
+    dc.resolve();
 }
+
 
 // ---------------------------------------------------------------- direct tile calls
 void execute_tiles(costa_dtype_t dtype, const costa_tile_op_t* ops, int64_t n,

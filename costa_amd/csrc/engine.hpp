@@ -96,7 +96,12 @@ int comm_rank(const struct comm* c);
 int comm_size(const struct comm* c);
 void comm_destroy(struct comm* c);
 
-void transform(const std::vector<job>& jobs, struct comm* c);
+// blocking (default) or stream-ordered (async: device-resident layouts only; `user_stream`, a
+// hipStream_t or null, is joined at entry and waits for the result)
+void transform(const std::vector<job>& jobs, struct comm* c, void* user_stream = nullptr,
+               bool async = false);
+void synchronize(struct comm* c);  // wait for every queued transform of c's device
+void resolve_pending();            // fold finished timing brackets into the statistics
 
 void copy_and_transform(costa_dtype_t dtype, int n_rows, int n_cols, const void* src,
                         int src_stride, bool src_cm, void* dst, int dst_stride, bool dst_cm,

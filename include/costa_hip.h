@@ -146,6 +146,18 @@ int costa_hip_transform_batch(int n, const costa_layout_t* A, const costa_layout
                               const char* trans, const void* alpha, const void* beta,
                               costa_comm_t comm);
 
+/* ---- stream-ordered variants (MI355X-native; no reference counterpart) ----
+ * Enqueue the transform and return.  Layouts must be device-resident.  `stream` (a hipStream_t,
+ * may be NULL) is joined at entry and made to wait for the result, so work queued on it after
+ * this call sees sub(C) complete.  Transforms of one process run in call order.
+ * costa_hip_synchronize waits for everything queued on the communicator's device. */
+int costa_hip_transform_async(costa_layout_t A, costa_layout_t C, char trans, const void* alpha,
+                              const void* beta, costa_comm_t comm, void* stream);
+int costa_hip_transform_batch_async(int n, const costa_layout_t* A, const costa_layout_t* C,
+                                    const char* trans, const void* alpha, const void* beta,
+                                    costa_comm_t comm, void* stream);
+int costa_hip_synchronize(costa_comm_t comm);
+
 /* ---- direct tile entry points (device pointers) ---- */
 int costa_hip_copy_and_transform(costa_dtype_t dtype, int n_rows, int n_cols, const void* src,
                                  int src_stride, int src_col_major, void* dst, int dst_stride,

@@ -229,6 +229,32 @@ def test_full_size_axpby_checksum(gpu):
     assert got.tobytes() == np.ascontiguousarray(expected).tobytes()
 
 
+def test_async_stream_ordered(gpu):
+    """stream-ordered transforms: queued back to back with changing scalars on the same
+    handles, consumed by torch on the same stream without a host sync"""
+    n, b = 1024, 128
+    A = torch.arange(n * n, dtype=torch.float64, device="cuda") % 97 - 48
+    Cm = torch.full((n * n,), float("nan"), dtype=torch.float64, device="cuda")
+    LA = gpu.block_cyclic_layout(n, n, b, b, 1, 1, n, n, 1, 1, "R", 0, 0, A.data_ptr(), n, "C", 0)
+    LC = gpu.block_cyclic_layout(n, n, b, b, 1, 1, n, n, 1, 1, "R", 0, 0, Cm.data_ptr(), n, "C", 0)
+    comm = gpu.Comm.self(0)
+    s = torch.cuda.current_stream()
+    gpu.transform_async(LA, LC, comm, "T", 2.0, 0.0, stream=s)   # C = 2 A^T   (C = NaN not read)
+    gpu.transform_async(LA, LC, comm, "T", 3.0, 1.0, stream=s)   # C = C + 3 A^T = 5 A^T
+    gpu.transform_async(LA, LC, comm, "T", -1.0, 0.5, stream=s)  # C = C/2 - A^T = 1.5 A^T
+    got = Cm.view(n, n).clone()  # queued on s after the transforms
+    assert torch.equal(got, 1.5 * A.view(n, n).t())
+
+
+def test_async_rejects_host_layouts(gpu):
+    a = np.zeros(64 * 64)
+    c = np.zeros(64 * 64)
+    LA = gpu.block_cyclic_layout(64, 64, 32, 32, 1, 1, 64, 64, 1, 1, "R", 0, 0, a, 64, "C", 0)
+    LC = gpu.block_cyclic_layout(64, 64, 32, 32, 1, 1, 64, 64, 1, 1, "R", 0, 0, c, 64, "C", 0)
+    with pytest.raises(gpu.CostaError, match="device-resident"):
+        gpu.transform_async(LA, LC, gpu.Comm.self(0), "T", 1.0, 0.0)
+
+
 def test_plan_cache_reuse(gpu):
     """the second identical call hits the plan cache and gives the same result"""
     case = [c for c in all_cases() if c.name == "block_cyclic"][0]

@@ -242,6 +242,55 @@ __global__ __launch_bounds__(NT) void v_gen(const op_t* ops, const uint64_t* wor
 }
 
 // ----------------------------------------------------------------------------------
+// V5: 128x128 / 1024 threads, row stores: one wave instruction writes a whole 1 KiB row
+// segment (128 s values of one f): lane l holds (2l, f), (2l+1, f) from two 8-byte LDS reads.
+// PAD selects the LDS row pitch in doubles (BF + PAD).
+template <int PAD, int NTL>
+__global__ __launch_bounds__(1024) void v_rowstore(const op_t* ops, const uint64_t* work) {
+    constexpr int BF = 128, BS = 128, NT = 1024, P = BF + PAD;
+    __shared__ __attribute__((aligned(16))) double tile[BS * P];
+    const uint64_t w = work[blockIdx.x];
+    const op_t op = ops[w >> 32];
+    const uint32_t sub = uint32_t(w);
+    const int nbf = op.nf / BF;
+    const int f0 = int(sub % nbf) * BF, s0 = int(sub / nbf) * BS;
+    const double* src = reinterpret_cast<const double*>(op.src) + int64_t(s0) * op.lds + f0;
+    double* dst = reinterpret_cast<double*>(op.dst) + int64_t(f0) * op.ldd + s0;
+    constexpr int LPC = BF / 2, CPP = NT / LPC, PL = BS / CPP;
+    const int lf = (threadIdx.x % LPC) * 2, c0 = threadIdx.x / LPC;
+    d2 x[PL];
+#pragma unroll
+    for (int k = 0; k < PL; ++k) {
+        const d2* p = reinterpret_cast<const d2*>(src + int64_t(c0 + CPP * k) * op.lds + lf);
+        x[k] = NTL ? __builtin_nontemporal_load(p) : *p;
+    }
+#pragma unroll
+    for (int k = 0; k < PL; ++k) {
+        if (PAD % 2 == 0) {
+            *reinterpret_cast<d2*>(&tile[(c0 + CPP * k) * P + lf]) = x[k];
+        } else {
+            tile[(c0 + CPP * k) * P + lf] = x[k].x;
+            tile[(c0 + CPP * k) * P + lf + 1] = x[k].y;
+        }
+    }
+    __syncthreads();
+    const int lane = threadIdx.x % 64, wave = threadIdx.x / 64;
+    constexpr int PS = BF / (NT / 64);  // rows per wave
+    d2 y[PS];
+#pragma unroll
+    for (int k = 0; k < PS; ++k) {
+        const int f = wave + 16 * k;
+        y[k].x = tile[(2 * lane) * P + f];
+        y[k].y = tile[(2 * lane + 1) * P + f];
+    }
+#pragma unroll
+    for (int k = 0; k < PS; ++k) {
+        const int f = wave + 16 * k;
+        *reinterpret_cast<d2*>(dst + int64_t(f) * op.ldd + 2 * lane) = y[k];
+    }
+}
+
+// ----------------------------------------------------------------------------------
 // V4: v_gen as a persistent loop: the next sub-tile's loads are issued before the current
 // sub-tile's LDS read-out and stores (register double buffering).
 template <int BF, int BS, int NT>
@@ -441,6 +490,10 @@ int main(int argc, char** argv) {
     V.push_back({"gen 64x128 t512", [&] { hipLaunchKernelGGL((v_gen<64, 128, 512, 0>), dim3(g64x128.second), dim3(512), 0, 0, d_ops, g64x128.first); }, true, {}});
     V.push_back({"gen 128x128 t1024", [&] { hipLaunchKernelGGL((v_gen<128, 128, 1024, 0>), dim3(g128x128.second), dim3(1024), 0, 0, d_ops, g128x128.first); }, true, {}});
     V.push_back({"gen 128x128 t1024 nt-load", [&] { hipLaunchKernelGGL((v_gen<128, 128, 1024, 1>), dim3(g128x128.second), dim3(1024), 0, 0, d_ops, g128x128.first); }, true, {}});
+    V.push_back({"rowstore 128x128 pad2", [&] { hipLaunchKernelGGL((v_rowstore<2, 0>), dim3(g128x128.second), dim3(1024), 0, 0, d_ops, g128x128.first); }, true, {}});
+    V.push_back({"rowstore 128x128 pad1", [&] { hipLaunchKernelGGL((v_rowstore<1, 0>), dim3(g128x128.second), dim3(1024), 0, 0, d_ops, g128x128.first); }, true, {}});
+    V.push_back({"rowstore 128x128 pad1 nt-load", [&] { hipLaunchKernelGGL((v_rowstore<1, 1>), dim3(g128x128.second), dim3(1024), 0, 0, d_ops, g128x128.first); }, true, {}});
+    V.push_back({"rowstore 128x128 pad3", [&] { hipLaunchKernelGGL((v_rowstore<3, 0>), dim3(g128x128.second), dim3(1024), 0, 0, d_ops, g128x128.first); }, true, {}});
     for (int k : {1, 2}) {
         V.push_back({"gpersist 128x128 t1024 x" + std::to_string(k), [&, k] { hipLaunchKernelGGL((v_gen_persist<128, 128, 1024>), dim3(cus * k), dim3(1024), 0, 0, d_ops, g128x128.first, g128x128.second); }, true, {}});
     }
