@@ -89,6 +89,56 @@ def cpu_baseline(n=16384, b=256, slab_cols=2048, target_s=10.0):
                       f"oracle_transform_tiles, OpenMP {threads} threads, verified={ok}"}
 
 
+def cfg5_workload(costa, torch, rank, world, op):
+    """BASELINE configs[4]: fp32 16384^2 custom_layout; A tile edges uniform in
+    [8, 96] (seeds 0xC5A1 rows / 0xC5A2 cols), C edges uniform in [16, 160] (0xC5A3 / 0xC5A4),
+    owners uniform over the ranks (0xC5A5 for A, 0xC5A6 for C); every owned block is its own
+    column-major buffer (ld = rows) in a 256-byte-aligned arena.  numpy PCG64 streams are used
+    for the draws.  op 'N' alpha=1 beta=0, or the 'T' variant alpha=-0.5 beta=2."""
+    import numpy as np
+    n = 16384
+
+    def splits(seed, lo, hi):
+        r = np.random.default_rng(seed)
+        s = [0]
+        while s[-1] < n:
+            s.append(min(n, s[-1] + int(r.integers(lo, hi + 1))))
+        return s
+
+    ars, acs = splits(0xC5A1, 8, 96), splits(0xC5A2, 8, 96)
+    crs, ccs = splits(0xC5A3, 16, 160), splits(0xC5A4, 16, 160)
+    aown = np.random.default_rng(0xC5A5).integers(0, world, (len(ars) - 1, len(acs) - 1))
+    cown = np.random.default_rng(0xC5A6).integers(0, world, (len(crs) - 1, len(ccs) - 1))
+
+    def arena(rs, cs, own):
+        blocks, off = [], 0
+        for i in range(len(rs) - 1):
+            for j in range(len(cs) - 1):
+                if own[i, j] != rank:
+                    continue
+                rows, cols = rs[i + 1] - rs[i], cs[j + 1] - cs[j]
+                blocks.append((off, rows, i, j))
+                off += (rows * cols + 63) // 64 * 64  # 256-byte aligned blocks
+        return blocks, max(off, 64)
+
+    ab, an = arena(ars, acs, aown)
+    cb, cn = arena(crs, ccs, cown)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(99 + rank)
+    A = torch.rand(an, dtype=torch.float32, device="cuda", generator=g)
+    C = torch.rand(cn, dtype=torch.float32, device="cuda", generator=g)
+    pa, pc = A.data_ptr(), C.data_ptr()
+    LA = costa.custom_layout(len(ars) - 1, len(acs) - 1, ars, acs, aown,
+                             [(pa + 4 * o, r, i, j) for o, r, i, j in ab], "C", costa.FLOAT)
+    LC = costa.custom_layout(len(crs) - 1, len(ccs) - 1, crs, ccs, cown,
+                             [(pc + 4 * o, r, i, j) for o, r, i, j in cb], "C", costa.FLOAT)
+    al, be = (1.0, 0.0) if op == "N" else (-0.5, 2.0)
+    wl = (f"costa::custom_layout fp32 16384x16384, irregular tiles (A edges 8-96: "
+          f"{len(ars) - 1}x{len(acs) - 1} blocks, C edges 16-160: {len(crs) - 1}x{len(ccs) - 1}), "
+          f"owners uniform over {world} rank(s), op {op} (BASELINE configs[4])")
+    return LA, LC, A, C, op, al, be, wl
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -96,6 +146,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--edge", type=int, default=16384, help="local matrix edge per rank")
     ap.add_argument("--block", type=int, default=256)
+    ap.add_argument("--workload", choices=["pxtran", "cfg5"], default="pxtran",
+                    help="pxtran: BASELINE configs[1] (default, the headline); cfg5: configs[4] "
+                         "custom_layout many-small fp32 tiles")
+    ap.add_argument("--cfg5-op", choices=["N", "T"], default="N")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     args = ap.parse_args()
@@ -138,23 +192,35 @@ def main():
     n, b = args.edge, args.block
     pm, pn = grid_for(world)
     M, N = n * pm, n * pn  # A: M x N on pm x pn; C = A^T: N x M on the same rank grid
-    lr_a, lc_a = M // pm, N // pn
-    lr_c, lc_c = N // pm, M // pn
-    g = torch.Generator(device="cuda")
-    g.manual_seed(1234 + rank)
-    A = torch.rand(lr_a * lc_a, dtype=torch.float64, device="cuda", generator=g)
-    Cm = torch.zeros(lr_c * lc_c, dtype=torch.float64, device="cuda")
-    LA = costa.block_cyclic_layout(M, N, b, b, 1, 1, M, N, pm, pn, "R", 0, 0, A.data_ptr(), lr_a,
-                                   "C", rank)
-    LC = costa.block_cyclic_layout(N, M, b, b, 1, 1, N, M, pm, pn, "R", 0, 0, Cm.data_ptr(), lr_c,
-                                   "C", rank)
+    if args.workload == "cfg5":
+        LA, LC, A, Cm, op, al, be, wl = cfg5_workload(costa, torch, rank, world, args.cfg5_op)
+        check = None
+    else:
+        lr_a, lc_a = M // pm, N // pn
+        lr_c, lc_c = N // pm, M // pn
+        g = torch.Generator(device="cuda")
+        g.manual_seed(1234 + rank)
+        A = torch.rand(lr_a * lc_a, dtype=torch.float64, device="cuda", generator=g)
+        Cm = torch.zeros(lr_c * lc_c, dtype=torch.float64, device="cuda")
+        LA = costa.block_cyclic_layout(M, N, b, b, 1, 1, M, N, pm, pn, "R", 0, 0, A.data_ptr(),
+                                       lr_a, "C", rank)
+        LC = costa.block_cyclic_layout(N, M, b, b, 1, 1, N, M, pm, pn, "R", 0, 0, Cm.data_ptr(),
+                                       lr_c, "C", rank)
+        op, al, be = "T", 1.0, 0.0
+        wl = (("pxtran fp64 16384x16384, 256x256 blocks, op T, alpha=1 beta=0, "
+               "1x1 grid (BASELINE configs[1])") if world == 1 else
+              (f"pxtran fp64 weak-scaled: {M}x{N} on a {pm}x{pn} rank grid "
+               f"(16384^2 per rank), 256x256 blocks, op T, alpha=1 beta=0"))
+
+        def check():
+            assert torch.equal(Cm.view(n, n), A.view(n, n).t()), "transpose result wrong"
     torch.cuda.synchronize()
 
     def step_blocking():
-        costa.transform(LA, LC, comm, "T", 1.0, 0.0)
+        costa.transform(LA, LC, comm, op, al, be)
 
     def step_async():  # stream-ordered: the host queues step k+1 while step k runs
-        costa.transform_async(LA, LC, comm, "T", 1.0, 0.0)
+        costa.transform_async(LA, LC, comm, op, al, be)
 
     def timed(step):
         costa.set_profiling(True)
@@ -174,14 +240,14 @@ def main():
 
     for _ in range(args.warmup):
         step_blocking()
-    if world == 1:  # correctness of what we time: C == A^T
-        assert torch.equal(Cm.view(n, n), A.view(n, n).t()), "transpose result wrong"
+    if world == 1 and check:  # correctness of what we time
+        check()
     el_block, _ = timed(step_blocking)
     for _ in range(args.warmup):
         step_async()
     el, st = timed(step_async)
-    if world == 1:
-        assert torch.equal(Cm.view(n, n), A.view(n, n).t()), "transpose result wrong (async)"
+    if world == 1 and check:
+        check()
 
     alg_bytes = st["local_bytes"] + st["pack_bytes"] + st["unpack_bytes"]  # this rank, K steps
     total_bytes = alg_bytes
@@ -190,6 +256,10 @@ def main():
         dist.all_reduce(t)
         total_bytes = t.item()
     value = total_bytes / el / 1e9
+    # SURVEY §8(d) node figure: kernel time only (pack + local + unpack), summed bytes / max t
+    kern_ms = (st["local_ms"] + st["pack_ms"] + st["unpack_ms"]) / args.steps
+    kern_ms = max_over_ranks(kern_ms)
+    kernel_node = total_bytes / args.steps / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else None
 
     # dominant kernel: the launch list moving the most bytes on this rank
     kern = max([("local", st["local_bytes"], st["local_ms"], st["local_launches"]),
@@ -201,26 +271,28 @@ def main():
     avg_ms = kms / max(kl, 1)
     achieved = per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     traffic, traffic_src = measured_traffic(int(per_launch))
+    kdt = "double" if args.workload != "cfg5" else "float"
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
             "traffic_source": traffic_src,
-            "kernel": f"tile_kernel<double> ({name} list)", "bytes_per_launch": int(per_launch),
+            "kernel": f"tile_kernel<{kdt}> ({name} list)", "bytes_per_launch": int(per_launch),
             "avg_launch_ms": round(avg_ms, 4)}
 
     # end-to-end from host memory (H2D + kernels + D2H), reported, never `value`
     e2e = None
-    if not args.no_e2e and world == 1:
+    if not args.no_e2e and world == 1 and args.workload == "pxtran":
         import numpy as np
         ha = A.cpu().numpy()
         hc = np.zeros_like(ha)
-        HA = costa.block_cyclic_layout(M, N, b, b, 1, 1, M, N, pm, pn, "R", 0, 0, ha, lr_a, "C", rank)
-        HC = costa.block_cyclic_layout(N, M, b, b, 1, 1, N, M, pm, pn, "R", 0, 0, hc, lr_c, "C", rank)
+        HA = costa.block_cyclic_layout(M, N, b, b, 1, 1, M, N, pm, pn, "R", 0, 0, ha, M, "C", rank)
+        HC = costa.block_cyclic_layout(N, M, b, b, 1, 1, N, M, pm, pn, "R", 0, 0, hc, N, "C", rank)
         costa.transform(HA, HC, comm, "T", 1.0, 0.0)  # plan + staging allocation
         reps, t1 = 3, time.perf_counter()
         for _ in range(reps):
             costa.transform(HA, HC, comm, "T", 1.0, 0.0)
         te = (time.perf_counter() - t1) / reps
-        e2e = {"GBps_algorithmic": round(2 * ha.nbytes / te / 1e9, 2), "ms_per_call": round(te * 1e3, 2),
+        e2e = {"GBps_algorithmic": round(2 * ha.nbytes / te / 1e9, 2),
+               "ms_per_call": round(te * 1e3, 2),
                "note": "pageable host A and C; H2D of A and C ranges + kernel + D2H of C"}
 
     # fixed cost of one blocking transform call (plan-cache hit, one 64x64 tile)
@@ -228,10 +300,10 @@ def main():
     if world == 1:
         ta = torch.zeros(64 * 64, dtype=torch.float64, device="cuda")
         tc = torch.zeros(64 * 64, dtype=torch.float64, device="cuda")
-        SA = costa.block_cyclic_layout(64, 64, 64, 64, 1, 1, 64, 64, 1, 1, "R", 0, 0, ta.data_ptr(),
-                                       64, "C", 0)
-        SC = costa.block_cyclic_layout(64, 64, 64, 64, 1, 1, 64, 64, 1, 1, "R", 0, 0, tc.data_ptr(),
-                                       64, "C", 0)
+        SA = costa.block_cyclic_layout(64, 64, 64, 64, 1, 1, 64, 64, 1, 1, "R", 0, 0,
+                                       ta.data_ptr(), 64, "C", 0)
+        SC = costa.block_cyclic_layout(64, 64, 64, 64, 1, 1, 64, 64, 1, 1, "R", 0, 0,
+                                       tc.data_ptr(), 64, "C", 0)
         for _ in range(10):
             costa.transform(SA, SC, comm, "T", 1.0, 0.0)
         t1 = time.perf_counter()
@@ -240,10 +312,15 @@ def main():
         overhead_us = round((time.perf_counter() - t1) / 200 * 1e6, 1)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "pxtran":
         cpu = cpu_baseline(n=n, b=b)
 
     if rank == 0:
+        cfg = {"workload": wl, "op": op, "alpha": al, "beta": be,
+               "parallelism": f"{world} rank(s), one per GPU, RCCL send/recv exchange",
+               "bytes_per_step": int(total_bytes / args.steps)}
+        if args.workload == "pxtran":
+            cfg.update({"m": M, "n": N, "block": b, "grid": f"{pm}x{pn}"})
         line = {
             "metric": "GB/s device-resident tile pack+transpose+unpack (fp64), % HBM peak",
             "value": round(value, 2),
@@ -254,19 +331,11 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if args.workload == "pxtran" else "strong",
             "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic (uniform random fp64, device-resident)",
-            "config": {
-                "workload": ("pxtran fp64 16384x16384, 256x256 blocks, op T, alpha=1 beta=0, "
-                             "1x1 grid (BASELINE configs[1])") if world == 1 else
-                            (f"pxtran fp64 weak-scaled: {M}x{N} on a {pm}x{pn} rank grid "
-                             f"(16384^2 per rank), 256x256 blocks, op T, alpha=1 beta=0"),
-                "m": M, "n": N, "block": b, "grid": f"{pm}x{pn}", "op": "T",
-                "parallelism": f"{world} rank(s), one per GPU, RCCL send/recv exchange",
-                "bytes_per_step": int(total_bytes / args.steps),
-            },
+            "dtype": "f64" if args.workload == "pxtran" else "f32",
+            "data": "synthetic (uniform random, device-resident)",
+            "config": cfg,
             "roofline": roof,
             "cpu_baseline": cpu,
             "e2e_host": e2e,
@@ -275,6 +344,7 @@ def main():
                          "GBps": round(total_bytes / el_block / 1e9, 2),
                          "note": "costa_hip_transform (reference semantics: host waits for C)"},
             "value_mode": "costa_hip_transform_async steps, stream-ordered, one sync at the end",
+            "kernel_node_GBps": round(kernel_node, 2) if kernel_node else None,
             "phase_ms_per_step": {k: round(st[k + "_ms"] / args.steps, 4)
                                   for k in ("pack", "local", "unpack", "exchange")},
         }
