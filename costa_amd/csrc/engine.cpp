@@ -186,25 +186,38 @@ bool any_transpose(const std::vector<costa_tile_op_t>& ops) {
 
 // An op goes to the large shape when it holds at least half a large sub-tile of data;
 // smaller (ragged, many-small) tiles go to the small shape so a workgroup is not mostly idle.
-int64_t build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops,
-                   std::vector<uint64_t>& work) {
+// Tiny ops (a wavefront's worth of data) go to the one-wave-per-op path.
+work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops,
+                      std::vector<uint64_t>& work) {
     int bfl = 0, bsl = 0, bfs = 0, bss = 0;
     tile_shapes(dtype, &bfl, &bsl, &bfs, &bss);
+    const int64_t E = int64_t(dtype_size(dtype));
     work.clear();
-    std::vector<uint64_t> small;
+    std::vector<uint64_t> small, tiny;
     for (size_t i = 0; i < ops.size(); ++i) {
         const auto& op = ops[i];
         if (op.nf <= 0 || op.ns <= 0) continue;
-        const bool large = 2 * int64_t(op.nf) * op.ns >= int64_t(bfl) * bsl;
+        if (i > 0xFFFFFFFFull) throw error(COSTA_ERR_ARG, "costa: too many tiles in one list");
+        const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
+        const int64_t elems = int64_t(op.nf) * op.ns;
+        if (tr ? int64_t(op.nf | 1) * op.ns * E <= kTinyLdsBytes : elems * E <= kTinyCopyBytes) {
+            tiny.push_back(uint64_t(i) << 32);
+            continue;
+        }
+        const bool large = 2 * elems >= int64_t(bfl) * bsl;
         const int bf = large ? bfl : bfs, bs = large ? bsl : bss;
         const uint64_t n = uint64_t((op.nf + bf - 1) / bf) * uint64_t((op.ns + bs - 1) / bs);
-        if (n > 0xFFFFFFFFull || i > 0xFFFFFFFFull) throw error(COSTA_ERR_ARG, "costa: tile too large");
+        if (n > 0xFFFFFFFFull) throw error(COSTA_ERR_ARG, "costa: tile too large");
         auto& dst = large ? work : small;
         for (uint64_t k = 0; k < n; ++k) dst.push_back((uint64_t(i) << 32) | k);
     }
-    const int64_t n_large = int64_t(work.size());
+    work_split w;
+    w.n_large = int64_t(work.size());
+    w.n_small = int64_t(small.size());
+    w.n_tiny = int64_t(tiny.size());
     work.insert(work.end(), small.begin(), small.end());
-    return n_large;
+    work.insert(work.end(), tiny.begin(), tiny.end());
+    return w;
 }
 
 // ---------------------------------------------------------------- residency / staging
@@ -315,7 +328,7 @@ struct cached_plan {
     // device copies of the op lists and work lists
     dbuf d_local, d_pack, d_unpack, w_local, w_pack, w_unpack, d_scal;
     int64_t n_local = 0, n_pack = 0, n_unpack = 0;
-    int64_t l_local = 0, l_pack = 0, l_unpack = 0;  // large-shape items at the front
+    work_split l_local, l_pack, l_unpack;  // how each work list splits over the kernel shapes
     bool tr_local = true, tr_unpack = true;          // any op of the list transposes
     std::vector<unsigned char> scal_host;
 };
@@ -614,7 +627,8 @@ void transform(const std::vector<job>& jobs, comm* c, void* user_stream, bool as
         tm.start(PH_LOCAL, ls);
         launch_tiles(p.dtype,
                      {static_cast<const costa_tile_op_t*>(cp.d_local.p),
-                      static_cast<const uint64_t*>(cp.w_local.p), cp.n_local, cp.l_local, nullptr,
+                      static_cast<const uint64_t*>(cp.w_local.p), cp.n_local, cp.l_local.n_large,
+                      cp.l_local.n_small, nullptr,
                       nullptr, cp.d_scal.p, cp.tr_local},
                      ls);
         tm.stop();
@@ -630,7 +644,8 @@ void transform(const std::vector<job>& jobs, comm* c, void* user_stream, bool as
             tm.start(PH_PACK, dc.main);
             launch_tiles(p.dtype,
                          {static_cast<const costa_tile_op_t*>(cp.d_pack.p),
-                          static_cast<const uint64_t*>(cp.w_pack.p), cp.n_pack, cp.l_pack, nullptr,
+                          static_cast<const uint64_t*>(cp.w_pack.p), cp.n_pack, cp.l_pack.n_large,
+                          cp.l_pack.n_small, nullptr,
                           sb, cp.d_scal.p, false},
                          dc.main);
             tm.stop();
@@ -653,7 +668,8 @@ void transform(const std::vector<job>& jobs, comm* c, void* user_stream, bool as
             tm.start(PH_UNPACK, dc.main);
             launch_tiles(p.dtype,
                          {static_cast<const costa_tile_op_t*>(cp.d_unpack.p),
-                          static_cast<const uint64_t*>(cp.w_unpack.p), cp.n_unpack, cp.l_unpack,
+                          static_cast<const uint64_t*>(cp.w_unpack.p), cp.n_unpack, cp.l_unpack.n_large,
+                          cp.l_unpack.n_small,
                           rb, nullptr, cp.d_scal.p, cp.tr_unpack},
                          dc.main);
             tm.stop();
@@ -706,7 +722,7 @@ void execute_tiles(costa_dtype_t dtype, const costa_tile_op_t* ops, int64_t n,
         if ((op.flags >> COSTA_SLOT_SHIFT) >= uint32_t(std::max(n_slots, 0)))
             throw error(COSTA_ERR_ARG, "costa_hip_execute_tiles: scalar slot out of range");
     std::vector<uint64_t> w;
-    const int64_t nl = build_work(dtype, v, w);
+    const work_split nl = build_work(dtype, v, w);
     dbuf d_ops, d_work, d_scal;
     d_ops.upload(v, dc.main);
     d_work.upload(w, dc.main);
@@ -716,7 +732,7 @@ void execute_tiles(costa_dtype_t dtype, const costa_tile_op_t* ops, int64_t n,
     d_scal.upload(sc, dc.main);
     launch_tiles(dtype,
                  {static_cast<const costa_tile_op_t*>(d_ops.p), static_cast<const uint64_t*>(d_work.p),
-                  int64_t(w.size()), nl, static_cast<const char*>(src_base), static_cast<char*>(dst_base),
+                  int64_t(w.size()), nl.n_large, nl.n_small, static_cast<const char*>(src_base), static_cast<char*>(dst_base),
                   d_scal.p, any_transpose(v)},
                  dc.main);
     HIP_CHECK(hipStreamSynchronize(dc.main));

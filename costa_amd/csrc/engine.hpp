@@ -112,11 +112,18 @@ void execute_tiles(costa_dtype_t dtype, const costa_tile_op_t* ops, int64_t n,
                    int device);
 
 // kernel launcher (tile_kernels.hip); `work` and `ops` are device arrays
+// ops small enough for one wavefront each (tiny path): copy mode up to kTinyCopyBytes of
+// data, transpose mode up to kTinyLdsBytes of staged tile (row pitch nf | 1)
+constexpr int kTinyCopyBytes = 16384;
+constexpr int kTinyLdsBytes = 8192;
+constexpr int tiny_lds_bytes = kTinyLdsBytes;
+
 struct launch_args {
     const costa_tile_op_t* ops;
-    const uint64_t* work;   // per workgroup: (op index << 32) | sub-tile index
-    int64_t n_work;         // total work items
-    int64_t n_large;        // the first n_large items use the large sub-tile shape
+    const uint64_t* work;   // per item: (op index << 32) | sub-tile index
+    int64_t n_work;         // total work items: [large | small | tiny]
+    int64_t n_large;        // items using the large sub-tile shape
+    int64_t n_small;        // items using the small shape; the rest are tiny ops
     const char* src_base;
     char* dst_base;
     const void* scalars;    // device: n_slots x (alpha, beta) of the dtype
@@ -126,9 +133,12 @@ bool any_transpose(const std::vector<costa_tile_op_t>& ops);
 void launch_tiles(costa_dtype_t dtype, const launch_args& a, void* stream /* hipStream_t */);
 // sub-tile shapes (elements along the source's fast dim, along its slow dim)
 void tile_shapes(costa_dtype_t dtype, int* bf_large, int* bs_large, int* bf_small, int* bs_small);
-// per-workgroup work list of an op list: large-shape items first; returns their count
-int64_t build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops,
-                   std::vector<uint64_t>& work);
+// work list of an op list: [large-shape sub-tiles | small-shape sub-tiles | tiny ops]
+struct work_split {
+    int64_t n_large = 0, n_small = 0, n_tiny = 0;
+};
+work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops,
+                      std::vector<uint64_t>& work);
 
 // errors
 struct error : std::runtime_error {

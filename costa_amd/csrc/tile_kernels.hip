@@ -312,6 +312,160 @@ __global__ __launch_bounds__(S::NT) void tile_kernel(const costa_tile_op_t* __re
         run_tile<T, S, false>(op, f0, s0, tf, ts, src_base, dst_base, alpha, beta, tile);
 }
 
+// ---------------------------------------------------------------- tiny ops
+// One wavefront per op (4 per workgroup).  Lanes walk the tile in linear order: source order
+// (f fastest) for loads, destination order for stores, with (f, s) advanced by a constant
+// per step (no per-element division).  Copy mode needs no LDS; transpose mode stages the tile
+// in the wave's own LDS region with an odd row pitch (conflict-free column reads).
+// Measured motivation: BASELINE cfg 5 (242k tiles of ~33x33 fp32) ran at 1.8 TB/s with one
+// 256-thread workgroup per tile: too few bytes in flight per CU.
+constexpr int TINY_WAVES = 4;
+template <typename T>
+constexpr int tiny_unroll() { return 64 / int(sizeof(T)); }  // 64 bytes in flight per lane
+
+template <typename T>
+struct lin {  // (f, s) of linear element index e = f + s*n, stepped by 64
+    int f, s, df, ds, n;
+    __device__ __forceinline__ lin(int lane, int n_) : n(n_) {
+        f = lane % n;
+        s = lane / n;
+        df = 64 % n;
+        ds = 64 / n;
+    }
+    __device__ __forceinline__ void step() {
+        f += df;
+        s += ds;
+        if (f >= n) {
+            f -= n;
+            ++s;
+        }
+    }
+};
+
+template <typename T>
+__global__ __launch_bounds__(64 * TINY_WAVES) void tiny_kernel(
+    const costa_tile_op_t* __restrict__ ops, const uint64_t* __restrict__ work, int64_t n_items,
+    const char* src_base, char* dst_base, const T* __restrict__ scalars, int lds_per_wave) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = int(threadIdx.x) % 64;
+    const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / 64);
+    const int64_t item = int64_t(blockIdx.x) * TINY_WAVES + wave;
+    if (item >= n_items) return;
+    const costa_tile_op_t op = ops[work[item] >> 32];
+    const uint32_t flags = op.flags;
+    const uint32_t kind = (flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT;
+    const bool conj = flags & COSTA_TILE_CONJ;
+    const uint32_t slot = flags >> COSTA_SLOT_SHIFT;
+    const T alpha = scalars[2 * slot];
+    const T beta = scalars[2 * slot + 1];
+    const T* src = reinterpret_cast<const T*>(src_base + op.src);
+    T* dst = reinterpret_cast<T*>(dst_base + op.dst);
+    const int nf = op.nf, ns = op.ns, total = nf * ns;
+    const int64_t lds = op.lds, ldd = op.ldd;
+    constexpr int U = tiny_unroll<T>();
+
+    if (!(flags & COSTA_TILE_TRANSPOSE)) {
+        // copy mode: dst(f, s) = g(src(f, s)), UNROLL independent loads in flight per lane
+        lin<T> p(lane, nf);
+        for (int e0 = 0; e0 < total; e0 += 64 * U) {
+            T x[U], y[U];
+            int fs[U], ss[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                x[u] = y[u] = e_zero<T>();
+                fs[u] = p.f;
+                ss[u] = p.s;
+                if (e0 + u * 64 + lane < total) x[u] = src[ss[u] * lds + fs[u]];
+                p.step();
+            }
+            if (kind == COSTA_SCALE_AXPBY) {
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (e0 + u * 64 + lane < total) y[u] = dst[ss[u] * ldd + fs[u]];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (e0 + u * 64 + lane >= total) continue;
+                T v = x[u];
+                if (kind != COSTA_SCALE_BITCOPY)
+                    v = scale(v, kind == COSTA_SCALE_AXPBY ? y[u] : e_zero<T>(), kind, conj, alpha,
+                              beta);
+                dst[ss[u] * ldd + fs[u]] = v;
+            }
+        }
+        return;
+    }
+    // transpose mode: stage in LDS (pitch odd), then write in destination order
+    T* t = reinterpret_cast<T*>(smem) + int64_t(wave) * lds_per_wave;
+    const int pitch = nf | 1;
+    {
+        lin<T> p(lane, nf);
+        for (int e0 = 0; e0 < total; e0 += 64 * U) {
+            T x[U];
+            int fs[U], ss[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                x[u] = e_zero<T>();
+                fs[u] = p.f;
+                ss[u] = p.s;
+                if (e0 + u * 64 + lane < total) x[u] = src[ss[u] * lds + fs[u]];
+                p.step();
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (e0 + u * 64 + lane < total) t[ss[u] * pitch + fs[u]] = x[u];
+        }
+    }
+    // LDS writes of this wave complete before its reads (in-order per wave + explicit wait)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    {
+        lin<T> q(lane, ns);  // destination order: s fastest (dst row f is contiguous in s)
+        for (int e0 = 0; e0 < total; e0 += 64 * U) {
+            T v[U], y[U];
+            int fs[U], ss[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                v[u] = y[u] = e_zero<T>();
+                ss[u] = q.f;  // q.f walks s, q.s walks f
+                fs[u] = q.s;
+                if (e0 + u * 64 + lane < total) v[u] = t[ss[u] * pitch + fs[u]];
+                q.step();
+            }
+            if (kind == COSTA_SCALE_AXPBY) {
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (e0 + u * 64 + lane < total) y[u] = dst[fs[u] * ldd + ss[u]];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (e0 + u * 64 + lane >= total) continue;
+                const T r = scale(v[u], kind == COSTA_SCALE_AXPBY ? y[u] : e_zero<T>(), kind, conj,
+                                  alpha, beta);
+                dst[fs[u] * ldd + ss[u]] = r;
+            }
+        }
+    }
+}
+
+template <typename T>
+void launch_tiny(const launch_args& a, hipStream_t stream) {
+    const int64_t n = a.n_work - a.n_large - a.n_small;
+    if (n <= 0) return;
+    const uint64_t* work = a.work + a.n_large + a.n_small;
+    const int per_wave = a.any_transpose ? int(tiny_lds_bytes / sizeof(T)) : 0;
+    const size_t lds = size_t(per_wave) * sizeof(T) * TINY_WAVES;
+    const int64_t max_items = (int64_t(1) << 30) * TINY_WAVES;
+    for (int64_t off = 0; off < n; off += max_items) {
+        const int64_t m = std::min(max_items, n - off);
+        hipLaunchKernelGGL(tiny_kernel<T>, dim3(unsigned((m + TINY_WAVES - 1) / TINY_WAVES)),
+                           dim3(64 * TINY_WAVES), lds, stream, a.ops, work + off, m, a.src_base,
+                           a.dst_base, static_cast<const T*>(a.scalars), per_wave);
+    }
+}
+
 template <typename T, typename S>
 void launch_shape(const launch_args& a, const uint64_t* work, int64_t n, hipStream_t stream) {
     const int64_t max_grid = 1LL << 30;
@@ -327,9 +481,10 @@ void launch_shape(const launch_args& a, const uint64_t* work, int64_t n, hipStre
 
 template <typename T>
 void launch_t(const launch_args& a, hipStream_t stream) {
-    // work list: [large sub-tiles | small sub-tiles]
+    // work list: [large sub-tiles | small sub-tiles | tiny ops]
     launch_shape<T, typename shapes<T>::large>(a, a.work, a.n_large, stream);
-    launch_shape<T, typename shapes<T>::small>(a, a.work + a.n_large, a.n_work - a.n_large, stream);
+    launch_shape<T, typename shapes<T>::small>(a, a.work + a.n_large, a.n_small, stream);
+    launch_tiny<T>(a, stream);
 }
 
 template <typename T>

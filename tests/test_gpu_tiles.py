@@ -1,0 +1,123 @@
+"""GPU parity of one batched tile launch against the oracle, on random op lists that mix every
+work class of the executor: tiny ops (one wavefront each, copy and LDS transpose), small and
+large sub-tile shapes, the class boundaries (engine.hpp kTinyCopyBytes / kTinyLdsBytes), thin
+ops (nf = 1, ns = 1), padded strides, unaligned offsets, and every scale kind.
+
+Each op is the reference's copy_and_transform (memory_utils.hpp:339-412); the oracle executes
+the same list op by op (oracle.exec_tile_ops).  Bit-exact: integers and finite floats with
+contraction off on both sides.
+"""
+import numpy as np
+import pytest
+
+import costa_amd
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+TINY_COPY, TINY_LDS = 16384, 8192  # engine.hpp kTinyCopyBytes / kTinyLdsBytes
+
+
+@pytest.fixture(scope="module")
+def gpu(costa):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return costa
+
+
+def _values(rng, dt, n):
+    if dt == np.int32:
+        return rng.integers(-1000, 1000, n, dtype=np.int32)
+    x = rng.standard_normal(n)
+    if np.issubdtype(dt, np.complexfloating):
+        x = x + 1j * rng.standard_normal(n)
+    return x.astype(dt)
+
+
+def _shape(rng, E, transpose):
+    """(nf, ns) drawn to hit every class and the boundaries between them"""
+    pick = rng.integers(0, 7)
+    if pick == 0:  # tiny, ragged
+        return int(rng.integers(1, 70)), int(rng.integers(1, 70))
+    if pick == 1:  # at the tiny boundary
+        limit = (TINY_LDS if transpose else TINY_COPY) // E
+        nf = int(rng.integers(1, 129))
+        ns = max(1, limit // ((nf | 1) if transpose else nf) + int(rng.integers(-1, 2)))
+        return nf, ns
+    if pick == 2:  # thin column
+        return 1, int(rng.integers(1, 5000))
+    if pick == 3:  # thin row
+        return int(rng.integers(1, 5000)), 1
+    if pick == 4:  # medium (small shape)
+        return int(rng.integers(60, 200)), int(rng.integers(40, 140))
+    if pick == 5:  # large shape, ragged edge
+        return int(rng.integers(200, 600)), int(rng.integers(100, 300))
+    return int(rng.integers(1, 400)), int(rng.integers(1, 400))
+
+
+def _random_list(rng, code, n_ops):
+    """op list whose scale kinds agree with the slot scalars (see SLOTS)"""
+    dt = oracle.NP[code]
+    E = np.dtype(dt).itemsize
+    cplx = np.issubdtype(dt, np.complexfloating)
+    ops = np.zeros(n_ops, costa_amd.TILE_OP_DTYPE)
+    src_off = dst_off = 0
+    for i in range(n_ops):
+        tr = bool(rng.integers(0, 2))
+        nf, ns = _shape(rng, E, tr)
+        lds = nf + int(rng.integers(0, 2)) * int(rng.integers(0, 5))
+        dn = ns if tr else nf
+        ldd = dn + int(rng.integers(0, 2)) * int(rng.integers(0, 5))
+        d_slow = nf if tr else ns
+        if rng.integers(0, 3) == 0:  # misalign the start by a few elements
+            src_off += int(rng.integers(1, 4))
+            dst_off += int(rng.integers(1, 4))
+        else:  # 16-byte aligned
+            src_off = -(-src_off * E // 16) * 16 // E
+            dst_off = -(-dst_off * E // 16) * 16 // E
+        conj = bool(cplx and rng.integers(0, 2))
+        kind = int(rng.integers(0, 4))
+        if kind == 0 and (tr or conj):  # the planner never bit-copies through a transpose/conj
+            kind = 2
+            slot = 0  # alpha = 1, beta = 0 evaluated as a product (memory_utils.hpp:101-291)
+        else:
+            slot = (0, 1, 2, 3)[kind] if kind != 2 else int(rng.choice([0, 2]))
+        flags = (1 if tr else 0) | (2 if conj else 0) | (kind << 4) | (slot << 16)
+        if (src_off * E) % 16 == 0 and (lds * E) % 16 == 0:
+            flags |= 4
+        if (dst_off * E) % 16 == 0 and (ldd * E) % 16 == 0:
+            flags |= 8
+        ops[i] = (src_off * E, dst_off * E, nf, ns, lds, ldd, flags, 0)
+        src_off += (ns - 1) * lds + nf
+        dst_off += (d_slow - 1) * ldd + dn
+    return ops, src_off, dst_off
+
+
+@pytest.mark.parametrize("code", [0, 1, 2, 3, 4], ids=["f32", "f64", "c64", "c128", "i32"])
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_mixed_tile_list(gpu, code, seed):
+    rng = np.random.default_rng(1000 * seed + code)
+    dt = oracle.NP[code]
+    ops, n_src, n_dst = _random_list(rng, code, 240)
+    src = _values(rng, dt, n_src)
+    dst0 = _values(rng, dt, n_dst)
+    # SLOTS: 0 = (1, 0) bit copy / unit scale, 1 = (0, 0), 2 = (alpha, 0), 3 = (alpha, beta)
+    if dt == np.int32:
+        scal = np.array([1, 0, 0, 0, 2, 0, -3, 5], dt)
+    else:
+        a, b = _values(rng, dt, 2)
+        scal = np.array([1, 0, 0, 0, a, 0, a, b], dt)
+    exp = dst0.copy()
+    oracle.exec_tile_ops(code, ops, scal, src.ctypes.data, exp.ctypes.data)
+
+    d_src = torch.from_numpy(src.view(np.uint8).copy()).cuda()
+    d_dst = torch.from_numpy(dst0.view(np.uint8).copy()).cuda()
+    gpu.execute_tiles(code, ops, scal, d_src.data_ptr(), d_dst.data_ptr())
+    torch.cuda.synchronize()
+    got = d_dst.cpu().numpy().view(dt)
+    E = np.dtype(dt).itemsize
+    bad = np.flatnonzero((got.view(np.uint8).reshape(n_dst, E)
+                          != exp.view(np.uint8).reshape(n_dst, E)).any(1))
+    assert bad.size == 0, f"{bad.size} elements differ, first at {bad[0]}: {got[bad[0]]} vs {exp[bad[0]]}"
