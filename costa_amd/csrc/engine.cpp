@@ -13,6 +13,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <list>
@@ -184,40 +186,135 @@ bool any_transpose(const std::vector<costa_tile_op_t>& ops) {
     return false;
 }
 
-// An op goes to the large shape when it holds at least half a large sub-tile of data;
-// smaller (ragged, many-small) tiles go to the small shape so a workgroup is not mostly idle.
-// Tiny ops (a wavefront's worth of data) go to the one-wave-per-op path.
+// Work classes.  An op goes to the large shape (a 1024-thread workgroup per sub-tile) when it
+// holds at least half a large sub-tile of data; every other op runs on the wavefront path
+// (tiny_kernel): ops over a wavefront's budget are first cut, here on the host, into
+// rectangular sub-ops within it (a sub-rectangle of a tile op is a tile op).  Budgets: copy
+// mode kTinyCopyBytes of data, transpose mode kTinyLdsBytes of staged tile (row pitch nf | 1).
+static bool is_tiny(const costa_tile_op_t& op, int64_t E) {
+    if (op.flags & COSTA_TILE_TRANSPOSE) return int64_t(op.nf | 1) * op.ns * E <= kTinyLdsBytes;
+    return int64_t(op.nf) * op.ns * E <= kTinyCopyBytes;
+}
+
+static uint32_t vec_flags(uint64_t src, int64_t lds, uint64_t dst, int64_t ldd, int64_t E) {
+    uint32_t f = 0;
+    if (src % 16 == 0 && (lds * E) % 16 == 0) f |= COSTA_TILE_VEC_SRC;
+    if (dst % 16 == 0 && (ldd * E) % 16 == 0) f |= COSTA_TILE_VEC_DST;
+    return f;
+}
+
+// cut `op` into near-equal rectangles that each fit the wavefront budget
+static void split_for_waves(const costa_tile_op_t& op, int64_t E, std::vector<costa_tile_op_t>& out) {
+    if (is_tiny(op, E)) {
+        out.push_back(op);
+        return;
+    }
+    const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
+    const int64_t budget = (tr ? kTinyLdsBytes : kTinyCopyBytes) / E;  // elements
+    const int64_t nf = op.nf, ns = op.ns;
+    // transpose: near-square pieces (both the source columns and the destination rows stay
+    // long); copy: whole columns when one fits, else tall pieces
+    const int64_t side = tr ? std::max<int64_t>(1, int64_t(std::sqrt(double(budget)))) : budget;
+    const int64_t nfc = (nf + side - 1) / side;
+    const int64_t cf = (nf + nfc - 1) / nfc;
+    const int64_t cs_max = std::max<int64_t>(1, budget / (tr ? (cf | 1) : cf));
+    const int64_t nsc = (ns + cs_max - 1) / cs_max;
+    const uint32_t keep = op.flags & ~uint32_t(COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST);
+    for (int64_t i = 0; i < nfc; ++i) {
+        const int64_t f0 = i * nf / nfc, f1 = (i + 1) * nf / nfc;
+        for (int64_t j = 0; j < nsc; ++j) {
+            const int64_t s0 = j * ns / nsc, s1 = (j + 1) * ns / nsc;
+            costa_tile_op_t sub = op;
+            sub.src = op.src + uint64_t((s0 * op.lds + f0) * E);
+            sub.dst = op.dst + uint64_t((tr ? f0 * op.ldd + s0 : s0 * op.ldd + f0) * E);
+            sub.nf = int32_t(f1 - f0);
+            sub.ns = int32_t(s1 - s0);
+            sub.flags = keep | vec_flags(sub.src, op.lds, sub.dst, op.ldd, E);
+            if (!is_tiny(sub, E)) throw error(COSTA_ERR_INTERNAL, "costa: wave split over budget");
+            out.push_back(sub);
+        }
+    }
+}
+
+namespace {
+struct wave_knobs {  // defaults, overridable for tuning runs
+    int policy = 1;  // COSTA_WAVE_POLICY 0: only ops within the budget take the wave path (the
+                     // rest: 256-thread small shape); 1: every op below the large threshold;
+                     // 2: also large ops that are not 16-byte aligned on both sides
+    int sort = 2;    // COSTA_TINY_SORT 0: plan order, 1: by source, 2: by destination address
+};
+const wave_knobs& knobs() {
+    static wave_knobs k = [] {
+        wave_knobs x;
+        if (const char* s = std::getenv("COSTA_WAVE_POLICY")) x.policy = std::atoi(s);
+        if (const char* s = std::getenv("COSTA_TINY_SORT")) x.sort = std::atoi(s);
+        return x;
+    }();
+    return k;
+}
+}  // namespace
+
 work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops,
-                      std::vector<uint64_t>& work) {
+                      std::vector<costa_tile_op_t>& ordered, std::vector<uint64_t>& work) {
     int bfl = 0, bsl = 0, bfs = 0, bss = 0;
     tile_shapes(dtype, &bfl, &bsl, &bfs, &bss);
     const int64_t E = int64_t(dtype_size(dtype));
+    const wave_knobs& kn = knobs();
+    ordered.clear();
     work.clear();
-    std::vector<uint64_t> small, tiny;
-    for (size_t i = 0; i < ops.size(); ++i) {
-        const auto& op = ops[i];
+    std::vector<costa_tile_op_t> tiny;
+    std::vector<uint64_t> small;
+    const uint32_t vec_both = COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST;
+    for (const auto& op : ops) {
         if (op.nf <= 0 || op.ns <= 0) continue;
-        if (i > 0xFFFFFFFFull) throw error(COSTA_ERR_ARG, "costa: too many tiles in one list");
-        const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
         const int64_t elems = int64_t(op.nf) * op.ns;
-        if (tr ? int64_t(op.nf | 1) * op.ns * E <= kTinyLdsBytes : elems * E <= kTinyCopyBytes) {
-            tiny.push_back(uint64_t(i) << 32);
+        bool large = 2 * elems >= int64_t(bfl) * bsl;
+        if (kn.policy == 2 && (op.flags & vec_both) != vec_both) large = false;
+        if (is_tiny(op, E) || (!large && kn.policy >= 1)) {
+            split_for_waves(op, E, tiny);
             continue;
         }
-        const bool large = 2 * elems >= int64_t(bfl) * bsl;
+        const uint64_t i = ordered.size();
+        if (i > 0xFFFFFFFFull) throw error(COSTA_ERR_ARG, "costa: too many tiles in one list");
+        ordered.push_back(op);
         const int bf = large ? bfl : bfs, bs = large ? bsl : bss;
         const uint64_t n = uint64_t((op.nf + bf - 1) / bf) * uint64_t((op.ns + bs - 1) / bs);
         if (n > 0xFFFFFFFFull) throw error(COSTA_ERR_ARG, "costa: tile too large");
         auto& dst = large ? work : small;
-        for (uint64_t k = 0; k < n; ++k) dst.push_back((uint64_t(i) << 32) | k);
+        for (uint64_t k = 0; k < n; ++k) dst.push_back((i << 32) | k);
     }
+    // ops are independent (disjoint destinations), so any order is valid; neighbours in
+    // memory run at the same time and share the partially used cache lines at their edges
+    if (kn.sort == 1)
+        std::stable_sort(tiny.begin(), tiny.end(), [](const costa_tile_op_t& a,
+                                                      const costa_tile_op_t& b) { return a.src < b.src; });
+    else if (kn.sort == 2)
+        std::stable_sort(tiny.begin(), tiny.end(), [](const costa_tile_op_t& a,
+                                                      const costa_tile_op_t& b) { return a.dst < b.dst; });
     work_split w;
     w.n_large = int64_t(work.size());
     w.n_small = int64_t(small.size());
+    w.tiny_first = int64_t(ordered.size());
     w.n_tiny = int64_t(tiny.size());
     work.insert(work.end(), small.begin(), small.end());
-    work.insert(work.end(), tiny.begin(), tiny.end());
+    ordered.insert(ordered.end(), tiny.begin(), tiny.end());
     return w;
+}
+
+launch_args make_launch(const work_split& w, const void* d_ordered, const void* d_work,
+                        const char* src_base, char* dst_base, const void* d_scalars, bool transpose) {
+    launch_args a;
+    a.ops = static_cast<const costa_tile_op_t*>(d_ordered);
+    a.work = static_cast<const uint64_t*>(d_work);
+    a.n_large = w.n_large;
+    a.n_small = w.n_small;
+    a.tiny_first = w.tiny_first;
+    a.n_tiny = w.n_tiny;
+    a.src_base = src_base;
+    a.dst_base = dst_base;
+    a.scalars = d_scalars;
+    a.any_transpose = transpose;
+    return a;
 }
 
 // ---------------------------------------------------------------- residency / staging
@@ -323,11 +420,10 @@ struct cached_plan {
     int device = 0;
     // staging of host-resident layouts (empty when everything is in HBM)
     bool staged = false;
-    std::vector<hrange> a_ranges, c_ranges;  // c_ranges also copied back
+    std::vector<hrange> h2d_ranges, d2h_ranges;  // uploaded / copied back
     dbuf stage;
     // device copies of the op lists and work lists
     dbuf d_local, d_pack, d_unpack, w_local, w_pack, w_unpack, d_scal;
-    int64_t n_local = 0, n_pack = 0, n_unpack = 0;
     work_split l_local, l_pack, l_unpack;  // how each work list splits over the kernel shapes
     bool tr_local = true, tr_unpack = true;          // any op of the list transposes
     std::vector<unsigned char> scal_host;
@@ -409,6 +505,8 @@ cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
         }
     std::vector<elayout> remapped;
     std::vector<job> pj = jobs;
+    std::vector<hrange> staged_ranges;
+    std::vector<uint8_t> range_flags;
     if (!all_dev) {
         cp->staged = true;
         std::vector<const elayout*> As, Cs;
@@ -426,26 +524,37 @@ cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
             off += ((r.hi - r.lo) + 255) & ~size_t(255);
         }
         cp->stage.reserve(std::max<size_t>(off, 256));
-        auto in_set = [](const std::vector<const elayout*>& v, const elayout* L) {
-            return std::find(v.begin(), v.end(), L) != v.end();
+        // per merged range: holds A data (bit 0), C data (bit 1), C blocks of more than one
+        // job (bit 2); C ranges are copied back, A ranges and C ranges the kernels do not
+        // overwrite completely are uploaded (decided once the ops are known, below)
+        range_flags.assign(ranges.size(), 0);
+        std::vector<int> c_job(ranges.size(), -1);
+        auto range_of = [&](uintptr_t p) {
+            auto it = std::upper_bound(ranges.begin(), ranges.end(), p,
+                                       [](uintptr_t v, const hrange& r) { return v < r.lo; });
+            return size_t(it - ranges.begin()) - 1;
         };
-        // which merged ranges hold A data (H2D) and C data (H2D + D2H)
-        for (const auto& r : ranges) {
-            bool a = false, cc = false;
-            for (const elayout* L : all) {
+        k = 0;
+        for (size_t t = 0; t < jobs.size(); ++t) {
+            const bool a_host = !on_dev[k++], c_host = !on_dev[k++];
+            for (int side = 0; side < 2; ++side) {
+                if (!(side == 0 ? a_host : c_host)) continue;
+                const elayout* L = side == 0 ? jobs[t].A : jobs[t].C;
                 const size_t E = dtype_size(L->dtype);
                 for (const auto& b : L->blocks) {
-                    uintptr_t lo = reinterpret_cast<uintptr_t>(b.data);
-                    if (lo >= r.lo && lo < r.hi && block_extent_bytes(b, L->ordering, E)) {
-                        if (in_set(As, L)) a = true;
-                        if (in_set(Cs, L)) cc = true;
+                    if (!block_extent_bytes(b, L->ordering, E)) continue;
+                    const size_t i = range_of(reinterpret_cast<uintptr_t>(b.data));
+                    if (side == 0) {
+                        range_flags[i] |= 1;
+                    } else {
+                        range_flags[i] |= 2;
+                        if (c_job[i] >= 0 && c_job[i] != int(t)) range_flags[i] |= 4;
+                        c_job[i] = int(t);
                     }
                 }
-                if (a && cc) break;
             }
-            if (a || cc) cp->a_ranges.push_back(r);  // everything staged is uploaded
-            if (cc) cp->c_ranges.push_back(r);
         }
+        staged_ranges = ranges;
         remapped.reserve(jobs.size() * 2);
         k = 0;
         for (auto& j : pj) {
@@ -461,21 +570,52 @@ cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
     }
     cp->p = make_plan(pj, c->rank, c->size);
     const plan& p = *cp->p;
-    std::vector<uint64_t> w;
-    cp->d_local.upload(p.local_ops, dc.main);
+    if (cp->staged) {
+        // A C-only range needs no upload when the kernels overwrite every byte of it: one job's
+        // C blocks only, no op reading C (beta = 0), and the ops' writes (disjoint: each C
+        // element is written once per job) add up to the whole range.
+        const size_t E = dtype_size(p.dtype);
+        const uintptr_t base = reinterpret_cast<uintptr_t>(cp->stage.p);
+        std::vector<size_t> written(staged_ranges.size(), 0);
+        std::vector<bool> reads_c(staged_ranges.size(), false);
+        auto account = [&](const std::vector<costa_tile_op_t>& ops) {
+            for (const auto& op : ops) {
+                if (op.dst < base) continue;  // device-resident destination
+                const size_t off = size_t(op.dst - base);
+                auto it = std::upper_bound(staged_ranges.begin(), staged_ranges.end(), off,
+                                           [](size_t v, const hrange& r) { return v < r.dev_off; });
+                if (it == staged_ranges.begin()) continue;
+                const size_t i = size_t(it - staged_ranges.begin()) - 1;
+                if (off >= staged_ranges[i].dev_off + (staged_ranges[i].hi - staged_ranges[i].lo))
+                    continue;
+                written[i] += size_t(op.nf) * size_t(op.ns) * E;
+                if (((op.flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT) == COSTA_SCALE_AXPBY)
+                    reads_c[i] = true;
+            }
+        };
+        account(p.local_ops);
+        account(p.unpack_ops);
+        for (size_t i = 0; i < staged_ranges.size(); ++i) {
+            const hrange& r = staged_ranges[i];
+            const uint8_t f = range_flags[i];
+            const bool overwritten = f == 2 && !reads_c[i] && written[i] == r.hi - r.lo;
+            if ((f & 1) || ((f & 2) && !overwritten)) cp->h2d_ranges.push_back(r);
+            if (f & 2) cp->d2h_ranges.push_back(r);
+        }
+    }
     cp->tr_local = any_transpose(p.local_ops);
     cp->tr_unpack = any_transpose(p.unpack_ops);
-    cp->l_local = build_work(p.dtype, p.local_ops, w);
-    cp->n_local = int64_t(w.size());
-    cp->w_local.upload(w, dc.main);
-    cp->d_pack.upload(p.pack_ops, dc.main);
-    cp->l_pack = build_work(p.dtype, p.pack_ops, w);
-    cp->n_pack = int64_t(w.size());
-    cp->w_pack.upload(w, dc.main);
-    cp->d_unpack.upload(p.unpack_ops, dc.main);
-    cp->l_unpack = build_work(p.dtype, p.unpack_ops, w);
-    cp->n_unpack = int64_t(w.size());
-    cp->w_unpack.upload(w, dc.main);
+    std::vector<costa_tile_op_t> ord_l, ord_p, ord_u;
+    std::vector<uint64_t> w_l, w_p, w_u;
+    cp->l_local = build_work(p.dtype, p.local_ops, ord_l, w_l);
+    cp->l_pack = build_work(p.dtype, p.pack_ops, ord_p, w_p);
+    cp->l_unpack = build_work(p.dtype, p.unpack_ops, ord_u, w_u);
+    cp->d_local.upload(ord_l, dc.main);
+    cp->w_local.upload(w_l, dc.main);
+    cp->d_pack.upload(ord_p, dc.main);
+    cp->w_pack.upload(w_p, dc.main);
+    cp->d_unpack.upload(ord_u, dc.main);
+    cp->w_unpack.upload(w_u, dc.main);
     HIP_CHECK(hipStreamSynchronize(dc.main));  // host vectors above are temporaries
 
     g_plans.emplace_front(h.h, std::move(cp));
@@ -609,7 +749,7 @@ void transform(const std::vector<job>& jobs, comm* c, void* user_stream, bool as
     // H2D of host-resident data
     if (cp.staged) {
         tm.start(PH_H2D, dc.main);
-        for (const auto& r : cp.a_ranges)
+        for (const auto& r : cp.h2d_ranges)
             HIP_CHECK(hipMemcpyAsync(static_cast<char*>(cp.stage.p) + r.dev_off,
                                      reinterpret_cast<void*>(r.lo), r.hi - r.lo,
                                      hipMemcpyHostToDevice, dc.main));
@@ -623,13 +763,11 @@ void transform(const std::vector<job>& jobs, comm* c, void* user_stream, bool as
         HIP_CHECK(hipEventRecord(dc.ev_ready, dc.main));
         HIP_CHECK(hipStreamWaitEvent(dc.aux, dc.ev_ready, 0));
     }
-    if (cp.n_local) {
+    if (cp.l_local.n_items()) {
         tm.start(PH_LOCAL, ls);
         launch_tiles(p.dtype,
-                     {static_cast<const costa_tile_op_t*>(cp.d_local.p),
-                      static_cast<const uint64_t*>(cp.w_local.p), cp.n_local, cp.l_local.n_large,
-                      cp.l_local.n_small, nullptr,
-                      nullptr, cp.d_scal.p, cp.tr_local},
+                     make_launch(cp.l_local, cp.d_local.p, cp.w_local.p, nullptr, nullptr,
+                                 cp.d_scal.p, cp.tr_local),
                      ls);
         tm.stop();
     }
@@ -640,13 +778,11 @@ void transform(const std::vector<job>& jobs, comm* c, void* user_stream, bool as
         dc.recv.reserve(size_t(p.recv_elems) * E + 256);
         char* sb = static_cast<char*>(dc.send.p);
         char* rb = static_cast<char*>(dc.recv.p);
-        if (cp.n_pack) {
+        if (cp.l_pack.n_items()) {
             tm.start(PH_PACK, dc.main);
             launch_tiles(p.dtype,
-                         {static_cast<const costa_tile_op_t*>(cp.d_pack.p),
-                          static_cast<const uint64_t*>(cp.w_pack.p), cp.n_pack, cp.l_pack.n_large,
-                          cp.l_pack.n_small, nullptr,
-                          sb, cp.d_scal.p, false},
+                         make_launch(cp.l_pack, cp.d_pack.p, cp.w_pack.p, nullptr, sb, cp.d_scal.p,
+                                     false),
                          dc.main);
             tm.stop();
         }
@@ -664,13 +800,11 @@ void transform(const std::vector<job>& jobs, comm* c, void* user_stream, bool as
         }
         NCCL_CHECK(ncclGroupEnd());
         tm.stop();
-        if (cp.n_unpack) {
+        if (cp.l_unpack.n_items()) {
             tm.start(PH_UNPACK, dc.main);
             launch_tiles(p.dtype,
-                         {static_cast<const costa_tile_op_t*>(cp.d_unpack.p),
-                          static_cast<const uint64_t*>(cp.w_unpack.p), cp.n_unpack, cp.l_unpack.n_large,
-                          cp.l_unpack.n_small,
-                          rb, nullptr, cp.d_scal.p, cp.tr_unpack},
+                         make_launch(cp.l_unpack, cp.d_unpack.p, cp.w_unpack.p, rb, nullptr,
+                                     cp.d_scal.p, cp.tr_unpack),
                          dc.main);
             tm.stop();
         }
@@ -680,7 +814,7 @@ void transform(const std::vector<job>& jobs, comm* c, void* user_stream, bool as
     // D2H of the target data
     if (cp.staged) {
         tm.start(PH_D2H, dc.main);
-        for (const auto& r : cp.c_ranges)
+        for (const auto& r : cp.d2h_ranges)
             HIP_CHECK(hipMemcpyAsync(reinterpret_cast<void*>(r.lo),
                                      static_cast<char*>(cp.stage.p) + r.dev_off, r.hi - r.lo,
                                      hipMemcpyDeviceToHost, dc.main));
@@ -688,15 +822,15 @@ void transform(const std::vector<job>& jobs, comm* c, void* user_stream, bool as
     }
 
     g_stats.transforms++;
-    if (cp.n_local) {
+    if (cp.l_local.n_items()) {
         g_stats.local_launches++;
         g_stats.local_bytes += p.local_bytes;
     }
-    if (exchange && cp.n_pack) {
+    if (exchange && cp.l_pack.n_items()) {
         g_stats.pack_launches++;
         g_stats.pack_bytes += p.pack_bytes;
     }
-    if (exchange && cp.n_unpack) {
+    if (exchange && cp.l_unpack.n_items()) {
         g_stats.unpack_launches++;
         g_stats.unpack_bytes += p.unpack_bytes;
     }
@@ -721,19 +855,19 @@ void execute_tiles(costa_dtype_t dtype, const costa_tile_op_t* ops, int64_t n,
     for (const auto& op : v)
         if ((op.flags >> COSTA_SLOT_SHIFT) >= uint32_t(std::max(n_slots, 0)))
             throw error(COSTA_ERR_ARG, "costa_hip_execute_tiles: scalar slot out of range");
+    std::vector<costa_tile_op_t> ord;
     std::vector<uint64_t> w;
-    const work_split nl = build_work(dtype, v, w);
+    const work_split nl = build_work(dtype, v, ord, w);
     dbuf d_ops, d_work, d_scal;
-    d_ops.upload(v, dc.main);
+    d_ops.upload(ord, dc.main);
     d_work.upload(w, dc.main);
     const size_t E = dtype_size(dtype);
     std::vector<unsigned char> sc(static_cast<const unsigned char*>(scalars),
                                   static_cast<const unsigned char*>(scalars) + size_t(n_slots) * 2 * E);
     d_scal.upload(sc, dc.main);
     launch_tiles(dtype,
-                 {static_cast<const costa_tile_op_t*>(d_ops.p), static_cast<const uint64_t*>(d_work.p),
-                  int64_t(w.size()), nl.n_large, nl.n_small, static_cast<const char*>(src_base), static_cast<char*>(dst_base),
-                  d_scal.p, any_transpose(v)},
+                 make_launch(nl, d_ops.p, d_work.p, static_cast<const char*>(src_base),
+                             static_cast<char*>(dst_base), d_scal.p, any_transpose(v)),
                  dc.main);
     HIP_CHECK(hipStreamSynchronize(dc.main));
 }

@@ -119,11 +119,12 @@ constexpr int kTinyLdsBytes = 8192;
 constexpr int tiny_lds_bytes = kTinyLdsBytes;
 
 struct launch_args {
-    const costa_tile_op_t* ops;
-    const uint64_t* work;   // per item: (op index << 32) | sub-tile index
-    int64_t n_work;         // total work items: [large | small | tiny]
-    int64_t n_large;        // items using the large sub-tile shape
-    int64_t n_small;        // items using the small shape; the rest are tiny ops
+    const costa_tile_op_t* ops;  // device, in build_work order: [sub-tiled ops | tiny ops]
+    const uint64_t* work;   // per sub-tile: (op index << 32) | sub-tile index
+    int64_t n_large;        // work items using the large sub-tile shape
+    int64_t n_small;        // work items using the small shape (after the large ones)
+    int64_t tiny_first;     // ops[tiny_first, tiny_first + n_tiny) run one per wavefront
+    int64_t n_tiny;
     const char* src_base;
     char* dst_base;
     const void* scalars;    // device: n_slots x (alpha, beta) of the dtype
@@ -133,12 +134,18 @@ bool any_transpose(const std::vector<costa_tile_op_t>& ops);
 void launch_tiles(costa_dtype_t dtype, const launch_args& a, void* stream /* hipStream_t */);
 // sub-tile shapes (elements along the source's fast dim, along its slow dim)
 void tile_shapes(costa_dtype_t dtype, int* bf_large, int* bs_large, int* bf_small, int* bs_small);
-// work list of an op list: [large-shape sub-tiles | small-shape sub-tiles | tiny ops]
+// Execution order of an op list: `ordered` = [sub-tiled ops | tiny ops] (tiny ops sorted by
+// source address, so wavefronts running at the same time share partially used cache lines),
+// `work` = [large-shape sub-tiles | small-shape sub-tiles], indices into `ordered`.
 struct work_split {
-    int64_t n_large = 0, n_small = 0, n_tiny = 0;
+    int64_t n_large = 0, n_small = 0, tiny_first = 0, n_tiny = 0;
+    int64_t n_items() const { return n_large + n_small + n_tiny; }
 };
 work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops,
-                      std::vector<uint64_t>& work);
+                      std::vector<costa_tile_op_t>& ordered, std::vector<uint64_t>& work);
+// launch arguments of one ordered op list
+launch_args make_launch(const work_split& w, const void* d_ordered, const void* d_work,
+                        const char* src_base, char* dst_base, const void* d_scalars, bool transpose);
 
 // errors
 struct error : std::runtime_error {

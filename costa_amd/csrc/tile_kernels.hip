@@ -24,6 +24,9 @@
 // 91 % of the best flat 16-byte copy of the same bytes.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "engine.hpp"
 
 #pragma clang fp contract(off)
@@ -313,12 +316,15 @@ __global__ __launch_bounds__(S::NT) void tile_kernel(const costa_tile_op_t* __re
 }
 
 // ---------------------------------------------------------------- tiny ops
-// One wavefront per op (4 per workgroup).  Lanes walk the tile in linear order: source order
-// (f fastest) for loads, destination order for stores, with (f, s) advanced by a constant
-// per step (no per-element division).  Copy mode needs no LDS; transpose mode stages the tile
-// in the wave's own LDS region with an odd row pitch (conflict-free column reads).
+// One wavefront per op at a time (4 wavefronts per workgroup), each wavefront running K ops
+// with the next op's descriptor fetched before the current op's data.  Lanes walk the tile in
+// linear order: source order (f fastest) for loads, destination order for stores, with (f, s)
+// advanced by a constant per step (no per-element division).  Copy mode needs no LDS;
+// transpose mode stages the tile in the wave's own LDS region with an odd row pitch
+// (conflict-free column reads).
 // Measured motivation: BASELINE cfg 5 (242k tiles of ~33x33 fp32) ran at 1.8 TB/s with one
-// 256-thread workgroup per tile: too few bytes in flight per CU.
+// 256-thread workgroup per tile (too few bytes in flight per CU), 2.65 TB/s with one
+// wavefront per op (each op still waits on its own descriptor and scalar loads).
 constexpr int TINY_WAVES = 4;
 template <typename T>
 constexpr int tiny_unroll() { return 64 / int(sizeof(T)); }  // 64 bytes in flight per lane
@@ -343,21 +349,18 @@ struct lin {  // (f, s) of linear element index e = f + s*n, stepped by 64
 };
 
 template <typename T>
-__global__ __launch_bounds__(64 * TINY_WAVES) void tiny_kernel(
-    const costa_tile_op_t* __restrict__ ops, const uint64_t* __restrict__ work, int64_t n_items,
-    const char* src_base, char* dst_base, const T* __restrict__ scalars, int lds_per_wave) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int lane = int(threadIdx.x) % 64;
-    const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / 64);
-    const int64_t item = int64_t(blockIdx.x) * TINY_WAVES + wave;
-    if (item >= n_items) return;
-    const costa_tile_op_t op = ops[work[item] >> 32];
+__device__ __forceinline__ void tiny_op(const costa_tile_op_t& op, int lane, T* t,
+                                        const char* src_base, char* dst_base,
+                                        const T* __restrict__ scalars) {
     const uint32_t flags = op.flags;
     const uint32_t kind = (flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT;
     const bool conj = flags & COSTA_TILE_CONJ;
     const uint32_t slot = flags >> COSTA_SLOT_SHIFT;
-    const T alpha = scalars[2 * slot];
-    const T beta = scalars[2 * slot + 1];
+    T alpha = e_zero<T>(), beta = e_zero<T>();
+    if (kind >= COSTA_SCALE_ALPHA) {  // BITCOPY / ZERO never read the scalars
+        alpha = scalars[2 * slot];
+        beta = scalars[2 * slot + 1];
+    }
     const T* src = reinterpret_cast<const T*>(src_base + op.src);
     T* dst = reinterpret_cast<T*>(dst_base + op.dst);
     const int nf = op.nf, ns = op.ns, total = nf * ns;
@@ -365,7 +368,7 @@ __global__ __launch_bounds__(64 * TINY_WAVES) void tiny_kernel(
     constexpr int U = tiny_unroll<T>();
 
     if (!(flags & COSTA_TILE_TRANSPOSE)) {
-        // copy mode: dst(f, s) = g(src(f, s)), UNROLL independent loads in flight per lane
+        // copy mode: dst(f, s) = g(src(f, s)), U independent loads in flight per lane
         lin<T> p(lane, nf);
         for (int e0 = 0; e0 < total; e0 += 64 * U) {
             T x[U], y[U];
@@ -396,7 +399,6 @@ __global__ __launch_bounds__(64 * TINY_WAVES) void tiny_kernel(
         return;
     }
     // transpose mode: stage in LDS (pitch odd), then write in destination order
-    T* t = reinterpret_cast<T*>(smem) + int64_t(wave) * lds_per_wave;
     const int pitch = nf | 1;
     {
         lin<T> p(lane, nf);
@@ -448,22 +450,63 @@ __global__ __launch_bounds__(64 * TINY_WAVES) void tiny_kernel(
             }
         }
     }
+    // the next op of this wave overwrites the staging area: all lanes' reads are done first
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Wave w of the grid (W waves in all) runs ops w, w + W, w + 2W, ... (strided: the waves
+// resident at one time work on neighbouring ops of the address-sorted list), or, with
+// `chunked`, ops [w*K, w*K + K).
+template <typename T>
+__global__ __launch_bounds__(64 * TINY_WAVES) void tiny_kernel(
+    const costa_tile_op_t* __restrict__ ops, int64_t n_ops, int k_per_wave, int chunked,
+    const char* src_base, char* dst_base, const T* __restrict__ scalars, int lds_per_wave) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = int(threadIdx.x) % 64;
+    const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / 64);
+    const int64_t w = int64_t(blockIdx.x) * TINY_WAVES + wave;
+    const int64_t n_waves = int64_t(gridDim.x) * TINY_WAVES;
+    const int64_t first = chunked ? w * k_per_wave : w;
+    const int64_t step = chunked ? 1 : n_waves;
+    const int64_t end = chunked ? min(n_ops, first + k_per_wave) : n_ops;
+    if (first >= end) return;
+    T* t = reinterpret_cast<T*>(smem) + int64_t(wave) * lds_per_wave;
+    costa_tile_op_t next = ops[first];
+    for (int64_t i = first; i < end; i += step) {
+        const costa_tile_op_t op = next;
+        if (i + step < end) next = ops[i + step];  // in flight while this op moves its data
+        tiny_op<T>(op, lane, t, src_base, dst_base, scalars);
+    }
+}
+
+struct tiny_cfg {
+    int k = 4;        // ops per wavefront
+    int chunked = 0;  // 0: strided assignment, 1: contiguous chunks
+};
+const tiny_cfg& tiny_config() {  // COSTA_TINY_K / COSTA_TINY_CHUNKED override (tuning)
+    static tiny_cfg c = [] {
+        tiny_cfg x;
+        if (const char* s = std::getenv("COSTA_TINY_K")) x.k = std::max(1, std::atoi(s));
+        if (const char* s = std::getenv("COSTA_TINY_CHUNKED")) x.chunked = std::atoi(s) != 0;
+        return x;
+    }();
+    return c;
 }
 
 template <typename T>
 void launch_tiny(const launch_args& a, hipStream_t stream) {
-    const int64_t n = a.n_work - a.n_large - a.n_small;
+    const int64_t n = a.n_tiny;
     if (n <= 0) return;
-    const uint64_t* work = a.work + a.n_large + a.n_small;
+    const tiny_cfg& cfg = tiny_config();
     const int per_wave = a.any_transpose ? int(tiny_lds_bytes / sizeof(T)) : 0;
     const size_t lds = size_t(per_wave) * sizeof(T) * TINY_WAVES;
-    const int64_t max_items = (int64_t(1) << 30) * TINY_WAVES;
-    for (int64_t off = 0; off < n; off += max_items) {
-        const int64_t m = std::min(max_items, n - off);
-        hipLaunchKernelGGL(tiny_kernel<T>, dim3(unsigned((m + TINY_WAVES - 1) / TINY_WAVES)),
-                           dim3(64 * TINY_WAVES), lds, stream, a.ops, work + off, m, a.src_base,
-                           a.dst_base, static_cast<const T*>(a.scalars), per_wave);
-    }
+    const int64_t waves = (n + cfg.k - 1) / cfg.k;
+    const int64_t blocks = std::min<int64_t>((waves + TINY_WAVES - 1) / TINY_WAVES, 1LL << 30);
+    const int k = int((n + blocks * TINY_WAVES - 1) / (blocks * TINY_WAVES));  // covers all ops
+    hipLaunchKernelGGL(tiny_kernel<T>, dim3(unsigned(blocks)), dim3(64 * TINY_WAVES), lds, stream,
+                       a.ops + a.tiny_first, n, k, cfg.chunked, a.src_base, a.dst_base,
+                       static_cast<const T*>(a.scalars), per_wave);
 }
 
 template <typename T, typename S>
@@ -481,7 +524,7 @@ void launch_shape(const launch_args& a, const uint64_t* work, int64_t n, hipStre
 
 template <typename T>
 void launch_t(const launch_args& a, hipStream_t stream) {
-    // work list: [large sub-tiles | small sub-tiles | tiny ops]
+    // work list: [large sub-tiles | small sub-tiles], then the tiny ops
     launch_shape<T, typename shapes<T>::large>(a, a.work, a.n_large, stream);
     launch_shape<T, typename shapes<T>::small>(a, a.work + a.n_large, a.n_small, stream);
     launch_tiny<T>(a, stream);
@@ -517,7 +560,7 @@ void tile_shapes(costa_dtype_t dtype, int* bf_large, int* bs_large, int* bf_smal
 }
 
 void launch_tiles(costa_dtype_t dtype, const launch_args& a, void* stream) {
-    if (a.n_work <= 0) return;
+    if (a.n_large + a.n_small + a.n_tiny <= 0) return;
     static bool once = [] {
         set_lds_limits<float>();
         set_lds_limits<double>();

@@ -148,6 +148,30 @@ def test_golden_host_staged(gpu, case):
         assert matches(fx, f"C{k}_r0", got[k])
 
 
+@pytest.mark.parametrize("ld_pad,sub,beta", [(0, False, 0.0), (3, False, 0.0), (0, True, 0.0),
+                                             (0, False, 0.5)])
+def test_host_staged_c_upload_rules(gpu, ld_pad, sub, beta):
+    """The staged path skips uploading C ranges the kernels overwrite completely (beta = 0, no
+    ld padding, whole matrix).  Padding bytes, rows outside a sub-matrix and beta != 0 must
+    still see the caller's C: the whole host buffer is compared, padding included."""
+    m, n, b = 300, 200, 64
+    rng = np.random.default_rng(7)
+    a = rng.standard_normal(m * n)                     # A: m x n, col-major, ld m
+    ldc = n + ld_pad
+    c0 = rng.standard_normal(ldc * m)                  # C: n x m, col-major, ld n + pad
+    c = c0.copy()
+    sm, sn = (m - 40, n - 30) if sub else (m, n)       # sub(C) = op(sub(A)): sn x sm
+    LA = gpu.block_cyclic_layout(m, n, b, b, 1, 1, sm, sn, 1, 1, "R", 0, 0, a, m, "C", 0)
+    LC = gpu.block_cyclic_layout(n, m, b, b, 1, 1, sn, sm, 1, 1, "R", 0, 0, c, ldc, "C", 0)
+    gpu.transform(LA, LC, gpu.Comm.self(0), "T", 1.5, beta)
+    exp = c0.copy().reshape(m, ldc)                    # row j of exp = column j of C
+    at = a.reshape(n, m)[:sn, :sm]                     # at[j, i] = A(i, j) = op(A)(j, i)
+    cur = exp[:sm, :sn]
+    new = 1.5 * at.T if beta == 0 else beta * cur + 1.5 * at.T
+    exp[:sm, :sn] = new
+    assert np.array_equal(c.view(np.uint64), exp.reshape(-1).view(np.uint64))
+
+
 # ------------------------------------------------------------------ edge cases vs oracle
 def assert_bits_equal_or_both_nan(got, expected):
     """Bit-exact, except NaNs GENERATED by arithmetic (inf*0, inf-inf): x86 produces the
