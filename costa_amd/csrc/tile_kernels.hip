@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "engine.hpp"
 
@@ -315,19 +316,23 @@ __global__ __launch_bounds__(S::NT) void tile_kernel(const costa_tile_op_t* __re
         run_tile<T, S, false>(op, f0, s0, tf, ts, src_base, dst_base, alpha, beta, tile);
 }
 
-// ---------------------------------------------------------------- tiny ops
-// One wavefront per op at a time (4 wavefronts per workgroup), each wavefront running K ops
-// with the next op's descriptor fetched before the current op's data.  Lanes walk the tile in
-// linear order: source order (f fastest) for loads, destination order for stores, with (f, s)
-// advanced by a constant per step (no per-element division).  Copy mode needs no LDS;
+// ---------------------------------------------------------------- wavefront path
+// Every op below the large shape, cut on the host into wave-sized rectangles (engine.cpp
+// split_for_waves), runs on one wavefront; by default each wavefront runs one op (K = 1 beat
+// K = 2..16 on cfg 5: more resident wavefronts beat descriptor prefetch).  Lanes walk the tile
+// in linear order: source order (f fastest) for loads, destination order for stores, with
+// (f, s) advanced by a constant per step (no per-element division).  Copy mode needs no LDS;
 // transpose mode stages the tile in the wave's own LDS region with an odd row pitch
 // (conflict-free column reads).
-// Measured motivation: BASELINE cfg 5 (242k tiles of ~33x33 fp32) ran at 1.8 TB/s with one
-// 256-thread workgroup per tile (too few bytes in flight per CU), 2.65 TB/s with one
-// wavefront per op (each op still waits on its own descriptor and scalar loads).
-constexpr int TINY_WAVES = 4;
-template <typename T>
-constexpr int tiny_unroll() { return 64 / int(sizeof(T)); }  // 64 bytes in flight per lane
+// Measured on BASELINE cfg 5 (242k tiles of ~33x33 fp32, 'N'): 1.8 TB/s with one 256-thread
+// workgroup per tile (too few bytes in flight per CU), 2.65 TB/s with one wavefront per op,
+// 3.35-3.5 TB/s with the directly indexed, destination-sorted list and the host split.
+// Wavefronts per workgroup: 2 for lists that transpose (8 KiB of LDS per wavefront), 8 for
+// copy-only lists (no LDS).  Measured on cfg 5 (profiles/r06/c5_knobs.log): transposes 3.1-3.3
+// TB/s at 2 against 2.95 at 4; copies 3.40 at 8 against 3.36 at 4.
+constexpr int TINY_WAVES_TR = 2;
+constexpr int TINY_WAVES_COPY = 8;
+constexpr int TINY_BYTES = 64;  // bytes in flight per lane per pass
 
 template <typename T>
 struct lin {  // (f, s) of linear element index e = f + s*n, stepped by 64
@@ -348,7 +353,7 @@ struct lin {  // (f, s) of linear element index e = f + s*n, stepped by 64
     }
 };
 
-template <typename T>
+template <typename T, int UB>
 __device__ __forceinline__ void tiny_op(const costa_tile_op_t& op, int lane, T* t,
                                         const char* src_base, char* dst_base,
                                         const T* __restrict__ scalars) {
@@ -365,7 +370,7 @@ __device__ __forceinline__ void tiny_op(const costa_tile_op_t& op, int lane, T* 
     T* dst = reinterpret_cast<T*>(dst_base + op.dst);
     const int nf = op.nf, ns = op.ns, total = nf * ns;
     const int64_t lds = op.lds, ldd = op.ldd;
-    constexpr int U = tiny_unroll<T>();
+    constexpr int U = UB / int(sizeof(T)) > 0 ? UB / int(sizeof(T)) : 1;
 
     if (!(flags & COSTA_TILE_TRANSPOSE)) {
         // copy mode: dst(f, s) = g(src(f, s)), U independent loads in flight per lane
@@ -455,18 +460,26 @@ __device__ __forceinline__ void tiny_op(const costa_tile_op_t& op, int lane, T* 
     __builtin_amdgcn_wave_barrier();
 }
 
-// Wave w of the grid (W waves in all) runs ops w, w + W, w + 2W, ... (strided: the waves
-// resident at one time work on neighbouring ops of the address-sorted list), or, with
-// `chunked`, ops [w*K, w*K + K).
-template <typename T>
-__global__ __launch_bounds__(64 * TINY_WAVES) void tiny_kernel(
+// Wave w of the grid runs ops w, w + n_waves, ... (strided: the waves resident at one time
+// work on neighbouring ops of the address-sorted list), or, with `chunked`, ops [w*K, w*K + K).
+// `xcd_remap`: blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup
+// dispatch); renumbering them so that each XCD walks one contiguous slice of the list keeps
+// neighbouring ops (which share partially written cache lines) in one L2.
+template <typename T, int W, int UB>
+__global__ __launch_bounds__(64 * W) void tiny_kernel(
     const costa_tile_op_t* __restrict__ ops, int64_t n_ops, int k_per_wave, int chunked,
-    const char* src_base, char* dst_base, const T* __restrict__ scalars, int lds_per_wave) {
+    int xcd_remap, const char* src_base, char* dst_base, const T* __restrict__ scalars,
+    int lds_per_wave) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = int(threadIdx.x) % 64;
     const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / 64);
-    const int64_t w = int64_t(blockIdx.x) * TINY_WAVES + wave;
-    const int64_t n_waves = int64_t(gridDim.x) * TINY_WAVES;
+    int64_t b = blockIdx.x;
+    if (xcd_remap) {
+        const int64_t nb = gridDim.x, x = b % 8, i = b / 8, per = nb / 8, rem = nb % 8;
+        b = x < rem ? x * (per + 1) + i : rem * (per + 1) + (x - rem) * per + i;
+    }
+    const int64_t w = b * W + wave;
+    const int64_t n_waves = int64_t(gridDim.x) * W;
     const int64_t first = chunked ? w * k_per_wave : w;
     const int64_t step = chunked ? 1 : n_waves;
     const int64_t end = chunked ? min(n_ops, first + k_per_wave) : n_ops;
@@ -476,37 +489,60 @@ __global__ __launch_bounds__(64 * TINY_WAVES) void tiny_kernel(
     for (int64_t i = first; i < end; i += step) {
         const costa_tile_op_t op = next;
         if (i + step < end) next = ops[i + step];  // in flight while this op moves its data
-        tiny_op<T>(op, lane, t, src_base, dst_base, scalars);
+        tiny_op<T, UB>(op, lane, t, src_base, dst_base, scalars);
     }
 }
 
 struct tiny_cfg {
-    int k = 4;        // ops per wavefront
-    int chunked = 0;  // 0: strided assignment, 1: contiguous chunks
+    int k = 1;          // ops per wavefront
+    int chunked = 0;    // 0: strided assignment, 1: contiguous chunks
+    int waves = 0;      // 0: by list kind (TINY_WAVES_TR / TINY_WAVES_COPY)
+    int bytes = TINY_BYTES;
+    int xcd = 0;
 };
-const tiny_cfg& tiny_config() {  // COSTA_TINY_K / COSTA_TINY_CHUNKED override (tuning)
+const tiny_cfg& tiny_config() {  // COSTA_TINY_{K,CHUNKED,WAVES,BYTES,XCD}: tuning overrides
     static tiny_cfg c = [] {
         tiny_cfg x;
-        if (const char* s = std::getenv("COSTA_TINY_K")) x.k = std::max(1, std::atoi(s));
-        if (const char* s = std::getenv("COSTA_TINY_CHUNKED")) x.chunked = std::atoi(s) != 0;
+        auto env = [](const char* n, int d) {
+            const char* s = std::getenv(n);
+            return s ? std::atoi(s) : d;
+        };
+        x.k = std::max(1, env("COSTA_TINY_K", x.k));
+        x.chunked = env("COSTA_TINY_CHUNKED", x.chunked) != 0;
+        x.waves = env("COSTA_TINY_WAVES", x.waves);
+        x.bytes = env("COSTA_TINY_BYTES", x.bytes);
+        x.xcd = env("COSTA_TINY_XCD", x.xcd) != 0;
         return x;
     }();
     return c;
 }
 
+template <typename T, int W, int UB>
+void launch_tiny_v(const launch_args& a, const tiny_cfg& cfg, hipStream_t stream) {
+    const int64_t n = a.n_tiny;
+    const int per_wave = a.any_transpose ? int(tiny_lds_bytes / sizeof(T)) : 0;
+    const size_t lds = size_t(per_wave) * sizeof(T) * W;
+    const int64_t waves = (n + cfg.k - 1) / cfg.k;
+    const int64_t blocks = std::min<int64_t>((waves + W - 1) / W, 1LL << 30);
+    const int k = int((n + blocks * W - 1) / (blocks * W));  // chunked: covers all ops
+    hipLaunchKernelGGL((tiny_kernel<T, W, UB>), dim3(unsigned(blocks)), dim3(64 * W), lds, stream,
+                       a.ops + a.tiny_first, n, k, cfg.chunked, cfg.xcd, a.src_base, a.dst_base,
+                       static_cast<const T*>(a.scalars), per_wave);
+}
+
 template <typename T>
 void launch_tiny(const launch_args& a, hipStream_t stream) {
-    const int64_t n = a.n_tiny;
-    if (n <= 0) return;
+    if (a.n_tiny <= 0) return;
     const tiny_cfg& cfg = tiny_config();
-    const int per_wave = a.any_transpose ? int(tiny_lds_bytes / sizeof(T)) : 0;
-    const size_t lds = size_t(per_wave) * sizeof(T) * TINY_WAVES;
-    const int64_t waves = (n + cfg.k - 1) / cfg.k;
-    const int64_t blocks = std::min<int64_t>((waves + TINY_WAVES - 1) / TINY_WAVES, 1LL << 30);
-    const int k = int((n + blocks * TINY_WAVES - 1) / (blocks * TINY_WAVES));  // covers all ops
-    hipLaunchKernelGGL(tiny_kernel<T>, dim3(unsigned(blocks)), dim3(64 * TINY_WAVES), lds, stream,
-                       a.ops + a.tiny_first, n, k, cfg.chunked, a.src_base, a.dst_base,
-                       static_cast<const T*>(a.scalars), per_wave);
+    if constexpr (std::is_same<T, float>::value) {  // tuning variants (cfg 5 is fp32)
+        if (cfg.waves == 4 && cfg.bytes == 64) return launch_tiny_v<T, 4, 64>(a, cfg, stream);
+        if (cfg.waves == 4 && cfg.bytes == 32) return launch_tiny_v<T, 4, 32>(a, cfg, stream);
+        if (cfg.waves == 8 && cfg.bytes == 32) return launch_tiny_v<T, 8, 32>(a, cfg, stream);
+        if (cfg.waves == 4 && cfg.bytes == 128) return launch_tiny_v<T, 4, 128>(a, cfg, stream);
+    }
+    const int w = cfg.waves ? cfg.waves : (a.any_transpose ? TINY_WAVES_TR : TINY_WAVES_COPY);
+    if (w == TINY_WAVES_TR) return launch_tiny_v<T, TINY_WAVES_TR, TINY_BYTES>(a, cfg, stream);
+    launch_tiny_v<T, TINY_WAVES_COPY, TINY_BYTES>(a, cfg, stream);
 }
 
 template <typename T, typename S>

@@ -37,4 +37,30 @@ if [ "${PMC:-1}" = "1" ]; then
     step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o write --output-format csv \
         -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-e2e
 fi
+if [ "${CFG5:-1}" = "1" ]; then
+    for op in N T; do
+        C5="python3 bench.py --workload cfg5 --cfg5-op $op --no-cpu-baseline --no-e2e"
+        step c5${op}_bench 300 $C5 --steps 20 --warmup 3
+        step c5${op}_rocprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/c5${op}_prof" -o trace \
+            --output-format csv -- $C5 --steps 10 --warmup 2
+        if [ "${PMC:-1}" = "1" ]; then
+            step c5${op}_pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/c5${op}_pmc_fetch" -o fetch \
+                --output-format csv -- $C5 --steps 5 --warmup 1
+            step c5${op}_pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/c5${op}_pmc_write" -o write \
+                --output-format csv -- $C5 --steps 5 --warmup 1
+        fi
+    done
+fi
+if [ "${KNOBS:-0}" = "1" ]; then  # repeated A/B of wavefront-path variants on cfg 5
+    for rep in 1 2; do
+        for v in "T 4 64 0" "T 2 64 1" "T 2 64 0" "T 4 64 1" "N 4 64 0" "N 8 64 0" "N 8 64 1" "N 2 64 1"; do
+            set -- $v
+            COSTA_TINY_WAVES=$2 COSTA_TINY_BYTES=$3 COSTA_TINY_XCD=$4 timeout -k 10 300 python3 bench.py \
+                --workload cfg5 --cfg5-op $1 --steps 20 --warmup 3 --no-cpu-baseline --no-e2e \
+                > "$OUT/knob.log" 2>&1 || { echo "knob run failed"; exit 3; }
+            python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(sys.argv[2], d['value'], d['kernel_node_GBps'])" \
+                "$OUT/knob.log" "rep$rep op=$1 waves=$2 bytes=$3 xcd=$4" | tee -a "$OUT/c5_knobs.log"
+        done
+    done
+fi
 echo "done"

@@ -1,12 +1,22 @@
 #!/usr/bin/env python3
 """Copy one gpu_check.sh session's summaries from gpurun_out/<tag>/ into profiles/<tag>/ and
-derive the HBM traffic per launch of the tile kernel from the PMC passes, corrected as
-MI355X_MICROARCH.md prescribes for gfx950 (FETCH_SIZE reports half of a wide streaming read:
-double it; WRITE_SIZE exact for 16-B stores; both in KiB)."""
+derive the HBM traffic per launch phase from the PMC passes, corrected as MI355X_MICROARCH.md
+prescribes for gfx950 (FETCH_SIZE reports half of a wide streaming read: double it;
+WRITE_SIZE exact for 16-B stores; both in KiB).
+
+A bench step's phase may run several kernels (tile_kernel for large ops, tiny_kernel for the
+wavefront path): for each kernel name of the workload's element type the dispatches of its main
+grid are taken, the median per kernel is summed.  One json per workload:
+  pmc_tile_kernel.json  (default bench, BASELINE cfg 2)
+  pmc_cfg5_N.json / pmc_cfg5_T.json
+bench.py's measured_traffic() picks the file whose bytes_per_launch_alg equals its own.
+Caveat written into each file: the x2 FETCH correction is calibrated for 16-B-per-lane loads;
+the wavefront path of cfg 5 uses 4-B loads, for which it is uncalibrated."""
 import csv
 import json
 import os
 import shutil
+import statistics
 import sys
 
 tag = sys.argv[1]
@@ -14,32 +24,60 @@ src = os.path.join("gpurun_out", tag)
 dst = os.path.join("profiles", tag)
 os.makedirs(dst, exist_ok=True)
 for rel in ["prof/trace_kernel_stats.csv", "bench.log", "pytest_gpu.log", "smoke.log", "nproc.txt",
-            "gpu.txt"]:
+            "gpu.txt", "c5N_prof/trace_kernel_stats.csv", "c5T_prof/trace_kernel_stats.csv",
+            "c5N_bench.log", "c5T_bench.log", "c5_knobs.log"]:
     p = os.path.join(src, rel)
     if os.path.exists(p):
-        shutil.copy(p, os.path.join(dst, os.path.basename(rel)))
-out = {}
-for f, c in [("pmc_fetch/fetch_counter_collection.csv", "FETCH_SIZE"),
-             ("pmc_write/write_counter_collection.csv", "WRITE_SIZE")]:
-    p = os.path.join(src, f)
-    if not os.path.exists(p):
-        continue
-    rows = [r for r in csv.DictReader(open(p))
-            if "tile_kernel" in r["Kernel_Name"] and r["Counter_Name"] == c]
-    big = max(int(r["Grid_Size"]) for r in rows)  # the bench's dominant launch
-    vals = [float(r["Counter_Value"]) for r in rows if int(r["Grid_Size"]) == big]
-    out[c + "_KiB_per_launch"] = vals
-if out:
-    f = sorted(out.get("FETCH_SIZE_KiB_per_launch", [0]))
-    w = sorted(out.get("WRITE_SIZE_KiB_per_launch", [0]))
-    fm, wm = f[len(f) // 2], w[len(w) // 2]
-    out["hbm_bytes_per_launch_corrected"] = int((2 * fm + wm) * 1024)
+        name = rel.replace("/", "_") if rel.startswith("c5") else os.path.basename(rel)
+        shutil.copy(p, os.path.join(dst, name))
+
+
+def bench_line(path):
     try:
-        line = [l for l in open(os.path.join(src, "bench.log")) if l.startswith("{")][-1]
-        out["bytes_per_launch_alg"] = json.loads(line)["roofline"]["bytes_per_launch"]
+        return json.loads([l for l in open(path) if l.startswith("{")][-1])
     except Exception:
-        pass
-    out["correction"] = "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halving)"
-    json.dump(out, open(os.path.join(dst, "pmc_tile_kernel.json"), "w"), indent=1)
-    print(json.dumps({k: v for k, v in out.items() if not k.endswith("launch")}))
+        return None
+
+
+def phase_kib(csv_path, counter, dtype):
+    """sum over the phase's kernels (tile_kernel / tiny_kernel of `dtype`) of the median
+    counter value of each kernel's main-grid dispatches"""
+    rows = [r for r in csv.DictReader(open(csv_path)) if r["Counter_Name"] == counter]
+    total, per = 0.0, {}
+    for kname in ("tile_kernel", "tiny_kernel"):
+        rs = [r for r in rows if f"{kname}<{dtype}" in r["Kernel_Name"]]
+        if not rs:
+            continue
+        big = max(int(r["Grid_Size"]) for r in rs)
+        vals = [float(r["Counter_Value"]) for r in rs if int(r["Grid_Size"]) == big]
+        per[kname] = {"grid": big, "dispatches": len(vals), "median_KiB": statistics.median(vals)}
+        total += statistics.median(vals)
+    return total, per
+
+
+def derive(prefix, dtype, out_name):
+    f = os.path.join(src, f"{prefix}pmc_fetch/fetch_counter_collection.csv")
+    w = os.path.join(src, f"{prefix}pmc_write/write_counter_collection.csv")
+    if not (os.path.exists(f) and os.path.exists(w)):
+        return
+    fk, fper = phase_kib(f, "FETCH_SIZE", dtype)
+    wk, wper = phase_kib(w, "WRITE_SIZE", dtype)
+    out = {"FETCH_SIZE_KiB_per_phase": fk, "WRITE_SIZE_KiB_per_phase": wk,
+           "kernels_fetch": fper, "kernels_write": wper,
+           "hbm_bytes_per_launch_corrected": int((2 * fk + wk) * 1024),
+           "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halving; "
+                         "calibrated for 16-B/lane loads only)"}
+    d = bench_line(os.path.join(src, f"{prefix}pmc_fetch.log"))
+    if d:
+        out["bytes_per_launch_alg"] = d["roofline"]["bytes_per_launch"]
+        out["workload"] = d["config"]["workload"]
+        out["ratio_to_algorithmic"] = round(out["hbm_bytes_per_launch_corrected"] /
+                                            out["bytes_per_launch_alg"], 4)
+    json.dump(out, open(os.path.join(dst, out_name), "w"), indent=1)
+    print(out_name, json.dumps({k: v for k, v in out.items() if not k.startswith("kernels")}))
+
+
+derive("", "double", "pmc_tile_kernel.json")
+derive("c5N_", "float", "pmc_cfg5_N.json")
+derive("c5T_", "float", "pmc_cfg5_T.json")
 print("saved", dst)
