@@ -43,7 +43,7 @@ SCALE_BITCOPY, SCALE_ZERO, SCALE_ALPHA, SCALE_AXPBY = 0, 1, 2, 3
 # numpy view of costa_tile_op_t (40 bytes)
 TILE_OP_DTYPE = np.dtype([("src", "<u8"), ("dst", "<u8"), ("nf", "<i4"), ("ns", "<i4"),
                           ("lds", "<i4"), ("ldd", "<i4"), ("flags", "<u4"),
-                          ("reserved", "<u4")])
+                          ("order", "<u4")])
 
 
 class CostaError(RuntimeError):
@@ -75,7 +75,7 @@ class _Block(C.Structure):
 class TileOp(C.Structure):
     _fields_ = [("src", C.c_uint64), ("dst", C.c_uint64), ("nf", C.c_int32), ("ns", C.c_int32),
                 ("lds", C.c_int32), ("ldd", C.c_int32), ("flags", C.c_uint32),
-                ("reserved", C.c_uint32)]
+                ("order", C.c_uint32)]
 
 
 class PlanInfo(C.Structure):

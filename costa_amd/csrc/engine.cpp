@@ -241,7 +241,8 @@ struct wave_knobs {  // defaults, overridable for tuning runs
     int policy = 1;  // COSTA_WAVE_POLICY 0: only ops within the budget take the wave path (the
                      // rest: 256-thread small shape); 1: every op below the large threshold;
                      // 2: also large ops that are not 16-byte aligned on both sides
-    int sort = 2;    // COSTA_TINY_SORT 0: plan order, 1: by source, 2: by destination address
+    int sort = 3;    // COSTA_TINY_SORT 0: list order, 1: by source, 2: by destination address,
+                     // 3: by the planner's locality hint (costa_tile_op_t::order), else as 2
 };
 const wave_knobs& knobs() {
     static wave_knobs k = [] {
@@ -285,10 +286,15 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     }
     // ops are independent (disjoint destinations), so any order is valid; neighbours in
     // memory run at the same time and share the partially used cache lines at their edges
+    const bool hinted = std::any_of(tiny.begin(), tiny.end(),
+                                    [](const costa_tile_op_t& o) { return o.order != 0; });
     if (kn.sort == 1)
         std::stable_sort(tiny.begin(), tiny.end(), [](const costa_tile_op_t& a,
                                                       const costa_tile_op_t& b) { return a.src < b.src; });
-    else if (kn.sort == 2)
+    else if (kn.sort == 3 && hinted)
+        std::stable_sort(tiny.begin(), tiny.end(), [](const costa_tile_op_t& a,
+                                                      const costa_tile_op_t& b) { return a.order < b.order; });
+    else if (kn.sort >= 2)
         std::stable_sort(tiny.begin(), tiny.end(), [](const costa_tile_op_t& a,
                                                       const costa_tile_op_t& b) { return a.dst < b.dst; });
     work_split w;

@@ -160,6 +160,21 @@ void decompose(const view& sv, const view& dv, int tag, size_t elem, std::vector
 
 char upper(char c) { return char(std::toupper(static_cast<unsigned char>(c))); }
 
+// costa_tile_op_t::order = 1 + rank of the tile in column-major order of its target
+// coordinates (per tag): consecutive ranks walk down a column band, so each tile shares the
+// partially used cache lines at its edges with the next one, on the source side (same source
+// block) or on the destination side (same target block).
+void set_order(std::vector<costa_tile_op_t>& ops, const std::vector<const side_tile*>& at) {
+    std::vector<uint32_t> idx(ops.size());
+    for (size_t i = 0; i < idx.size(); ++i) idx[i] = uint32_t(i);
+    std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) {
+        const side_tile& x = *at[a];
+        const side_tile& y = *at[b];
+        return std::tie(x.tag, x.cols.start, x.rows.start) < std::tie(y.tag, y.cols.start, y.rows.start);
+    });
+    for (size_t r = 0; r < idx.size(); ++r) ops[idx[r]].order = uint32_t(r + 1);
+}
+
 }  // namespace
 
 uint32_t scale_kind(costa_dtype_t dtype, const scal& s, bool copy_mode, bool conj) {
@@ -256,6 +271,9 @@ std::unique_ptr<plan> make_plan(const std::vector<job>& jobs, int rank, int n_ra
         return int64_t(E) * n * (1 + (k != COSTA_SCALE_ZERO) + (k == COSTA_SCALE_AXPBY));
     };
 
+    // target coordinates of every op, for the locality hint (costa_tile_op_t::order)
+    std::vector<const side_tile*> at_pack, at_unpack, at_local;
+
     // ---- send side: local tiles stay, remote tiles are packed in sorted order ----
     std::vector<const side_tile*> local_src;
     int64_t off = 0;
@@ -270,6 +288,7 @@ std::unique_ptr<plan> make_plan(const std::vector<job>& jobs, int rank, int n_ra
         p->pack_ops.push_back(make_tile_op(m.n_rows, m.n_cols, uint64_t(m.ptr), m.ld, ti.a_cm,
                                            uint64_t(off) * E, 0, ti.a_cm, false, false,
                                            COSTA_SCALE_BITCOPY, 0, E));
+        at_pack.push_back(&m);
         p->send_counts[size_t(m.peer)] += n;
         off += n;
     }
@@ -293,6 +312,7 @@ std::unique_ptr<plan> make_plan(const std::vector<job>& jobs, int rank, int n_ra
         p->unpack_ops.push_back(make_tile_op(nr, nc, uint64_t(off) * E, 0, ti.a_cm, uint64_t(m.ptr),
                                              m.ld, ti.c_cm, ti.transpose, ti.conj,
                                              kind_of(ti, wt), uint32_t(m.tag), E));
+        at_unpack.push_back(&m);
         p->recv_counts[size_t(m.peer)] += n;
         off += n;
     }
@@ -311,6 +331,7 @@ std::unique_ptr<plan> make_plan(const std::vector<job>& jobs, int rank, int n_ra
         p->local_ops.push_back(make_tile_op(s.n_rows, s.n_cols, uint64_t(s.ptr), s.ld, ti.a_cm,
                                             uint64_t(d.ptr), d.ld, ti.c_cm, ti.transpose, ti.conj,
                                             kind_of(ti, wt), uint32_t(s.tag), E));
+        at_local.push_back(&d);
         p->local_elems += int64_t(s.n_rows) * s.n_cols;
     }
 
@@ -318,6 +339,9 @@ std::unique_ptr<plan> make_plan(const std::vector<job>& jobs, int rank, int n_ra
         p->send_displs[size_t(r)] = p->send_displs[size_t(r - 1)] + p->send_counts[size_t(r - 1)];
         p->recv_displs[size_t(r)] = p->recv_displs[size_t(r - 1)] + p->recv_counts[size_t(r - 1)];
     }
+    set_order(p->pack_ops, at_pack);
+    set_order(p->unpack_ops, at_unpack);
+    set_order(p->local_ops, at_local);
     for (auto& op : p->local_ops) p->local_bytes += op_bytes(op);
     for (auto& op : p->pack_ops) p->pack_bytes += op_bytes(op);
     for (auto& op : p->unpack_ops) p->unpack_bytes += op_bytes(op);

@@ -99,7 +99,10 @@ typedef struct {
     int32_t lds;
     int32_t ldd;
     uint32_t flags;
-    uint32_t reserved;
+    uint32_t order; /* locality hint: the executor may run ops in ascending `order` (ops are
+                       independent, so any order gives the same result); the planner sets
+                       the tile's rank in column-major order of its target coordinates, so
+                       tiles sharing partially used cache lines run together.  0 = none. */
 } costa_tile_op_t; /* 40 bytes */
 
 /* ---- library ---- */
