@@ -42,13 +42,14 @@ def grid_for(n: int):
 
 
 def measured_traffic(alg_bytes: int):
-    """HBM bytes per launch of this workload's dominant kernel, from the newest committed
-    rocprofv3 PMC pass of this same bench command (profiles/<tag>/pmc_tile_kernel.json,
-    written by tools/save_profiles.py with the gfx950 FETCH_SIZE correction).  PMC counters
-    cannot be read from inside this process, so they come from that separate pass."""
+    """HBM bytes per launch phase of this workload, from the newest committed rocprofv3 PMC
+    pass of this same bench command (profiles/<tag>/pmc_*.json, one per workload, written by
+    tools/save_profiles.py with the gfx950 FETCH_SIZE correction; matched on the algorithmic
+    bytes per launch).  PMC counters cannot be read from inside this process, so they come
+    from that separate pass."""
     import glob
     best = None
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_tile_kernel.json"))):
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_*.json"))):
         try:
             d = json.load(open(p))
         except Exception:
@@ -238,6 +239,11 @@ def main():
         costa.set_profiling(False)
         return el, st
 
+    # first call on these layouts: host planning + descriptor upload + kernels (plan-cache miss)
+    barrier()
+    t0 = time.perf_counter()
+    step_blocking()
+    first_call_ms = max_over_ranks(time.perf_counter() - t0) * 1e3
     for _ in range(args.warmup):
         step_blocking()
     if world == 1 and check:  # correctness of what we time
@@ -342,6 +348,7 @@ def main():
             "cpu_baseline": cpu,
             "e2e_host": e2e,
             "call_overhead_us": overhead_us,
+            "first_call_ms": round(first_call_ms, 2),  # plan-cache miss: planning + upload + kernels
             "blocking": {"ms_per_step": round(el_block / args.steps * 1e3, 4),
                          "GBps": round(total_bytes / el_block / 1e9, 2),
                          "note": "costa_hip_transform (reference semantics: host waits for C)"},

@@ -288,15 +288,17 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     // memory run at the same time and share the partially used cache lines at their edges
     const bool hinted = std::any_of(tiny.begin(), tiny.end(),
                                     [](const costa_tile_op_t& o) { return o.order != 0; });
-    if (kn.sort == 1)
-        std::stable_sort(tiny.begin(), tiny.end(), [](const costa_tile_op_t& a,
-                                                      const costa_tile_op_t& b) { return a.src < b.src; });
-    else if (kn.sort == 3 && hinted)
-        std::stable_sort(tiny.begin(), tiny.end(), [](const costa_tile_op_t& a,
-                                                      const costa_tile_op_t& b) { return a.order < b.order; });
-    else if (kn.sort >= 2)
-        std::stable_sort(tiny.begin(), tiny.end(), [](const costa_tile_op_t& a,
-                                                      const costa_tile_op_t& b) { return a.dst < b.dst; });
+    const int mode = kn.sort == 3 && !hinted ? 2 : kn.sort;
+    if (mode >= 1 && mode <= 3) {  // sort (key, index) pairs: stable, and cheap to move
+        std::vector<std::pair<uint64_t, uint32_t>> key(tiny.size());
+        for (size_t i = 0; i < tiny.size(); ++i)
+            key[i] = {mode == 1 ? tiny[i].src : mode == 2 ? tiny[i].dst : tiny[i].order,
+                      uint32_t(i)};
+        std::sort(key.begin(), key.end());
+        std::vector<costa_tile_op_t> sorted(tiny.size());
+        for (size_t i = 0; i < key.size(); ++i) sorted[i] = tiny[key[i].second];
+        tiny.swap(sorted);
+    }
     work_split w;
     w.n_large = int64_t(work.size());
     w.n_small = int64_t(small.size());

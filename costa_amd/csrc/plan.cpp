@@ -20,6 +20,8 @@
 #include <cctype>
 #include <complex>
 #include <cstring>
+#include <exception>
+#include <thread>
 
 namespace costa {
 namespace engine {
@@ -128,6 +130,7 @@ struct view {
 // decompose every local block of `src` (seen through `sv`) by the grid of `dst` (seen
 // through `dv`) and append the tiles (utils.hpp:26-115)
 void decompose(const view& sv, const view& dv, int tag, size_t elem, std::vector<side_tile>& out) {
+    out.reserve(out.size() + sv.L->blocks.size() * 4);
     const auto& drs = dv.rsplit();
     const auto& dcs = dv.csplit();
     if (sv.rsplit().back() != drs.back() || sv.csplit().back() != dcs.back())
@@ -165,14 +168,16 @@ char upper(char c) { return char(std::toupper(static_cast<unsigned char>(c))); }
 // partially used cache lines at its edges with the next one, on the source side (same source
 // block) or on the destination side (same target block).
 void set_order(std::vector<costa_tile_op_t>& ops, const std::vector<const side_tile*>& at) {
-    std::vector<uint32_t> idx(ops.size());
-    for (size_t i = 0; i < idx.size(); ++i) idx[i] = uint32_t(i);
-    std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) {
-        const side_tile& x = *at[a];
-        const side_tile& y = *at[b];
-        return std::tie(x.tag, x.cols.start, x.rows.start) < std::tie(y.tag, y.cols.start, y.rows.start);
-    });
-    for (size_t r = 0; r < idx.size(); ++r) ops[idx[r]].order = uint32_t(r + 1);
+    // packed key (tag:16 | col start:24 | row start:24; matrix edges < 2^24) + index
+    std::vector<std::pair<uint64_t, uint32_t>> k(ops.size());
+    for (size_t i = 0; i < k.size(); ++i) {
+        const side_tile& t = *at[i];
+        k[i] = {(uint64_t(uint32_t(t.tag)) << 48) | (uint64_t(uint32_t(t.cols.start)) << 24) |
+                    uint64_t(uint32_t(t.rows.start)),
+                uint32_t(i)};
+    }
+    std::sort(k.begin(), k.end());
+    for (size_t r = 0; r < k.size(); ++r) ops[k[r].second].order = uint32_t(r + 1);
 }
 
 }  // namespace
@@ -248,11 +253,43 @@ std::unique_ptr<plan> make_plan(const std::vector<job>& jobs, int rank, int n_ra
         tags.push_back({tr, cj, jb.A->ordering == 'C', jb.C->ordering == 'C',
                         scale_kind(p->dtype, jb.s, true, cj), scale_kind(p->dtype, jb.s, false, cj)});
         p->slots.push_back(jb.s);
-        decompose(view{jb.A, tr}, view{jb.C, false}, int(t), E, send);  // prepare_to_send
-        decompose(view{jb.C, false}, view{jb.A, tr}, int(t), E, recv);  // prepare_to_recv
     }
-    std::sort(send.begin(), send.end(), key_less);
-    std::sort(recv.begin(), recv.end(), key_less);
+    // prepare_to_send and prepare_to_recv are independent: the receive side runs on a second
+    // thread when there are enough blocks to pay for it
+    auto side = [&](bool send_side, std::vector<side_tile>& out) {
+        for (size_t t = 0; t < jobs.size(); ++t) {
+            const job& jb = jobs[t];
+            const bool tr = tags[t].transpose;
+            if (send_side)
+                decompose(view{jb.A, tr}, view{jb.C, false}, int(t), E, out);  // prepare_to_send
+            else
+                decompose(view{jb.C, false}, view{jb.A, tr}, int(t), E, out);  // prepare_to_recv
+        }
+        std::sort(out.begin(), out.end(), key_less);
+    };
+    size_t n_blocks = 0;
+    for (const job& jb : jobs) n_blocks += jb.A->blocks.size() + jb.C->blocks.size();
+    if (n_blocks >= 4096) {
+        std::exception_ptr err;
+        std::thread th([&] {
+            try {
+                side(false, recv);
+            } catch (...) {
+                err = std::current_exception();
+            }
+        });
+        try {
+            side(true, send);
+        } catch (...) {
+            th.join();
+            throw;
+        }
+        th.join();
+        if (err) std::rethrow_exception(err);
+    } else {
+        side(true, send);
+        side(false, recv);
+    }
 
     p->send_counts.assign(size_t(n_ranks), 0);
     p->recv_counts.assign(size_t(n_ranks), 0);
