@@ -358,6 +358,130 @@ __global__ __launch_bounds__(NT) void v_gen_persist(const op_t* ops, const uint6
     }
 }
 
+
+// ----------------------------------------------------------------------------------
+// V7: copy-shaped transpose: 128 (f) x 32 (s) fp64 per 256-thread WG (32 KiB, like the best
+// flat copy's one 32 KiB chunk per WG); 4 WGs per CU interleave load and store phases.
+// Store: half-waves of 32 lanes cover the 32 s values of one row pair (pair exchange).
+template <int NTL>
+__global__ __launch_bounds__(256) void v_copyshape(const op_t* ops, const uint64_t* work) {
+    constexpr int BF = 128, BS = 32, NT = 256, P = BF + 2;
+    __shared__ __attribute__((aligned(16))) double tile[BS * P];
+    const uint64_t w = work[blockIdx.x];
+    const op_t op = ops[w >> 32];
+    const uint32_t sub = uint32_t(w);
+    const int nbf = op.nf / BF;
+    const int f0 = int(sub % nbf) * BF, s0 = int(sub / nbf) * BS;
+    const double* src = reinterpret_cast<const double*>(op.src) + int64_t(s0) * op.lds + f0;
+    double* dst = reinterpret_cast<double*>(op.dst) + int64_t(f0) * op.ldd + s0;
+    constexpr int LPC = BF / 2, CPP = NT / LPC, PL = BS / CPP;  // 64 lanes/col, 4 cols, 8 passes
+    const int lf = (threadIdx.x % LPC) * 2, c0 = threadIdx.x / LPC;
+    d2 x[PL];
+#pragma unroll
+    for (int k = 0; k < PL; ++k) {
+        const d2* p = reinterpret_cast<const d2*>(src + int64_t(c0 + CPP * k) * op.lds + lf);
+        x[k] = NTL ? __builtin_nontemporal_load(p) : *p;
+    }
+#pragma unroll
+    for (int k = 0; k < PL; ++k) *reinterpret_cast<d2*>(&tile[(c0 + CPP * k) * P + lf]) = x[k];
+    __syncthreads();
+    // 64 row pairs; a wave does 2 per pass (one per half), 4 waves -> 8 passes
+    const int lane = threadIdx.x % 64, wave = threadIdx.x / 64;
+    const int half = lane / 32, sl = lane % 32;
+    const bool odd = sl & 1;
+    constexpr int PS = (BF / 2) / (2 * (NT / 64));
+    d2 y[PS];
+#pragma unroll
+    for (int k = 0; k < PS; ++k) {
+        const int rp = 2 * (wave + 4 * k) + half;
+        y[k] = *reinterpret_cast<const d2*>(&tile[sl * P + 2 * rp]);
+    }
+#pragma unroll
+    for (int k = 0; k < PS; ++k) {
+        const int rp = 2 * (wave + 4 * k) + half;
+        d2 v = y[k];
+        double got = __shfl_xor(odd ? v.x : v.y, 1);
+        d2 o;
+        if (!odd) { o.x = v.x; o.y = got; } else { o.x = got; o.y = v.y; }
+        *reinterpret_cast<d2*>(dst + int64_t(2 * rp + (odd ? 1 : 0)) * op.ldd + (sl & ~1)) = o;
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// V6: persistent, double-buffered LDS filled by global_load_lds_dwordx4: a 128 (f) x 64 (s)
+// fp64 sub-tile per buffer, one 1 KiB source column per wave instruction into one padded LDS
+// row; the next sub-tile's loads are in flight while the current one is stored.
+template <int NTL>
+__global__ __launch_bounds__(512) void v_glds(const op_t* ops, const uint64_t* work, int64_t n) {
+    constexpr int BF = 128, BS = 64, NT = 512, P = BF + 2;
+    extern __shared__ __attribute__((aligned(16))) double lds_buf[];  // 2 x BS x P
+    const int lane = threadIdx.x % 64;
+    const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / 64);
+    constexpr int NW = NT / 64, CPW = BS / NW;  // columns per wave per tile
+    auto geo = [&](int64_t wi, const double*& src, double*& dst, int& ld_s, int& ld_d) {
+        const uint64_t w = work[wi];
+        const op_t op = ops[w >> 32];
+        const uint32_t sub = uint32_t(w);
+        const int nbf = op.nf / BF;
+        const int f0 = int(sub % nbf) * BF, s0 = int(sub / nbf) * BS;
+        src = reinterpret_cast<const double*>(op.src) + int64_t(s0) * op.lds + f0;
+        dst = reinterpret_cast<double*>(op.dst) + int64_t(f0) * op.ldd + s0;
+        ld_s = op.lds;
+        ld_d = op.ldd;
+    };
+    auto issue = [&](const double* src, int ld_s, int b) {
+#pragma unroll
+        for (int k = 0; k < CPW; ++k) {
+            const int c = wave + NW * k;
+            const double* g = src + int64_t(c) * ld_s + 2 * lane;
+            __builtin_amdgcn_global_load_lds(
+                (__attribute__((address_space(1))) void*)(g),
+                (__attribute__((address_space(3))) void*)(&lds_buf[(b * BS + c) * P]), 16, 0,
+                NTL ? 2 : 0);
+        }
+    };
+    int64_t i = blockIdx.x;
+    if (i >= n) return;
+    const double* src;
+    double* dst;
+    int ls, ld;
+    geo(i, src, dst, ls, ld);
+    issue(src, ls, 0);
+    int b = 0;
+    constexpr int RP = BF / 2, PS = RP / NW;  // row pairs per wave (BS = 64 = one wave of s)
+    const bool odd = lane & 1;
+    while (true) {
+        const int64_t nxt = i + gridDim.x;
+        double* cdst = dst;
+        const int cld = ld;
+        __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0): own DMA + stores done
+        __syncthreads();
+        if (nxt < n) {
+            geo(nxt, src, dst, ls, ld);
+            issue(src, ls, b ^ 1);
+        }
+        const double* t = &lds_buf[b * BS * P];
+        d2 y[PS];
+#pragma unroll
+        for (int k = 0; k < PS; ++k) {
+            const int rp = wave + NW * k;
+            y[k] = *reinterpret_cast<const d2*>(&t[lane * P + 2 * rp]);
+        }
+#pragma unroll
+        for (int k = 0; k < PS; ++k) {
+            const int rp = wave + NW * k;
+            d2 v = y[k];
+            double got = __shfl_xor(odd ? v.x : v.y, 1);
+            d2 o;
+            if (!odd) { o.x = v.x; o.y = got; } else { o.x = got; o.y = v.y; }
+            *reinterpret_cast<d2*>(cdst + int64_t(2 * rp + (odd ? 1 : 0)) * cld + (lane & ~1)) = o;
+        }
+        if (nxt >= n) break;
+        i = nxt;
+        b ^= 1;
+    }
+}
+
 // ----------------------------------------------------------------------------------
 // ceiling: flat 16-B copy of the same bytes (grid-stride)
 __global__ __launch_bounds__(256) void v_copy(const d2* a, d2* c, int64_t n) {
@@ -454,6 +578,7 @@ int main(int argc, char** argv) {
     auto w64 = mkwork(64), w128 = mkwork(128);
     auto w64x = mkwork(64, 64, true);
     auto g128x64 = mkwork(64, 128), g128x128 = mkwork(128, 128), g64x128 = mkwork(128, 64);
+    auto g128x32 = mkwork(32, 128);
     unsigned long long* bad;
     CK(hipMalloc(&bad, 8));
     hipEvent_t e0, e1;
@@ -502,6 +627,15 @@ int main(int argc, char** argv) {
     }
     V.push_back({"gpersist 64x64 t256 x4", [&] { hipLaunchKernelGGL((v_gen_persist<64, 64, 256>), dim3(cus * 4), dim3(256), 0, 0, d_ops, w64.first, w64.second); }, true, {}});
     V.push_back({"gen 128x128 t512", [&] { hipLaunchKernelGGL((v_gen<128, 128, 512, 0>), dim3(g128x128.second), dim3(512), 0, 0, d_ops, g128x128.first); }, true, {}});
+    V.push_back({"copyshape 128x32 t256", [&] { hipLaunchKernelGGL((v_copyshape<0>), dim3(g128x32.second), dim3(256), 0, 0, d_ops, g128x32.first); }, true, {}});
+    V.push_back({"copyshape 128x32 t256 nt-load", [&] { hipLaunchKernelGGL((v_copyshape<1>), dim3(g128x32.second), dim3(256), 0, 0, d_ops, g128x32.first); }, true, {}});
+    {
+        const int glds_bytes = 2 * 64 * 130 * 8;
+        CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&v_glds<0>), hipFuncAttributeMaxDynamicSharedMemorySize, glds_bytes));
+        CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&v_glds<1>), hipFuncAttributeMaxDynamicSharedMemorySize, glds_bytes));
+        V.push_back({"glds 128x64 t512 x1", [&, glds_bytes] { hipLaunchKernelGGL((v_glds<0>), dim3(cus), dim3(512), glds_bytes, 0, d_ops, g128x64.first, g128x64.second); }, true, {}});
+        V.push_back({"glds 128x64 t512 x1 nt-load", [&, glds_bytes] { hipLaunchKernelGGL((v_glds<1>), dim3(cus), dim3(512), glds_bytes, 0, d_ops, g128x64.first, g128x64.second); }, true, {}});
+    }
     const int64_t n2 = int64_t(n) * n / 2;
     for (int g : {2, 4, 8, 32}) {
         V.push_back({"copy U8 grid " + std::to_string(g) + "/CU", [&, g] { hipLaunchKernelGGL((v_copy_ilp<8, 0, 0>), dim3(cus * g), dim3(256), 0, 0, (const d2*)A, (d2*)Cm, n2); }, false, {}});
@@ -514,6 +648,23 @@ int main(int argc, char** argv) {
     V.push_back({"read-only 2GiB x2 (as 4GiB)", [&] { hipLaunchKernelGGL((v_read<8>), dim3(cus * 8), dim3(256), 0, 0, (const d2*)A, n2, (d2*)Cm); hipLaunchKernelGGL((v_read<8>), dim3(cus * 8), dim3(256), 0, 0, (const d2*)Cm, n2, (d2*)A); }, false, {}});
     V.push_back({"write-only 2GiB x2 (as 4GiB)", [&] { hipLaunchKernelGGL((v_write<8>), dim3(cus * 8), dim3(256), 0, 0, (d2*)Cm, n2); hipLaunchKernelGGL((v_write<8>), dim3(cus * 8), dim3(256), 0, 0, (d2*)Cm, n2); }, false, {}});
 
+    if (argc > 2) {  // keep variants whose name contains one of the comma-separated tokens
+        std::vector<std::string> toks;
+        std::string f = argv[2];
+        for (size_t a = 0, b; a <= f.size(); a = b + 1) {
+            b = f.find(',', a);
+            if (b == std::string::npos) b = f.size();
+            if (b > a) toks.push_back(f.substr(a, b - a));
+        }
+        std::vector<var> keep;
+        for (auto& v : V)
+            for (auto& t : toks)
+                if (v.name.find(t) != std::string::npos) {
+                    keep.push_back(v);
+                    break;
+                }
+        V.swap(keep);
+    }
     for (auto& v : V) {  // warm + verify
         CK(hipMemset(Cm, 0, sizeof(double) * n * n));
         v.run();
