@@ -1,4 +1,4 @@
-"""The N > 1 path on the CPU: one process per rank (torch.distributed, gloo, world size 2).
+"""The N > 1 path on the CPU: one process per rank (torch.distributed, gloo, world size 2-4).
 
 Each rank plans its own transform with the product planner (costa_hip_plan_export), packs with
 the oracle executor, exchanges the packed segments with all_to_all_single using exactly the
@@ -17,7 +17,7 @@ import torch.multiprocessing as mp  # noqa: E402
 
 from cases import all_cases  # noqa: E402
 
-CASES2 = [c.name for c in all_cases() if c.P == 2]
+CASES = {p: [c.name for c in all_cases() if c.P == p] for p in (2, 3, 4)}
 
 
 def _free_port():
@@ -77,11 +77,14 @@ def _worker(rank, world, port, names, result_dir):
     dist.destroy_process_group()
 
 
-def test_two_ranks_gloo(tmp_path):
-    assert CASES2, "no 2-rank golden cases"
-    mp.spawn(_worker, args=(2, _free_port(), CASES2, str(tmp_path)), nprocs=2, join=True)
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_ranks_gloo(tmp_path, world):
+    """every golden case of `world` ranks (grids 1x2 .. 2x2, remaps, custom grids, batches)"""
+    names = CASES[world]
+    assert names, f"no {world}-rank golden cases"
+    mp.spawn(_worker, args=(world, _free_port(), names, str(tmp_path)), nprocs=world, join=True)
     bad = []
-    for r in range(2):
+    for r in range(world):
         txt = (tmp_path / f"rank{r}.txt").read_text().strip()
         if txt:
             bad += txt.splitlines()
