@@ -90,6 +90,33 @@ def cpu_baseline(n=16384, b=256, slab_cols=2048, target_s=10.0):
                       f"oracle_transform_tiles, OpenMP {threads} threads, verified={ok}"}
 
 
+def cpu_baseline_reference(n=16384, b=256, slab_cols=2048, target_s=10.0):
+    """The REFERENCE itself on the host cores: oracle/_ref/ref_harness (eth-cscs/COSTA compiled
+    from its own sources by oracle/Makefile; the binary travels with the repo snapshot) runs
+    costa::transform 'T' (alpha 1, beta 0) on a 16384 x 2048 fp64 slab in 256^2 blocks (the
+    same 512 tiles as cpu_baseline) for ~target_s seconds.  Started as a child process before
+    this process touches the GPU.  None when the binary is absent."""
+    import subprocess
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(exe):
+        return None
+    threads = min(16, os.cpu_count() or 1)
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+    try:
+        r = subprocess.run([exe, "bench", str(n), str(slab_cols), str(b), str(target_s)],
+                           capture_output=True, text=True, timeout=6 * target_s + 120, env=env)
+        d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    except Exception:
+        return None
+    if r.returncode != 0 or not d.get("verified"):
+        return None
+    return {"value": round(d["GBps"], 3), "unit": "GB/s", "cores": d["threads"], "kind": "reference",
+            "sample": f"{n}x{slab_cols} fp64 slab, {b}x{b} blocks on one rank: the reference's "
+                      f"costa::transform 'T' (alpha=1, beta=0; planning included, as every "
+                      f"reference call re-plans), {d['reps']} calls in {d['seconds']:.1f} s, "
+                      f"OpenMP {d['threads']} threads, verified C == A^T"}
+
+
 def cfg5_workload(costa, torch, rank, world, op):
     """BASELINE configs[4]: fp32 16384^2 custom_layout; A tile edges uniform in
     [8, 96] (seeds 0xC5A1 rows / 0xC5A2 cols), C edges uniform in [16, 160] (0xC5A3 / 0xC5A4),
@@ -158,6 +185,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "pxtran"
+    # the reference's own CPU path, as a child process before anything touches the GPU
+    cpu_ref = cpu_baseline_reference(n=args.edge, b=args.block) if want_cpu else None
     import torch
     import torch.distributed as dist
     import costa_amd as costa
@@ -320,8 +350,11 @@ def main():
         overhead_us = round((time.perf_counter() - t1) / 200 * 1e6, 1)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "pxtran":
-        cpu = cpu_baseline(n=n, b=b)
+    if want_cpu:
+        port = cpu_baseline(n=n, b=b)  # our restatement of the tile loop (oracle/), same tiles
+        cpu = cpu_ref or port
+        if cpu_ref:
+            cpu["port"] = {k: port[k] for k in ("value", "cores", "kind", "sample")}
 
     if rank == 0:
         cfg = {"workload": wl, "op": op, "alpha": al, "beta": be,

@@ -7,6 +7,12 @@
 //                                        tests/unit/test_utils.cpp, inputs + outputs dumped
 //   ref_harness case <spec> <outdir>     one transform case (spec written by
 //                                        make_fixtures.py); every rank dumps its C buffer
+//   ref_harness bench <m> <n> <nb> <s>   CPU baseline: the reference's own transform 'T'
+//                                        (alpha 1, beta 0) of an m x n fp64 matrix in nb x nb
+//                                        blocks on one rank, repeated for ~s seconds (OpenMP
+//                                        threads: OMP_NUM_THREADS); prints one JSON line.
+//                                        Run by bench.py (cpu_baseline, rank 0, N = 1) on the
+//                                        GPU box as a child process, as the timed baseline.
 #include <costa/layout.hpp>
 #include <costa/grid2grid/transform.hpp>
 #include <costa/grid2grid/transformer.hpp>
@@ -14,6 +20,9 @@
 #include <costa/grid2grid/workspace.hpp>
 #include <mpi.h>
 
+#include <omp.h>
+
+#include <chrono>
 #include <complex>
 #include <cstdint>
 #include <cstdio>
@@ -225,6 +234,36 @@ int run_kat(const std::string& out) {
     return 0;
 }
 
+int run_bench(int m, int n, int nb, double seconds) {
+    std::vector<double> a(size_t(m) * n), c(size_t(n) * m, 0.0);
+    for (size_t k = 0; k < a.size(); ++k) a[k] = gen<double>(0xC057A0, 0, k);
+    auto A = costa::block_cyclic_layout<double>(m, n, nb, nb, 1, 1, m, n, 1, 1, 'R', 0, 0,
+                                                a.data(), m, 'C', 0);
+    auto C = costa::block_cyclic_layout<double>(n, m, nb, nb, 1, 1, n, m, 1, 1, 'R', 0, 0,
+                                                c.data(), n, 'C', 0);
+    costa::transform<double>(A, C, 'T', 1.0, 0.0, MPI_COMM_WORLD);  // warm-up: first touch
+    int reps = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    double el = 0;
+    do {
+        costa::transform<double>(A, C, 'T', 1.0, 0.0, MPI_COMM_WORLD);
+        ++reps;
+        el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    } while (el < seconds && reps < 100000);
+    bool ok = true;
+    for (int j = 0; j < n && ok; ++j)
+        for (int i = 0; i < m; ++i)
+            if (c[size_t(i) * n + j] != a[size_t(j) * m + i]) {
+                ok = false;
+                break;
+            }
+    const double bytes = 2.0 * sizeof(double) * double(m) * n;  // read A + write C
+    std::printf("{\"GBps\": %.3f, \"reps\": %d, \"seconds\": %.3f, \"threads\": %d, "
+                "\"verified\": %s}\n",
+                bytes * reps / el / 1e9, reps, el, omp_get_max_threads(), ok ? "true" : "false");
+    return ok ? 0 : 1;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -247,8 +286,13 @@ int main(int argc, char** argv) {
         case 3: rc = run_case<std::complex<double>>(in, argv[3], rank, P); break;
         default: break;  // the reference instantiates transform for the 4 FP types only
         }
+    } else if (argc >= 6 && std::string(argv[1]) == "bench") {
+        rc = rank == 0 ? run_bench(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]),
+                                   std::atof(argv[5]))
+                       : 0;
     } else {
-        if (rank == 0) std::cerr << "usage: ref_harness kat <out> | case <spec> <out>\n";
+        if (rank == 0)
+            std::cerr << "usage: ref_harness kat <out> | case <spec> <out> | bench <m> <n> <nb> <s>\n";
     }
     MPI_Finalize();
     return rc;
