@@ -143,7 +143,8 @@ int device_count() {
     return n;
 }
 
-comm* comm_self(int device) {
+namespace {
+comm* new_comm(int device) {
     const int n = device_count();
     if (device < 0 || device >= n) throw error(COSTA_ERR_ARG, "costa: device index out of range");
     auto* c = new comm;
@@ -151,22 +152,44 @@ comm* comm_self(int device) {
     return c;
 }
 
-comm* comm_create(const unsigned char* id, int nranks, int rank, int device) {
-    if (nranks < 1 || rank < 0 || rank >= nranks) throw error(COSTA_ERR_ARG, "costa: bad rank/size");
-    auto* c = comm_self(device);
-    c->rank = rank;
-    c->size = nranks;
-    if (nranks > 1) {
-        HIP_CHECK(hipSetDevice(device));
+void init_nccl(comm* c, const ncclUniqueId& uid, int nranks, int rank, const char* what) {
+    HIP_CHECK(hipSetDevice(c->device));
+    ncclResult_t r = ncclCommInitRank(&c->nccl, nranks, uid, rank);
+    if (r != ncclSuccess) {
+        delete c;
+        throw error(COSTA_ERR_NCCL, std::string(what) + ": " + ncclGetErrorString(r));
+    }
+}
+}  // namespace
+
+comm* comm_self(int device) {
+    comm* c = new_comm(device);
+    if (loopback_exchange()) {  // test mode: a real one-rank RCCL communicator
         ncclUniqueId uid;
-        std::memcpy(uid.internal, id, NCCL_UNIQUE_ID_BYTES);
-        ncclResult_t r = ncclCommInitRank(&c->nccl, nranks, uid, rank);
-        if (r != ncclSuccess) {
-            delete c;
-            throw error(COSTA_ERR_NCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
-        }
+        NCCL_CHECK(ncclGetUniqueId(&uid));
+        init_nccl(c, uid, 1, 0, "loopback ncclCommInitRank");
     }
     return c;
+}
+
+comm* comm_create(const unsigned char* id, int nranks, int rank, int device) {
+    if (nranks < 1 || rank < 0 || rank >= nranks) throw error(COSTA_ERR_ARG, "costa: bad rank/size");
+    if (nranks == 1) return comm_self(device);
+    comm* c = new_comm(device);
+    c->rank = rank;
+    c->size = nranks;
+    ncclUniqueId uid;
+    std::memcpy(uid.internal, id, NCCL_UNIQUE_ID_BYTES);
+    init_nccl(c, uid, nranks, rank, "ncclCommInitRank");
+    return c;
+}
+
+bool loopback_exchange() {
+    static const bool on = [] {
+        const char* s = std::getenv("COSTA_LOOPBACK");
+        return s && std::atoi(s) != 0;
+    }();
+    return on;
 }
 
 int comm_rank(const comm* c) { return c->rank; }
@@ -576,7 +599,7 @@ cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
             }
         }
     }
-    cp->p = make_plan(pj, c->rank, c->size);
+    cp->p = make_plan(pj, c->rank, c->size, c->size == 1 && c->nccl != nullptr);
     const plan& p = *cp->p;
     if (cp->staged) {
         // A C-only range needs no upload when the kernels overwrite every byte of it: one job's
@@ -764,7 +787,7 @@ void transform(const std::vector<job>& jobs, comm* c, void* user_stream, bool as
         tm.stop();
     }
 
-    const bool exchange = c->size > 1 && (p.send_elems > 0 || p.recv_elems > 0);
+    const bool exchange = c->nccl != nullptr && (p.send_elems > 0 || p.recv_elems > 0);
     // LOCAL on the aux stream when there is an exchange to overlap, else on main
     hipStream_t ls = exchange ? dc.aux : dc.main;
     if (exchange) {

@@ -75,8 +75,16 @@ struct plan {
     int64_t local_bytes = 0, pack_bytes = 0, unpack_bytes = 0;
 };
 
-// Build the plan of `rank` (of `n_ranks`) for a batch of jobs (host only).
-std::unique_ptr<plan> make_plan(const std::vector<job>& jobs, int rank, int n_ranks);
+// Build the plan of `rank` (of `n_ranks`) for a batch of jobs (host only).  `loopback`: the
+// rank's own tiles go through pack -> exchange with itself -> unpack instead of the local list
+// (test mode, see loopback_exchange()).
+std::unique_ptr<plan> make_plan(const std::vector<job>& jobs, int rank, int n_ranks,
+                                bool loopback = false);
+
+// COSTA_LOOPBACK=1 (test only): a one-rank communicator gets a one-rank RCCL communicator and
+// every transform moves its tiles through PACK -> ncclSend/ncclRecv to itself -> UNPACK, so the
+// exchange path runs on a single GPU (two ranks cannot share one GPU under RCCL).
+bool loopback_exchange();
 
 // normalise one copy_and_transform call (memory_utils.hpp:339-412) into a tile op
 costa_tile_op_t make_tile_op(int n_rows, int n_cols, uint64_t src, int src_stride, bool src_cm,
@@ -134,8 +142,9 @@ bool any_transpose(const std::vector<costa_tile_op_t>& ops);
 void launch_tiles(costa_dtype_t dtype, const launch_args& a, void* stream /* hipStream_t */);
 // sub-tile shapes (elements along the source's fast dim, along its slow dim)
 void tile_shapes(costa_dtype_t dtype, int* bf_large, int* bs_large, int* bf_small, int* bs_small);
-// Execution order of an op list: `ordered` = [sub-tiled ops | tiny ops] (tiny ops sorted by
-// source address, so wavefronts running at the same time share partially used cache lines),
+// Execution order of an op list: `ordered` = [sub-tiled ops | tiny ops] (tiny ops sorted by the
+// planner's locality hint, so wavefronts running at the same time share partially used cache
+// lines),
 // `work` = [large-shape sub-tiles | small-shape sub-tiles], indices into `ordered`.
 struct work_split {
     int64_t n_large = 0, n_small = 0, tiny_first = 0, n_tiny = 0;

@@ -220,7 +220,8 @@ costa_tile_op_t make_tile_op(int n_rows, int n_cols, uint64_t src, int src_strid
     return op;
 }
 
-std::unique_ptr<plan> make_plan(const std::vector<job>& jobs, int rank, int n_ranks) {
+std::unique_ptr<plan> make_plan(const std::vector<job>& jobs, int rank, int n_ranks,
+                                bool loopback) {
     if (jobs.empty()) throw error(COSTA_ERR_ARG, "costa::transform: nothing scheduled");
     if (jobs.size() > 0xFFFF) throw error(COSTA_ERR_ARG, "costa::transform: too many layout pairs");
     auto p = std::make_unique<plan>();
@@ -315,7 +316,7 @@ std::unique_ptr<plan> make_plan(const std::vector<job>& jobs, int rank, int n_ra
     std::vector<const side_tile*> local_src;
     int64_t off = 0;
     for (const side_tile& m : send) {
-        if (m.peer == rank) {
+        if (m.peer == rank && !loopback) {
             local_src.push_back(&m);
             continue;
         }
@@ -335,7 +336,7 @@ std::unique_ptr<plan> make_plan(const std::vector<job>& jobs, int rank, int n_ra
     std::vector<const side_tile*> local_dst;
     off = 0;
     for (const side_tile& m : recv) {
-        if (m.peer == rank) {
+        if (m.peer == rank && !loopback) {
             local_dst.push_back(&m);
             continue;
         }

@@ -1,0 +1,63 @@
+"""Child process of test_gpu_loopback.py (run with COSTA_LOOPBACK=1): every single-rank golden
+case and an 8192^2 fp64 'T' case go through PACK -> ncclSend/ncclRecv to self -> UNPACK.
+Prints one line per failure and a final 'OK <cases> <pack launches> <unpack launches>'."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "tests", "golden")):
+    sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import costa_amd as costa  # noqa: E402
+import oracle  # noqa: E402
+from cases import all_cases  # noqa: E402
+from golden_io import load, matches  # noqa: E402
+
+
+def dev(arr):
+    return torch.from_numpy(np.ascontiguousarray(arr).view(np.uint8).copy()).cuda()
+
+
+def main():
+    assert os.environ.get("COSTA_LOOPBACK") == "1"
+    comm = costa.Comm.self(0)
+    costa.set_profiling(True)
+    costa.get_stats(reset=True)
+    bad, n = [], 0
+    for case in all_cases():
+        if case.P != 1:
+            continue
+        n += 1
+        bufs = [tuple(dev(x) for x in case.inputs(k, 0)) for k in range(len(case.pairs))]
+        As = [p.A.make_layout(0, bufs[k][0].data_ptr(), 1, case.dtype) for k, p in enumerate(case.pairs)]
+        Cs = [p.C.make_layout(0, bufs[k][1].data_ptr(), 1, case.dtype) for k, p in enumerate(case.pairs)]
+        eff = [case.effective(k) for k in range(len(case.pairs))]
+        costa.transform_batch(As, Cs, comm, [e[0] for e in eff], [e[1] for e in eff],
+                              [e[2] for e in eff])
+        fx = load(case.name)
+        for k in range(len(case.pairs)):
+            out = bufs[k][1].cpu().numpy().view(oracle.NP[case.dtype])
+            if not matches(fx, f"C{k}_r0", out):
+                bad.append(f"{case.name} C{k}")
+    m = 8192
+    A = torch.rand(m * m, dtype=torch.float64, device="cuda")
+    Cm = torch.zeros(m * m, dtype=torch.float64, device="cuda")
+    LA = costa.block_cyclic_layout(m, m, 256, 256, 1, 1, m, m, 1, 1, "R", 0, 0, A.data_ptr(), m, "C", 0)
+    LC = costa.block_cyclic_layout(m, m, 256, 256, 1, 1, m, m, 1, 1, "R", 0, 0, Cm.data_ptr(), m, "C", 0)
+    costa.transform(LA, LC, comm, "T", 1.0, 0.0)
+    torch.cuda.synchronize()
+    if not torch.equal(Cm.view(m, m), A.view(m, m).t()):
+        bad.append("8192^2 fp64 T")
+    st = costa.get_stats()
+    for b in bad:
+        print("FAIL", b)
+    print("OK" if not bad else "BAD", n + 1, st["pack_launches"], st["unpack_launches"],
+          st["local_launches"])
+    return 1 if bad else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
