@@ -192,6 +192,15 @@ bool loopback_exchange() {
     return on;
 }
 
+size_t max_message_bytes() {
+    static const size_t v = [] {
+        const char* s = std::getenv("COSTA_MAX_MSG_BYTES");  // tuning / reproduction override
+        const long long x = s ? std::atoll(s) : 0;
+        return x > 0 ? size_t(x) : (size_t(1) << 28);       // 256 MiB
+    }();
+    return v;
+}
+
 int comm_rank(const comm* c) { return c->rank; }
 int comm_size(const comm* c) { return c->size; }
 void comm_destroy(comm* c) { delete c; }
@@ -819,15 +828,19 @@ void transform(const std::vector<job>& jobs, comm* c, void* user_stream, bool as
         }
         tm.start(PH_EXCHANGE, dc.main);
         NCCL_CHECK(ncclGroupStart());
+        // each peer's package moves as pieces of at most max_message_bytes(): RCCL was measured
+        // to lose the second half of a single >1 GiB self send/recv (tools/loopback_probe.py);
+        // pieces to one peer match in issue order on both sides
+        const size_t piece = max_message_bytes();
         for (int r = 0; r < c->size; ++r) {
-            if (p.send_counts[size_t(r)] > 0)
-                NCCL_CHECK(ncclSend(sb + size_t(p.send_displs[size_t(r)]) * E,
-                                    size_t(p.send_counts[size_t(r)]) * E, ncclUint8, r, c->nccl,
-                                    dc.main));
-            if (p.recv_counts[size_t(r)] > 0)
-                NCCL_CHECK(ncclRecv(rb + size_t(p.recv_displs[size_t(r)]) * E,
-                                    size_t(p.recv_counts[size_t(r)]) * E, ncclUint8, r, c->nccl,
-                                    dc.main));
+            const size_t sbytes = size_t(p.send_counts[size_t(r)]) * E;
+            const size_t rbytes = size_t(p.recv_counts[size_t(r)]) * E;
+            for (size_t o = 0; o < sbytes; o += piece)
+                NCCL_CHECK(ncclSend(sb + size_t(p.send_displs[size_t(r)]) * E + o,
+                                    std::min(piece, sbytes - o), ncclUint8, r, c->nccl, dc.main));
+            for (size_t o = 0; o < rbytes; o += piece)
+                NCCL_CHECK(ncclRecv(rb + size_t(p.recv_displs[size_t(r)]) * E + o,
+                                    std::min(piece, rbytes - o), ncclUint8, r, c->nccl, dc.main));
         }
         NCCL_CHECK(ncclGroupEnd());
         tm.stop();

@@ -86,6 +86,9 @@ std::unique_ptr<plan> make_plan(const std::vector<job>& jobs, int rank, int n_ra
 // exchange path runs on a single GPU (two ranks cannot share one GPU under RCCL).
 bool loopback_exchange();
 
+// largest single ncclSend/ncclRecv of the exchange (COSTA_MAX_MSG_BYTES, default 256 MiB)
+size_t max_message_bytes();
+
 // normalise one copy_and_transform call (memory_utils.hpp:339-412) into a tile op
 costa_tile_op_t make_tile_op(int n_rows, int n_cols, uint64_t src, int src_stride, bool src_cm,
                              uint64_t dst, int dst_stride, bool dst_cm, bool transpose, bool conj,

@@ -1,5 +1,5 @@
 """Child process of test_gpu_loopback.py (run with COSTA_LOOPBACK=1): every single-rank golden
-case and an 8192^2 fp64 'T' case go through PACK -> ncclSend/ncclRecv to self -> UNPACK.
+case and a 12288^2 fp64 'T' case go through PACK -> ncclSend/ncclRecv to self -> UNPACK.
 Prints one line per failure and a final 'OK <cases> <pack launches> <unpack launches>'."""
 import os
 import sys
@@ -42,7 +42,7 @@ def main():
             out = bufs[k][1].cpu().numpy().view(oracle.NP[case.dtype])
             if not matches(fx, f"C{k}_r0", out):
                 bad.append(f"{case.name} C{k}")
-    m = 8192
+    m = 12288  # a 1.2 GB package: one unchunked RCCL self send/recv of it loses half
     A = torch.rand(m * m, dtype=torch.float64, device="cuda")
     Cm = torch.zeros(m * m, dtype=torch.float64, device="cuda")
     LA = costa.block_cyclic_layout(m, m, 256, 256, 1, 1, m, m, 1, 1, "R", 0, 0, A.data_ptr(), m, "C", 0)
@@ -50,7 +50,7 @@ def main():
     costa.transform(LA, LC, comm, "T", 1.0, 0.0)
     torch.cuda.synchronize()
     if not torch.equal(Cm.view(m, m), A.view(m, m).t()):
-        bad.append("8192^2 fp64 T")
+        bad.append(f"{m}^2 fp64 T")
     st = costa.get_stats()
     for b in bad:
         print("FAIL", b)
