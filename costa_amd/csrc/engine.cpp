@@ -184,12 +184,13 @@ comm* comm_create(const unsigned char* id, int nranks, int rank, int device) {
     return c;
 }
 
-bool loopback_exchange() {
-    static const bool on = [] {
+int loopback_exchange() {
+    static const int mode = [] {
         const char* s = std::getenv("COSTA_LOOPBACK");
-        return s && std::atoi(s) != 0;
+        const int m = s ? std::atoi(s) : 0;
+        return m == 1 || m == 2 ? m : 0;
     }();
-    return on;
+    return mode;
 }
 
 size_t max_message_bytes() {
@@ -608,7 +609,7 @@ cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
             }
         }
     }
-    cp->p = make_plan(pj, c->rank, c->size, c->size == 1 && c->nccl != nullptr);
+    cp->p = make_plan(pj, c->rank, c->size, c->size == 1 && c->nccl ? loopback_exchange() : 0);
     const plan& p = *cp->p;
     if (cp->staged) {
         // A C-only range needs no upload when the kernels overwrite every byte of it: one job's

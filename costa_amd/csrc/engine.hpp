@@ -75,16 +75,18 @@ struct plan {
     int64_t local_bytes = 0, pack_bytes = 0, unpack_bytes = 0;
 };
 
-// Build the plan of `rank` (of `n_ranks`) for a batch of jobs (host only).  `loopback`: the
-// rank's own tiles go through pack -> exchange with itself -> unpack instead of the local list
-// (test mode, see loopback_exchange()).
+// Build the plan of `rank` (of `n_ranks`) for a batch of jobs (host only).  `loopback` (test
+// mode, see loopback_exchange()): 1 = the rank's own tiles all go through pack -> exchange with
+// itself -> unpack instead of the local list; 2 = half of them (by a parity of their target
+// coordinates, the same on both sides), the rest stays local.
 std::unique_ptr<plan> make_plan(const std::vector<job>& jobs, int rank, int n_ranks,
-                                bool loopback = false);
+                                int loopback = 0);
 
-// COSTA_LOOPBACK=1 (test only): a one-rank communicator gets a one-rank RCCL communicator and
-// every transform moves its tiles through PACK -> ncclSend/ncclRecv to itself -> UNPACK, so the
-// exchange path runs on a single GPU (two ranks cannot share one GPU under RCCL).
-bool loopback_exchange();
+// COSTA_LOOPBACK=1 or 2 (test only): a one-rank communicator gets a one-rank RCCL communicator
+// and its transforms route tiles through PACK -> ncclSend/ncclRecv to itself -> UNPACK (all of
+// them, or half with the rest on the concurrent LOCAL path), so the exchange machinery runs on
+// a single GPU (two ranks cannot share one GPU under RCCL).  0 = off.
+int loopback_exchange();
 
 // largest single ncclSend/ncclRecv of the exchange (COSTA_MAX_MSG_BYTES, default 256 MiB)
 size_t max_message_bytes();

@@ -221,7 +221,14 @@ costa_tile_op_t make_tile_op(int n_rows, int n_cols, uint64_t src, int src_strid
 }
 
 std::unique_ptr<plan> make_plan(const std::vector<job>& jobs, int rank, int n_ranks,
-                                bool loopback) {
+                                int loopback) {
+    // loopback test mode: which of the rank's own tiles stay local
+    auto stays_local = [&](const side_tile& m) {
+        if (m.peer != rank) return false;
+        if (loopback == 1) return false;
+        if (loopback == 2) return ((m.rows.start / 7 + m.cols.start / 5) & 1) == 0;
+        return true;
+    };
     if (jobs.empty()) throw error(COSTA_ERR_ARG, "costa::transform: nothing scheduled");
     if (jobs.size() > 0xFFFF) throw error(COSTA_ERR_ARG, "costa::transform: too many layout pairs");
     auto p = std::make_unique<plan>();
@@ -316,7 +323,7 @@ std::unique_ptr<plan> make_plan(const std::vector<job>& jobs, int rank, int n_ra
     std::vector<const side_tile*> local_src;
     int64_t off = 0;
     for (const side_tile& m : send) {
-        if (m.peer == rank && !loopback) {
+        if (stays_local(m)) {
             local_src.push_back(&m);
             continue;
         }
@@ -336,7 +343,7 @@ std::unique_ptr<plan> make_plan(const std::vector<job>& jobs, int rank, int n_ra
     std::vector<const side_tile*> local_dst;
     off = 0;
     for (const side_tile& m : recv) {
-        if (m.peer == rank && !loopback) {
+        if (stays_local(m)) {
             local_dst.push_back(&m);
             continue;
         }

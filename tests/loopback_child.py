@@ -1,6 +1,8 @@
-"""Child process of test_gpu_loopback.py (run with COSTA_LOOPBACK=1): every single-rank golden
-case and a 12288^2 fp64 'T' case go through PACK -> ncclSend/ncclRecv to self -> UNPACK.
-Prints one line per failure and a final 'OK <cases> <pack launches> <unpack launches>'."""
+"""Child process of test_gpu_loopback.py (run with COSTA_LOOPBACK=1 or 2): every single-rank
+golden case and a 12288^2 fp64 'T' case go through PACK -> ncclSend/ncclRecv to self -> UNPACK
+(mode 2: half of the tiles, the rest through the concurrent LOCAL launch), then a loop of
+stream-ordered async transforms with A updated on torch's stream between them.
+Prints one line per failure and a final 'OK <cases> <pack> <unpack> <local launches>'."""
 import os
 import sys
 
@@ -22,7 +24,7 @@ def dev(arr):
 
 
 def main():
-    assert os.environ.get("COSTA_LOOPBACK") == "1"
+    assert os.environ.get("COSTA_LOOPBACK") in ("1", "2")
     comm = costa.Comm.self(0)
     costa.set_profiling(True)
     costa.get_stats(reset=True)
@@ -51,6 +53,15 @@ def main():
     torch.cuda.synchronize()
     if not torch.equal(Cm.view(m, m), A.view(m, m).t()):
         bad.append(f"{m}^2 fp64 T")
+    # stream-ordered: A changes on torch's stream between queued transforms
+    s = torch.cuda.current_stream()
+    for k in range(4):
+        A.mul_(-1.5)
+        costa.transform_async(LA, LC, comm, "T", 1.0, 0.0, stream=s)
+    costa.synchronize(comm)
+    torch.cuda.synchronize()
+    if not torch.equal(Cm.view(m, m), A.view(m, m).t()):
+        bad.append(f"{m}^2 fp64 T async")
     st = costa.get_stats()
     for b in bad:
         print("FAIL", b)

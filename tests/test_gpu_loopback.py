@@ -1,7 +1,8 @@
 """The exchange path (PACK -> RCCL group of ncclSend/ncclRecv -> UNPACK, with its streams,
 events and send/recv workspaces) on ONE GPU: in COSTA_LOOPBACK=1 mode a one-rank communicator
 holds a one-rank RCCL communicator and routes its own tiles through the exchange with itself
-(engine.hpp loopback_exchange).  Two ranks cannot share a GPU under RCCL, so this is how the
+(engine.hpp loopback_exchange); mode 2 routes half of them, the rest runs through the LOCAL
+launch on the second stream concurrently with the exchange, as on a multi-GPU node.  Two ranks cannot share a GPU under RCCL, so this is how the
 multi-rank machinery runs on the one-GPU box; results must equal the reference's golden
 outputs bit for bit.  Runs in a child process (the mode is fixed per process)."""
 import os
@@ -13,15 +14,19 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def test_loopback_exchange_matches_golden():
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_loopback_exchange_matches_golden(mode):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "loopback_child.py")
-    r = subprocess.run([sys.executable, child], env=dict(os.environ, COSTA_LOOPBACK="1"),
+    r = subprocess.run([sys.executable, child], env=dict(os.environ, COSTA_LOOPBACK=mode),
                        capture_output=True, text=True, timeout=600)
     out = r.stdout.strip().splitlines()
     assert r.returncode == 0 and out and out[-1].startswith("OK"), r.stdout + r.stderr
     _, n, packs, unpacks, locals_ = out[-1].split()
     assert int(packs) >= int(n) and int(unpacks) >= int(n), out[-1]  # every case exchanged
-    assert int(locals_) == 0, out[-1]
+    if mode == "1":
+        assert int(locals_) == 0, out[-1]
+    else:  # half the tiles local: the LOCAL launch overlaps the exchange
+        assert int(locals_) >= int(n) // 2, out[-1]
