@@ -174,9 +174,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--edge", type=int, default=16384, help="local matrix edge per rank")
     ap.add_argument("--block", type=int, default=256)
-    ap.add_argument("--workload", choices=["pxtran", "cfg5"], default="pxtran",
-                    help="pxtran: BASELINE configs[1] (default, the headline); cfg5: configs[4] "
-                         "custom_layout many-small fp32 tiles")
+    ap.add_argument("--workload", choices=["pxtran", "cfg4", "cfg5"], default="pxtran",
+                    help="pxtran: BASELINE configs[1] (default, the headline); cfg4: configs[3] "
+                         "pztranu c128 alpha,beta != 0, 128^2 blocks (16384^2 per rank); cfg5: "
+                         "configs[4] custom_layout many-small fp32 tiles")
     ap.add_argument("--cfg5-op", choices=["N", "T"], default="N")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
@@ -226,6 +227,31 @@ def main():
     if args.workload == "cfg5":
         LA, LC, A, Cm, op, al, be, wl = cfg5_workload(costa, torch, rank, world, args.cfg5_op)
         check = None
+    elif args.workload == "cfg4":
+        # BASELINE configs[3]: pztranu, c128, 128^2 blocks, alpha=(0.75,-0.5),
+        # beta=(1.25,0.25) (C is read); per rank 16384^2, weak-scaled on the pm x pn grid
+        b = 128
+        lr_a, lc_a = M // pm, N // pn
+        lr_c, lc_c = N // pm, M // pn
+        g = torch.Generator(device="cuda")
+        g.manual_seed(4321 + rank)
+        A = torch.rand(lr_a * lc_a, dtype=torch.complex128, device="cuda", generator=g)
+        Cm = torch.rand(lr_c * lc_c, dtype=torch.complex128, device="cuda", generator=g)
+        LA = costa.block_cyclic_layout(M, N, b, b, 1, 1, M, N, pm, pn, "R", 0, 0, A.data_ptr(),
+                                       lr_a, "C", rank, dtype=costa.CDOUBLE)
+        LC = costa.block_cyclic_layout(N, M, b, b, 1, 1, N, M, pm, pn, "R", 0, 0, Cm.data_ptr(),
+                                       lr_c, "C", rank, dtype=costa.CDOUBLE)
+        op, al, be = "T", complex(0.75, -0.5), complex(1.25, 0.25)
+        wl = (f"pztranu c128 {M}x{N} on a {pm}x{pn} rank grid (16384^2 per rank), 128x128 "
+              f"blocks, op T, alpha=(0.75,-0.5) beta=(1.25,0.25) (BASELINE configs[3], "
+              f"{'single-GPU slice' if world == 1 else 'weak-scaled'})")
+        C0 = Cm.clone() if world == 1 else None
+
+        def check():  # after the first call only (beta != 0: every step changes C)
+            k = torch.randint(0, n * n, (100000,), device="cuda")
+            i, j = k % n, k // n  # C(i, j) at i + j*n; A(j, i) at j + i*n
+            exp = be * C0[k] + al * A[j + i * n]
+            assert torch.allclose(Cm[k], exp, rtol=1e-13, atol=1e-13), "cfg4 result wrong"
     else:
         lr_a, lc_a = M // pm, N // pn
         lr_c, lc_c = N // pm, M // pn
@@ -274,15 +300,18 @@ def main():
     t0 = time.perf_counter()
     step_blocking()
     first_call_ms = max_over_ranks(time.perf_counter() - t0) * 1e3
+    repeatable = args.workload != "cfg4"  # beta != 0: only the first call's result is known
+    if world == 1 and check and not repeatable:
+        check()
     for _ in range(args.warmup):
         step_blocking()
-    if world == 1 and check:  # correctness of what we time
+    if world == 1 and check and repeatable:  # correctness of what we time
         check()
     el_block, _ = timed(step_blocking)
     for _ in range(args.warmup):
         step_async()
     el, st = timed(step_async)
-    if world == 1 and check:
+    if world == 1 and check and repeatable:
         check()
 
     alg_bytes = st["local_bytes"] + st["pack_bytes"] + st["unpack_bytes"]  # this rank, K steps
@@ -307,7 +336,7 @@ def main():
     avg_ms = kms / max(kl, 1)
     achieved = per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     traffic, traffic_src = measured_traffic(int(per_launch))
-    kdt = "double" if args.workload != "cfg5" else "float"
+    kdt = {"pxtran": "double", "cfg4": "cpx<double>", "cfg5": "float"}[args.workload]
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
             "traffic_source": traffic_src,
@@ -357,10 +386,12 @@ def main():
             cpu["port"] = {k: port[k] for k in ("value", "cores", "kind", "sample")}
 
     if rank == 0:
-        cfg = {"workload": wl, "op": op, "alpha": al, "beta": be,
+        def js(x):  # complex scalars as [re, im]
+            return [x.real, x.imag] if isinstance(x, complex) else x
+        cfg = {"workload": wl, "op": op, "alpha": js(al), "beta": js(be),
                "parallelism": f"{world} rank(s), one per GPU, RCCL send/recv exchange",
                "bytes_per_step": int(total_bytes / args.steps)}
-        if args.workload == "pxtran":
+        if args.workload in ("pxtran", "cfg4"):
             cfg.update({"m": M, "n": N, "block": b, "grid": f"{pm}x{pn}"})
         line = {
             "metric": "GB/s device-resident tile pack+transpose+unpack (fp64), % HBM peak",
@@ -372,9 +403,9 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak" if args.workload == "pxtran" else "strong",
+            "scaling": "strong" if args.workload == "cfg5" else "weak",
             "vs_baseline": None,
-            "dtype": "f64" if args.workload == "pxtran" else "f32",
+            "dtype": {"pxtran": "f64", "cfg4": "c128", "cfg5": "f32"}[args.workload],
             "data": "synthetic (uniform random, device-resident)",
             "config": cfg,
             "roofline": roof,

@@ -222,17 +222,25 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
     if (!(flags & COSTA_TILE_TRANSPOSE)) {
         // ---- copy mode: dst(f, s) = g(src(f, s)), no LDS
         T* dst = reinterpret_cast<T*>(dst_base + op.dst) + int64_t(s0) * ldd + f0;
+        // beta != 0: every old value is requested before the first store (a load behind a
+        // store to the same array would otherwise wait for it: one round trip per strip)
+        vec<T> y[S::PL];
+        if (kind == COSTA_SCALE_AXPBY) {
+#pragma unroll
+            for (int k = 0; k < S::PL; ++k) {
+                const int s = c0 + k * S::CPP;
+                if (FULL || (nf_lane > 0 && s < ts)) vload(y[k], dst + s * ldd + lf, nf_lane, vd);
+            }
+        }
 #pragma unroll
         for (int k = 0; k < S::PL; ++k) {
             const int s = c0 + k * S::CPP;
             if (!FULL && (nf_lane <= 0 || s >= ts)) continue;
             T* d = dst + s * ldd + lf;
             if (kind != COSTA_SCALE_BITCOPY) {
-                vec<T> y;
-                if (kind == COSTA_SCALE_AXPBY) vload(y, d, nf_lane, vd);
 #pragma unroll
                 for (int e = 0; e < V; ++e)
-                    x[k].e[e] = scale(x[k].e[e], kind == COSTA_SCALE_AXPBY ? y.e[e] : e_zero<T>(),
+                    x[k].e[e] = scale(x[k].e[e], kind == COSTA_SCALE_AXPBY ? y[k].e[e] : e_zero<T>(),
                                       kind, conj, alpha, beta);
             }
             vstore(d, x[k], nf_lane, vd);
@@ -241,6 +249,30 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
     }
 
     // ---- transpose mode: dst(s, f) = g(src(f, s)) through LDS
+    T* dst = reinterpret_cast<T*>(dst_base + op.dst) + int64_t(f0) * ldd + s0;
+    const int lane = int(threadIdx.x) % 64, wave = int(threadIdx.x) / 64;
+    constexpr int FSLOTS = BF / V;
+    // store unit k of this lane: 64 s values x one f slot; after the lane exchange lane
+    // (base + j) stores f = q*V + j for s = sc*64 + base .. +V-1
+    auto unit = [&](int k, int& f, int& sb, int& n) {
+        const int u = wave + S::NW * k;
+        const int sc = u / FSLOTS, q = u % FSLOTS;
+        const int j = lane & (V - 1);
+        f = q * V + j;
+        sb = sc * 64 + (lane - j);
+        n = FULL ? V : ts - sb;
+        return FULL || (f < tf && n > 0);
+    };
+    // beta != 0: the old destination values are requested now, overlapping the source loads
+    // still in flight (not after the LDS exchange, one round trip per store unit)
+    vec<T> old[S::PS];
+    if (kind == COSTA_SCALE_AXPBY) {
+#pragma unroll
+        for (int k = 0; k < S::PS; ++k) {
+            int f, sb, n;
+            if (unit(k, f, sb, n)) vload(old[k], dst + f * ldd + sb, n, vd);
+        }
+    }
 #pragma unroll
     for (int k = 0; k < S::PL; ++k) {
         const int s = c0 + k * S::CPP;
@@ -252,9 +284,6 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
     }
     __syncthreads();
 
-    T* dst = reinterpret_cast<T*>(dst_base + op.dst) + int64_t(f0) * ldd + s0;
-    const int lane = int(threadIdx.x) % 64, wave = int(threadIdx.x) / 64;
-    constexpr int FSLOTS = BF / V;
     vec<T> y[S::PS];
 #pragma unroll
     for (int k = 0; k < S::PS; ++k) {
@@ -268,22 +297,14 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
     }
 #pragma unroll
     for (int k = 0; k < S::PS; ++k) {
-        const int u = wave + S::NW * k;
-        const int sc = u / FSLOTS, q = u % FSLOTS;
-        // after the exchange lane (base + j) holds f = q*V + j for s = sc*64 + base .. +V-1
         vec<T> o = lane_transpose(y[k], lane);
-        const int j = lane & (V - 1);
-        const int f = q * V + j;
-        const int sb = sc * 64 + (lane - j);
-        const int n = FULL ? V : ts - sb;
-        if (!FULL && (f >= tf || n <= 0)) continue;
+        int f, sb, n;
+        if (!unit(k, f, sb, n)) continue;
         T* d = dst + f * ldd + sb;
-        vec<T> old;
-        if (kind == COSTA_SCALE_AXPBY) vload(old, d, n, vd);
         if (kind != COSTA_SCALE_BITCOPY) {
 #pragma unroll
             for (int e = 0; e < V; ++e)
-                o.e[e] = scale(o.e[e], kind == COSTA_SCALE_AXPBY ? old.e[e] : e_zero<T>(), kind,
+                o.e[e] = scale(o.e[e], kind == COSTA_SCALE_AXPBY ? old[k].e[e] : e_zero<T>(), kind,
                                conj, alpha, beta);
         }
         vstore(d, o, n, vd);
@@ -353,7 +374,9 @@ struct lin {  // (f, s) of linear element index e = f + s*n, stepped by 64
     }
 };
 
-template <typename T, int UB>
+// TR = false: the list has no transposing op (the transpose path and its registers are
+// compiled out, so copy-only lists keep a high occupancy)
+template <typename T, int UB, bool TR>
 __device__ __forceinline__ void tiny_op(const costa_tile_op_t& op, int lane, T* t,
                                         const char* src_base, char* dst_base,
                                         const T* __restrict__ scalars) {
@@ -372,7 +395,7 @@ __device__ __forceinline__ void tiny_op(const costa_tile_op_t& op, int lane, T* 
     const int64_t lds = op.lds, ldd = op.ldd;
     constexpr int U = UB / int(sizeof(T)) > 0 ? UB / int(sizeof(T)) : 1;
 
-    if (!(flags & COSTA_TILE_TRANSPOSE)) {
+    if (!TR || !(flags & COSTA_TILE_TRANSPOSE)) {
         // copy mode: dst(f, s) = g(src(f, s)), U independent loads in flight per lane
         lin<T> p(lane, nf);
         for (int e0 = 0; e0 < total; e0 += 64 * U) {
@@ -405,6 +428,8 @@ __device__ __forceinline__ void tiny_op(const costa_tile_op_t& op, int lane, T* 
     }
     // transpose mode: stage in LDS (pitch odd), then write in destination order
     const int pitch = nf | 1;
+    // (requesting the first pass's old values before the staging loads was measured slower on
+    // cfg 5 'T': 2.92 against 3.13 TB/s; the 16 extra VGPRs cost a wavefront per SIMD)
     {
         lin<T> p(lane, nf);
         for (int e0 = 0; e0 < total; e0 += 64 * U) {
@@ -465,7 +490,7 @@ __device__ __forceinline__ void tiny_op(const costa_tile_op_t& op, int lane, T* 
 // `xcd_remap`: blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup
 // dispatch); renumbering them so that each XCD walks one contiguous slice of the list keeps
 // neighbouring ops (which share partially written cache lines) in one L2.
-template <typename T, int W, int UB>
+template <typename T, int W, int UB, bool TR>
 __global__ __launch_bounds__(64 * W) void tiny_kernel(
     const costa_tile_op_t* __restrict__ ops, int64_t n_ops, int k_per_wave, int chunked,
     int xcd_remap, const char* src_base, char* dst_base, const T* __restrict__ scalars,
@@ -489,14 +514,14 @@ __global__ __launch_bounds__(64 * W) void tiny_kernel(
     for (int64_t i = first; i < end; i += step) {
         const costa_tile_op_t op = next;
         if (i + step < end) next = ops[i + step];  // in flight while this op moves its data
-        tiny_op<T, UB>(op, lane, t, src_base, dst_base, scalars);
+        tiny_op<T, UB, TR>(op, lane, t, src_base, dst_base, scalars);
     }
 }
 
 struct tiny_cfg {
     int k = 1;          // ops per wavefront
     int chunked = 0;    // 0: strided assignment, 1: contiguous chunks
-    int waves = 0;      // 0: by list kind (TINY_WAVES_TR / TINY_WAVES_COPY)
+    int waves = 0;      // 0: by list kind (TINY_WAVES_TR / TINY_WAVES_COPY); 4: tuning variant
     int bytes = TINY_BYTES;
     int xcd = 0;
 };
@@ -517,7 +542,7 @@ const tiny_cfg& tiny_config() {  // COSTA_TINY_{K,CHUNKED,WAVES,BYTES,XCD}: tuni
     return c;
 }
 
-template <typename T, int W, int UB>
+template <typename T, int W, int UB, bool TR>
 void launch_tiny_v(const launch_args& a, const tiny_cfg& cfg, hipStream_t stream) {
     const int64_t n = a.n_tiny;
     const int per_wave = a.any_transpose ? int(tiny_lds_bytes / sizeof(T)) : 0;
@@ -525,7 +550,7 @@ void launch_tiny_v(const launch_args& a, const tiny_cfg& cfg, hipStream_t stream
     const int64_t waves = (n + cfg.k - 1) / cfg.k;
     const int64_t blocks = std::min<int64_t>((waves + W - 1) / W, 1LL << 30);
     const int k = int((n + blocks * W - 1) / (blocks * W));  // chunked: covers all ops
-    hipLaunchKernelGGL((tiny_kernel<T, W, UB>), dim3(unsigned(blocks)), dim3(64 * W), lds, stream,
+    hipLaunchKernelGGL((tiny_kernel<T, W, UB, TR>), dim3(unsigned(blocks)), dim3(64 * W), lds, stream,
                        a.ops + a.tiny_first, n, k, cfg.chunked, cfg.xcd, a.src_base, a.dst_base,
                        static_cast<const T*>(a.scalars), per_wave);
 }
@@ -535,14 +560,17 @@ void launch_tiny(const launch_args& a, hipStream_t stream) {
     if (a.n_tiny <= 0) return;
     const tiny_cfg& cfg = tiny_config();
     if constexpr (std::is_same<T, float>::value) {  // tuning variants (cfg 5 is fp32)
-        if (cfg.waves == 4 && cfg.bytes == 64) return launch_tiny_v<T, 4, 64>(a, cfg, stream);
-        if (cfg.waves == 4 && cfg.bytes == 32) return launch_tiny_v<T, 4, 32>(a, cfg, stream);
-        if (cfg.waves == 8 && cfg.bytes == 32) return launch_tiny_v<T, 8, 32>(a, cfg, stream);
-        if (cfg.waves == 4 && cfg.bytes == 128) return launch_tiny_v<T, 4, 128>(a, cfg, stream);
+        const bool tr = a.any_transpose;
+        if (cfg.waves == 4 && cfg.bytes == 64)
+            return tr ? launch_tiny_v<T, 4, 64, true>(a, cfg, stream)
+                      : launch_tiny_v<T, 4, 64, false>(a, cfg, stream);
+        if (cfg.waves == 4 && cfg.bytes == 32)
+            return tr ? launch_tiny_v<T, 4, 32, true>(a, cfg, stream)
+                      : launch_tiny_v<T, 4, 32, false>(a, cfg, stream);
     }
-    const int w = cfg.waves ? cfg.waves : (a.any_transpose ? TINY_WAVES_TR : TINY_WAVES_COPY);
-    if (w == TINY_WAVES_TR) return launch_tiny_v<T, TINY_WAVES_TR, TINY_BYTES>(a, cfg, stream);
-    launch_tiny_v<T, TINY_WAVES_COPY, TINY_BYTES>(a, cfg, stream);
+    // transposing lists: TINY_WAVES_TR wavefronts per workgroup; copy-only: TINY_WAVES_COPY
+    if (a.any_transpose) return launch_tiny_v<T, TINY_WAVES_TR, TINY_BYTES, true>(a, cfg, stream);
+    launch_tiny_v<T, TINY_WAVES_COPY, TINY_BYTES, false>(a, cfg, stream);
 }
 
 template <typename T, typename S>
