@@ -174,8 +174,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--edge", type=int, default=16384, help="local matrix edge per rank")
     ap.add_argument("--block", type=int, default=256)
-    ap.add_argument("--workload", choices=["pxtran", "cfg4", "cfg5"], default="pxtran",
-                    help="pxtran: BASELINE configs[1] (default, the headline); cfg4: configs[3] "
+    ap.add_argument("--workload", choices=["pxtran", "cfg3", "cfg4", "cfg5"], default="pxtran",
+                    help="pxtran: BASELINE configs[1] (default, the headline); cfg3: configs[2] "
+                         "pxgemr2d fp64 remap pm x pn -> world x 1, 128^2 blocks, 32768^2 per "
+                         "rank (65536^2 2x2 -> 4x1 at 4 ranks); cfg4: configs[3] "
                          "pztranu c128 alpha,beta != 0, 128^2 blocks (16384^2 per rank); cfg5: "
                          "configs[4] custom_layout many-small fp32 tiles")
     ap.add_argument("--cfg5-op", choices=["N", "T"], default="N")
@@ -227,6 +229,27 @@ def main():
     if args.workload == "cfg5":
         LA, LC, A, Cm, op, al, be, wl = cfg5_workload(costa, torch, rank, world, args.cfg5_op)
         check = None
+    elif args.workload == "cfg3":
+        # BASELINE configs[2]: pxgemr2d fp64 'N' (bit copy), 128^2 blocks, A on
+        # the pm x pn grid -> C on a world x 1 grid ('R' rank order both); 32768^2 per rank
+        b, e3 = 128, 32768
+        M, N = e3 * pm, e3 * pn
+        lr_a, lc_a = M // pm, N // pn
+        lr_c, lc_c = M // world, N
+        g = torch.Generator(device="cuda")
+        g.manual_seed(3333 + rank)
+        A = torch.rand(lr_a * lc_a, dtype=torch.float64, device="cuda", generator=g)
+        Cm = torch.zeros(lr_c * lc_c, dtype=torch.float64, device="cuda")
+        LA = costa.block_cyclic_layout(M, N, b, b, 1, 1, M, N, pm, pn, "R", 0, 0, A.data_ptr(),
+                                       lr_a, "C", rank)
+        LC = costa.block_cyclic_layout(M, N, b, b, 1, 1, M, N, world, 1, "R", 0, 0, Cm.data_ptr(),
+                                       lr_c, "C", rank)
+        op, al, be = "N", 1.0, 0.0
+        wl = (f"pxgemr2d fp64 {M}x{N}, 128x128 blocks, {pm}x{pn} -> {world}x1 grid remap, op N "
+              f"(BASELINE configs[2]{', single-GPU slice' if world == 1 else ''})")
+
+        def check():
+            assert torch.equal(Cm, A), "pxgemr2d copy wrong"
     elif args.workload == "cfg4":
         # BASELINE configs[3]: pztranu, c128, 128^2 blocks, alpha=(0.75,-0.5),
         # beta=(1.25,0.25) (C is read); per rank 16384^2, weak-scaled on the pm x pn grid
@@ -336,7 +359,7 @@ def main():
     avg_ms = kms / max(kl, 1)
     achieved = per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     traffic, traffic_src = measured_traffic(int(per_launch))
-    kdt = {"pxtran": "double", "cfg4": "cpx<double>", "cfg5": "float"}[args.workload]
+    kdt = {"pxtran": "double", "cfg3": "double", "cfg4": "cpx<double>", "cfg5": "float"}[args.workload]
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
             "traffic_source": traffic_src,
@@ -391,7 +414,7 @@ def main():
         cfg = {"workload": wl, "op": op, "alpha": js(al), "beta": js(be),
                "parallelism": f"{world} rank(s), one per GPU, RCCL send/recv exchange",
                "bytes_per_step": int(total_bytes / args.steps)}
-        if args.workload in ("pxtran", "cfg4"):
+        if args.workload in ("pxtran", "cfg3", "cfg4"):
             cfg.update({"m": M, "n": N, "block": b, "grid": f"{pm}x{pn}"})
         line = {
             "metric": "GB/s device-resident tile pack+transpose+unpack (fp64), % HBM peak",
@@ -405,7 +428,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong" if args.workload == "cfg5" else "weak",
             "vs_baseline": None,
-            "dtype": {"pxtran": "f64", "cfg4": "c128", "cfg5": "f32"}[args.workload],
+            "dtype": {"pxtran": "f64", "cfg3": "f64", "cfg4": "c128", "cfg5": "f32"}[args.workload],
             "data": "synthetic (uniform random, device-resident)",
             "config": cfg,
             "roofline": roof,

@@ -57,15 +57,16 @@ def _shape(rng, E, transpose):
     return int(rng.integers(1, 400)), int(rng.integers(1, 400))
 
 
-def _random_list(rng, code, n_ops):
-    """op list whose scale kinds agree with the slot scalars (see SLOTS)"""
+def _random_list(rng, code, n_ops, copy_only=False):
+    """op list whose scale kinds agree with the slot scalars (see SLOTS); copy_only: no
+    transposing op (the executor then runs large ops on its copy shape)"""
     dt = oracle.NP[code]
     E = np.dtype(dt).itemsize
     cplx = np.issubdtype(dt, np.complexfloating)
     ops = np.zeros(n_ops, costa_amd.TILE_OP_DTYPE)
     src_off = dst_off = 0
     for i in range(n_ops):
-        tr = bool(rng.integers(0, 2))
+        tr = bool(rng.integers(0, 2)) and not copy_only
         nf, ns = _shape(rng, E, tr)
         lds = nf + int(rng.integers(0, 2)) * int(rng.integers(0, 5))
         dn = ns if tr else nf
@@ -96,11 +97,12 @@ def _random_list(rng, code, n_ops):
 
 
 @pytest.mark.parametrize("code", [0, 1, 2, 3, 4], ids=["f32", "f64", "c64", "c128", "i32"])
-@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("seed", [1, 2, 3, "copy"])
 def test_mixed_tile_list(gpu, code, seed):
-    rng = np.random.default_rng(1000 * seed + code)
+    copy_only = seed == "copy"
+    rng = np.random.default_rng(1000 * (7 if copy_only else seed) + code)
     dt = oracle.NP[code]
-    ops, n_src, n_dst = _random_list(rng, code, 240)
+    ops, n_src, n_dst = _random_list(rng, code, 240, copy_only)
     src = _values(rng, dt, n_src)
     dst0 = _values(rng, dt, n_dst)
     # SLOTS: 0 = (1, 0) bit copy / unit scale, 1 = (0, 0), 2 = (alpha, 0), 3 = (alpha, beta)
