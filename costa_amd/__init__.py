@@ -96,7 +96,7 @@ class Stats(C.Structure):
                 ("unpack_launches", C.c_int64), ("pack_bytes", C.c_int64),
                 ("local_bytes", C.c_int64), ("unpack_bytes", C.c_int64),
                 ("transforms", C.c_int64), ("plan_hits", C.c_int64),
-                ("plan_misses", C.c_int64)]
+                ("plan_misses", C.c_int64), ("host_groups", C.c_int64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -152,6 +152,7 @@ def lib():
         "costa_hip_set_profiling": (i, [i]),
         "costa_hip_get_stats": (i, [C.POINTER(Stats), i]),
         "costa_hip_release_caches": (i, []),
+        "costa_hip_set_host_staging": (i, [i]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -483,3 +484,8 @@ def get_stats(reset: bool = False) -> dict:
 
 def release_caches():
     _check(lib().costa_hip_release_caches())
+
+
+def set_host_staging(mode: int):
+    """Host-resident layouts: 1 = pipelined (default), 0 = mirror (costa_hip_set_host_staging)."""
+    _check(lib().costa_hip_set_host_staging(int(mode)))

@@ -305,6 +305,13 @@ int costa_hip_get_stats(costa_stats_t* out, int reset) {
     });
 }
 
+int costa_hip_set_host_staging(int mode) {
+    return guarded([&] {
+        if (mode != 0 && mode != 1) throw costa::engine::error(COSTA_ERR_ARG, "mode must be 0 or 1");
+        costa::engine::set_host_staging_mode(mode);
+    });
+}
+
 int costa_hip_release_caches(void) {
     return guarded([&] { costa::engine::release_caches(); });
 }

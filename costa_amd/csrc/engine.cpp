@@ -413,6 +413,22 @@ bool layout_on_device(const elayout& L) {
 
 }  // namespace
 
+// ---------------------------------------------------------------- host staging mode
+namespace {
+int g_host_mode = -1;
+}
+int host_staging_mode() {
+    if (g_host_mode < 0) {
+        const char* s = std::getenv("COSTA_HOST_STAGING");
+        g_host_mode = s ? (std::atoi(s) != 0) : 1;
+    }
+    return g_host_mode;
+}
+void set_host_staging_mode(int mode) {
+    std::lock_guard<std::recursive_mutex> lk(g_mutex);
+    g_host_mode = mode != 0;
+}
+
 // ---------------------------------------------------------------- plan cache
 namespace {
 
@@ -468,6 +484,7 @@ struct cached_plan {
     work_split l_local, l_pack, l_unpack;  // how each work list splits over the kernel shapes
     bool tr_local = true, tr_unpack = true;          // any op of the list transposes
     std::vector<unsigned char> scal_host;
+    std::shared_ptr<host_pipeline> pipe;  // host-resident single-rank calls (host_pipe.cpp)
 };
 
 constexpr size_t kMaxPlans = 16;
@@ -514,6 +531,7 @@ cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
     h.mix(uint64_t(c->rank));
     h.mix(uint64_t(c->size));
     h.mix(uint64_t(c->device));
+    h.mix(uint64_t(host_staging_mode()));
     h.mix(jobs.size());
     for (const auto& j : jobs) {
         h.mix(j.A->hash ? j.A->hash : layout_hash(*j.A));  // handles cache their hash
@@ -564,7 +582,6 @@ cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
             r.dev_off = off;
             off += ((r.hi - r.lo) + 255) & ~size_t(255);
         }
-        cp->stage.reserve(std::max<size_t>(off, 256));
         // per merged range: holds A data (bit 0), C data (bit 1), C blocks of more than one
         // job (bit 2); C ranges are copied back, A ranges and C ranges the kernels do not
         // overwrite completely are uploaded (decided once the ops are known, below)
@@ -595,6 +612,22 @@ cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
                 }
             }
         }
+        // Pipelined staging (host_pipe.cpp) when every layout is host-resident, there is no
+        // exchange, no range holds both source and target data (in-place) and no target
+        // range is shared by two jobs (their updates would have to be applied in order).
+        bool pipe_ok = host_staging_mode() == 1 && c->size == 1 && !c->nccl &&
+                       std::none_of(on_dev.begin(), on_dev.end(), [](bool d) { return d; });
+        for (uint8_t f : range_flags)
+            if ((f & 3) == 3 || (f & 4)) pipe_ok = false;
+        if (pipe_ok) {
+            cp->staged = false;
+            cp->p = make_plan(jobs, c->rank, c->size, 0);  // host addresses
+            cp->pipe = make_host_pipeline(cp->p->dtype, cp->p->local_ops);
+            g_plans.emplace_front(h.h, std::move(cp));
+            while (g_plans.size() > kMaxPlans) g_plans.pop_back();
+            return g_plans.front().second.get();
+        }
+        cp->stage.reserve(std::max<size_t>(off, 256));
         staged_ranges = ranges;
         remapped.reserve(jobs.size() * 2);
         k = 0;
@@ -686,6 +719,7 @@ void upload_scalars(cached_plan& cp, const std::vector<job>& jobs, hipStream_t s
 void release_caches() {
     std::lock_guard<std::recursive_mutex> lk(g_mutex);
     g_plans.clear();
+    release_host_rings();
     ctx_map().clear();
 }
 
@@ -773,7 +807,7 @@ void transform(const std::vector<job>& jobs, comm* c, void* user_stream, bool as
     cached_plan& cp = *get_plan(jobs, c, dc);
     const plan& p = *cp.p;
     const size_t E = dtype_size(p.dtype);
-    if (async && cp.staged)
+    if (async && (cp.staged || cp.pipe))
         throw error(COSTA_ERR_ARG,
                     "costa: asynchronous transforms need device-resident layouts (host data is "
                     "staged synchronously)");
@@ -785,6 +819,11 @@ void transform(const std::vector<job>& jobs, comm* c, void* user_stream, bool as
         HIP_CHECK(hipStreamWaitEvent(dc.main, dc.ev_user, 0));
     }
     upload_scalars(cp, jobs, dc.main);
+    if (cp.pipe) {  // host-resident, single rank: pipelined H2D -> kernels -> D2H
+        run_host_pipeline(*cp.pipe, c->device, dc.main, cp.d_scal.p);
+        g_stats.transforms++;
+        return;
+    }
     phase_timer tm(dc, g_profiling);
 
     // H2D of host-resident data

@@ -161,6 +161,21 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
 launch_args make_launch(const work_split& w, const void* d_ordered, const void* d_work,
                         const char* src_base, char* dst_base, const void* d_scalars, bool transpose);
 
+// ---- host-resident pipeline (host_pipe.cpp) ----
+// Single-rank transforms whose layouts all live in host memory: the local ops in groups of
+// dense packages moving through a pinned/device slot ring (H2D, kernels and D2H overlap).
+struct host_pipeline;
+std::shared_ptr<host_pipeline> make_host_pipeline(costa_dtype_t dtype,
+                                                  const std::vector<costa_tile_op_t>& ops);
+size_t host_pipeline_groups(const host_pipeline& hp);
+// blocking: returns when every target byte is back in host memory
+void run_host_pipeline(host_pipeline& hp, int device, void* main_stream, const void* d_scalars);
+void release_host_rings();
+// host staging of host-resident layouts: 0 = mirror (every spanned range up, kernels, target
+// ranges down), 1 = pipelined (default; falls back to the mirror where it does not apply)
+int host_staging_mode();
+void set_host_staging_mode(int mode);
+
 // errors
 struct error : std::runtime_error {
     int code;

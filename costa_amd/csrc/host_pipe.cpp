@@ -1,0 +1,457 @@
+// Host-resident transforms as a pipeline over PCIe.
+//
+// The reference's path starts and ends in host memory (each rank's local matrix buffer).  The
+// mirror scheme of engine.cpp uploads every byte range a layout spans, runs the kernels, and
+// copies the target ranges back: one direction at a time, so a call costs H2D + D2H.  Here the
+// local tile ops are cut into groups of at most kSlot bytes of source and target data, and each
+// group moves through a ring of slots:
+//
+//   host threads : gather the group's source tiles (and, for beta != 0, its old target tiles)
+//                  densely into a pinned slot                         [the reference's PACK
+//                  format, communication_data.cpp:191-217: stored shape, dense]
+//   copy stream 1: pinned slot -> device slot (H2D)
+//   main stream  : the tile kernels, rewritten to read the dense source package and write a
+//                  dense target package (copy_and_transform of every tile, on the GPU)
+//   copy stream 2: device target package -> pinned slot (D2H)
+//   host threads : scatter the target package into the caller's C
+//
+// so H2D of group g+1, the kernels of group g and D2H of group g-1 overlap: the two copy
+// directions run at the same time (PCIe is full duplex only from pinned memory: 56 GB/s for
+// H2D and D2H together from pageable memory, 97 GB/s from pinned, tools/pcie_probe.hip,
+// profiles/r07/pcie_probe.log).  Device memory needed: the ring, not a mirror of A and C.
+// Only C bytes the ops write are ever stored to the caller's memory.  The host threads move
+// bytes only (strided memcpy); every element's transform runs in the tile kernels.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <mutex>
+#include <thread>
+
+#include "engine.hpp"
+
+namespace costa {
+namespace engine {
+
+#define HP_CHECK(x)                                                                    \
+    do {                                                                               \
+        hipError_t e_ = (x);                                                           \
+        if (e_ != hipSuccess)                                                          \
+            throw error(COSTA_ERR_HIP, std::string(#x " failed: ") + hipGetErrorString(e_)); \
+    } while (0)
+
+namespace {
+
+constexpr size_t kSlot = size_t(32) << 20;    // source (and target) bytes per group
+constexpr int kRing = 4;                      // slots in flight
+constexpr int kLag = 2;                       // scatter of group g runs at step g + kLag
+constexpr size_t kItemBytes = size_t(256) << 10;  // host copy work item
+constexpr size_t kAlign = 256;
+
+size_t align_up(size_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
+
+// ---------------------------------------------------------------- host thread pool
+class pool {
+  public:
+    explicit pool(int n) {
+        for (int i = 0; i < n - 1; ++i) th_.emplace_back([this] { loop(); });
+    }
+    ~pool() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    // run f(0..n-1) on the workers and the calling thread; returns when all are done
+    void run(size_t n, const std::function<void(size_t)>& f) {
+        if (n == 0) return;
+        if (th_.empty() || n == 1) {
+            for (size_t i = 0; i < n; ++i) f(i);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            fn_ = &f;
+            n_ = n;
+            next_.store(0);
+            busy_ = th_.size();
+            ++gen_;
+        }
+        cv_.notify_all();
+        work();
+        std::unique_lock<std::mutex> lk(m_);
+        done_.wait(lk, [this] { return busy_ == 0; });
+        fn_ = nullptr;
+    }
+
+  private:
+    void work() {
+        for (size_t i; (i = next_.fetch_add(1)) < n_;) (*fn_)(i);
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+            }
+            work();
+            std::lock_guard<std::mutex> lk(m_);
+            if (--busy_ == 0) done_.notify_all();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(size_t)>* fn_ = nullptr;
+    size_t n_ = 0;
+    std::atomic<size_t> next_{0};
+    size_t busy_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+int host_threads() {
+    if (const char* s = std::getenv("COSTA_HOST_THREADS")) return std::max(1, std::atoi(s));
+    const int hw = int(std::thread::hardware_concurrency());
+    return std::max(1, std::min(16, hw));
+}
+
+pool& thread_pool() {  // never destroyed: its threads outlive static destruction at exit
+    static pool* p = new pool(host_threads());
+    return *p;
+}
+
+// ---------------------------------------------------------------- per-device ring
+struct ring {
+    int device = 0;
+    hipStream_t up = nullptr, down = nullptr;
+    char* pin_in = nullptr;   // kRing x 2*kSlot: [source package | old target package]
+    char* pin_out = nullptr;  // kRing x kSlot: target package
+    char* dev = nullptr;      // kRing x 2*kSlot: [source package | target package]
+    hipEvent_t up_done[kRing]{}, kern_done[kRing]{}, down_done[kRing]{};
+    explicit ring(int d) : device(d) {
+        HP_CHECK(hipStreamCreateWithFlags(&up, hipStreamNonBlocking));
+        HP_CHECK(hipStreamCreateWithFlags(&down, hipStreamNonBlocking));
+        HP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&pin_in), kRing * 2 * kSlot, hipHostMallocDefault));
+        HP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&pin_out), kRing * kSlot, hipHostMallocDefault));
+        HP_CHECK(hipMalloc(reinterpret_cast<void**>(&dev), kRing * 2 * kSlot));
+        for (int k = 0; k < kRing; ++k)
+            for (hipEvent_t* e : {&up_done[k], &kern_done[k], &down_done[k]})
+                HP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    }
+    ~ring() {
+        (void)hipSetDevice(device);
+        (void)hipStreamSynchronize(up);
+        (void)hipStreamSynchronize(down);
+        for (int k = 0; k < kRing; ++k)
+            for (hipEvent_t e : {up_done[k], kern_done[k], down_done[k]}) (void)hipEventDestroy(e);
+        (void)hipFree(dev);
+        (void)hipHostFree(pin_in);
+        (void)hipHostFree(pin_out);
+        (void)hipStreamDestroy(up);
+        (void)hipStreamDestroy(down);
+    }
+};
+
+std::map<int, std::unique_ptr<ring>>& rings() {  // freed by release_caches(), not at exit
+    static auto* m = new std::map<int, std::unique_ptr<ring>>;
+    return *m;
+}
+
+ring& ring_of(int device) {
+    auto& m = rings();
+    auto it = m.find(device);
+    if (it == m.end()) it = m.emplace(device, std::make_unique<ring>(device)).first;
+    return *it->second;
+}
+
+}  // namespace
+
+void release_host_rings() { rings().clear(); }
+
+// ---------------------------------------------------------------- the pipeline of one plan
+struct host_pipeline {
+    struct hop {          // one op (or piece of one) with its host addresses
+        costa_tile_op_t op;
+        uint64_t in_off, out_off;  // offsets in the group's source / target packages
+    };
+    struct item {         // host copy work item: rows [lo, hi) of op `k`'s slow dimension
+        uint32_t k;
+        int32_t lo, hi;
+    };
+    struct group {
+        size_t first = 0, count = 0;  // hops
+        size_t in_bytes = 0, out_bytes = 0;
+        bool reads_old = false;
+        std::vector<item> gather, scatter;  // scatter items double as old-target gathers
+        work_split split;
+        size_t ord_first = 0, work_first = 0;
+        bool any_tr = false;
+        int64_t alg_bytes = 0;
+    };
+    costa_dtype_t dtype = COSTA_DOUBLE;
+    size_t E = 8;
+    std::vector<hop> hops;
+    std::vector<group> groups;
+    void* d_ops = nullptr;   // every group's ordered device ops (package offsets)
+    void* d_work = nullptr;
+    ~host_pipeline() {
+        if (d_ops) (void)hipFree(d_ops);
+        if (d_work) (void)hipFree(d_work);
+    }
+};
+
+namespace {
+
+// contiguous run length and count of the target side of an op (copy: columns of nf elements;
+// transpose: rows of ns elements)
+inline void target_shape(const costa_tile_op_t& op, int64_t& run, int64_t& runs) {
+    const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
+    run = tr ? op.ns : op.nf;
+    runs = tr ? op.nf : op.ns;
+}
+
+void add_items(std::vector<host_pipeline::item>& v, uint32_t k, int64_t run_bytes, int64_t runs) {
+    const int64_t per = std::max<int64_t>(1, int64_t(kItemBytes) / std::max<int64_t>(1, run_bytes));
+    for (int64_t lo = 0; lo < runs; lo += per)
+        v.push_back({k, int32_t(lo), int32_t(std::min(runs, lo + per))});
+}
+
+}  // namespace
+
+std::shared_ptr<host_pipeline> make_host_pipeline(costa_dtype_t dtype,
+                                                  const std::vector<costa_tile_op_t>& ops) {
+    auto hp = std::make_shared<host_pipeline>();
+    hp->dtype = dtype;
+    const size_t E = dtype_size(dtype);
+    hp->E = E;
+    const int64_t cap = int64_t(kSlot / E);  // elements per piece
+    // cut ops over a slot into pieces (a sub-rectangle of a tile op is a tile op)
+    std::vector<costa_tile_op_t> pieces;
+    pieces.reserve(ops.size());
+    for (const auto& op : ops) {
+        if (op.nf <= 0 || op.ns <= 0) continue;
+        if (align_up(size_t(op.nf) * size_t(op.ns) * E) <= kSlot) {
+            pieces.push_back(op);
+            continue;
+        }
+        const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
+        const int64_t cf = std::min<int64_t>(op.nf, cap - int64_t(kAlign / E));
+        const int64_t cs = std::max<int64_t>(1, (cap - int64_t(kAlign / E)) / cf);
+        for (int64_t f0 = 0; f0 < op.nf; f0 += cf)
+            for (int64_t s0 = 0; s0 < op.ns; s0 += cs) {
+                costa_tile_op_t p = op;
+                p.nf = int32_t(std::min<int64_t>(cf, op.nf - f0));
+                p.ns = int32_t(std::min<int64_t>(cs, op.ns - s0));
+                p.src = op.src + uint64_t((s0 * op.lds + f0) * int64_t(E));
+                p.dst = op.dst + uint64_t((tr ? f0 * op.ldd + s0 : s0 * op.ldd + f0) * int64_t(E));
+                pieces.push_back(p);
+            }
+    }
+    // groups in list order (the planner's target-key order: for block-cyclic layouts a group
+    // is a band of target rows, read from a band of source columns)
+    host_pipeline::group g;
+    auto close = [&] {
+        if (g.count) hp->groups.push_back(std::move(g));
+        g = host_pipeline::group{};
+        g.first = hp->hops.size();
+    };
+    g.first = 0;
+    for (const auto& p : pieces) {
+        const size_t bytes = align_up(size_t(p.nf) * size_t(p.ns) * E);
+        if (g.in_bytes + bytes > kSlot || g.out_bytes + bytes > kSlot) close();
+        hp->hops.push_back({p, g.in_bytes, g.out_bytes});
+        g.in_bytes += bytes;
+        g.out_bytes += bytes;
+        ++g.count;
+    }
+    close();
+
+    // device op lists: every op reads the dense source package (lds = nf) and writes the
+    // dense target package (ldd = contiguous run of the target); bases are added at launch
+    std::vector<costa_tile_op_t> all_ord;
+    std::vector<uint64_t> all_work;
+    for (auto& gr : hp->groups) {
+        std::vector<costa_tile_op_t> dev_ops;
+        dev_ops.reserve(gr.count);
+        for (size_t i = gr.first; i < gr.first + gr.count; ++i) {
+            const auto& h = hp->hops[i];
+            costa_tile_op_t d = h.op;
+            int64_t run, runs;
+            target_shape(d, run, runs);
+            d.src = h.in_off;
+            d.lds = d.nf;
+            d.dst = h.out_off;
+            d.ldd = int32_t(run);
+            d.flags &= ~uint32_t(COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST);
+            if ((int64_t(d.lds) * int64_t(E)) % 16 == 0) d.flags |= COSTA_TILE_VEC_SRC;
+            if ((int64_t(d.ldd) * int64_t(E)) % 16 == 0) d.flags |= COSTA_TILE_VEC_DST;
+            dev_ops.push_back(d);
+            const uint32_t kind = (d.flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT;
+            if (kind == COSTA_SCALE_AXPBY) gr.reads_old = true;
+            const int64_t n = int64_t(d.nf) * d.ns;
+            gr.alg_bytes += int64_t(E) * n * (1 + (kind != COSTA_SCALE_ZERO) + (kind == COSTA_SCALE_AXPBY));
+            const uint32_t k = uint32_t(i);
+            add_items(gr.gather, k, int64_t(d.nf) * int64_t(E), d.ns);
+            add_items(gr.scatter, k, run * int64_t(E), runs);
+        }
+        gr.any_tr = any_transpose(dev_ops);
+        std::vector<costa_tile_op_t> ord;
+        std::vector<uint64_t> work;
+        gr.split = build_work(dtype, dev_ops, ord, work);
+        gr.ord_first = all_ord.size();
+        gr.work_first = all_work.size();
+        all_ord.insert(all_ord.end(), ord.begin(), ord.end());
+        all_work.insert(all_work.end(), work.begin(), work.end());
+    }
+    if (!all_ord.empty()) {
+        HP_CHECK(hipMalloc(&hp->d_ops, all_ord.size() * sizeof(costa_tile_op_t)));
+        HP_CHECK(hipMemcpy(hp->d_ops, all_ord.data(), all_ord.size() * sizeof(costa_tile_op_t),
+                           hipMemcpyHostToDevice));
+    }
+    if (!all_work.empty()) {
+        HP_CHECK(hipMalloc(&hp->d_work, all_work.size() * sizeof(uint64_t)));
+        HP_CHECK(hipMemcpy(hp->d_work, all_work.data(), all_work.size() * sizeof(uint64_t),
+                           hipMemcpyHostToDevice));
+    }
+    return hp;
+}
+
+size_t host_pipeline_groups(const host_pipeline& hp) { return hp.groups.size(); }
+
+void run_host_pipeline(host_pipeline& hp, int device, void* main_stream, const void* d_scalars) {
+    ring& R = ring_of(device);
+    hipStream_t comp = static_cast<hipStream_t>(main_stream);
+    pool& P = thread_pool();
+    const size_t E = hp.E;
+    const size_t G = hp.groups.size();
+    const bool prof = profiling();
+    // timing brackets (profiling only): per group kernel, and the spans of both copy streams
+    std::vector<hipEvent_t> evs;
+    auto ev = [&](hipStream_t s) {
+        hipEvent_t e;
+        HP_CHECK(hipEventCreate(&e));
+        evs.push_back(e);
+        HP_CHECK(hipEventRecord(e, s));
+        return e;
+    };
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> kern_t;
+    hipEvent_t up0 = nullptr, up1 = nullptr, dn0 = nullptr, dn1 = nullptr;
+    // every slot starts free: the ring's events are recorded on idle streams
+    for (int k = 0; k < kRing; ++k) {
+        HP_CHECK(hipEventRecord(R.up_done[k], R.up));
+        HP_CHECK(hipEventRecord(R.down_done[k], R.down));
+    }
+
+    auto gather = [&](const host_pipeline::group& g, char* pin) {
+        P.run(g.gather.size(), [&](size_t i) {
+            const auto& it = g.gather[i];
+            const auto& h = hp.hops[it.k];
+            const size_t run = size_t(h.op.nf) * E;
+            const char* src = reinterpret_cast<const char*>(h.op.src);
+            char* dst = pin + h.in_off;
+            for (int64_t s = it.lo; s < it.hi; ++s)
+                std::memcpy(dst + size_t(s) * run, src + size_t(s) * size_t(h.op.lds) * E, run);
+        });
+        if (!g.reads_old) return;
+        P.run(g.scatter.size(), [&](size_t i) {  // old target values, for beta != 0 ops only
+            const auto& it = g.scatter[i];
+            const auto& h = hp.hops[it.k];
+            if (((h.op.flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT) != COSTA_SCALE_AXPBY) return;
+            int64_t run, runs;
+            target_shape(h.op, run, runs);
+            const size_t rb = size_t(run) * E;
+            const char* src = reinterpret_cast<const char*>(h.op.dst);
+            char* dst = pin + kSlot + h.out_off;
+            for (int64_t r = it.lo; r < it.hi; ++r)
+                std::memcpy(dst + size_t(r) * rb, src + size_t(r) * size_t(h.op.ldd) * E, rb);
+        });
+    };
+    auto scatter = [&](const host_pipeline::group& g, const char* pin) {
+        P.run(g.scatter.size(), [&](size_t i) {
+            const auto& it = g.scatter[i];
+            const auto& h = hp.hops[it.k];
+            int64_t run, runs;
+            target_shape(h.op, run, runs);
+            const size_t rb = size_t(run) * E;
+            char* dst = reinterpret_cast<char*>(h.op.dst);
+            const char* src = pin + h.out_off;
+            for (int64_t r = it.lo; r < it.hi; ++r)
+                std::memcpy(dst + size_t(r) * size_t(h.op.ldd) * E, src + size_t(r) * rb, rb);
+        });
+    };
+
+    for (size_t t = 0; t < G + kLag; ++t) {
+        if (t < G) {
+            const auto& g = hp.groups[t];
+            const int k = int(t % kRing);
+            char* pin = R.pin_in + size_t(k) * 2 * kSlot;
+            char* dev = R.dev + size_t(k) * 2 * kSlot;
+            // the pinned slot is free once its previous upload has landed
+            HP_CHECK(hipEventSynchronize(R.up_done[k]));
+            gather(g, pin);
+            // the device slot is free once its previous target package has been copied out
+            HP_CHECK(hipStreamWaitEvent(R.up, R.down_done[k], 0));
+            if (prof && !up0) up0 = ev(R.up);
+            HP_CHECK(hipMemcpyAsync(dev, pin, g.in_bytes, hipMemcpyHostToDevice, R.up));
+            if (g.reads_old)
+                HP_CHECK(hipMemcpyAsync(dev + kSlot, pin + kSlot, g.out_bytes, hipMemcpyHostToDevice, R.up));
+            HP_CHECK(hipEventRecord(R.up_done[k], R.up));
+            if (prof && t + 1 == G) up1 = ev(R.up);
+            HP_CHECK(hipStreamWaitEvent(comp, R.up_done[k], 0));
+            hipEvent_t k0 = prof ? ev(comp) : nullptr;
+            launch_tiles(hp.dtype,
+                         make_launch(g.split,
+                                     static_cast<const costa_tile_op_t*>(hp.d_ops) + g.ord_first,
+                                     static_cast<const uint64_t*>(hp.d_work) + g.work_first, dev,
+                                     dev + kSlot, d_scalars, g.any_tr),
+                         comp);
+            if (prof) kern_t.push_back({k0, ev(comp)});
+            HP_CHECK(hipEventRecord(R.kern_done[k], comp));
+            // the pinned target slot was scattered at step t - kRing + kLag < t
+            HP_CHECK(hipStreamWaitEvent(R.down, R.kern_done[k], 0));
+            if (prof && !dn0) dn0 = ev(R.down);
+            HP_CHECK(hipMemcpyAsync(R.pin_out + size_t(k) * kSlot, dev + kSlot, g.out_bytes,
+                                    hipMemcpyDeviceToHost, R.down));
+            HP_CHECK(hipEventRecord(R.down_done[k], R.down));
+            if (prof && t + 1 == G) dn1 = ev(R.down);
+        }
+        if (t >= size_t(kLag)) {
+            const size_t u = t - kLag;
+            const int k = int(u % kRing);
+            HP_CHECK(hipEventSynchronize(R.down_done[k]));
+            scatter(hp.groups[u], R.pin_out + size_t(k) * kSlot);
+        }
+    }
+    HP_CHECK(hipStreamSynchronize(R.up));
+    HP_CHECK(hipStreamSynchronize(comp));
+    HP_CHECK(hipStreamSynchronize(R.down));
+
+    auto& st = stats();
+    for (const auto& g : hp.groups) st.local_bytes += g.alg_bytes;
+    st.local_launches += int64_t(G);
+    st.host_groups += int64_t(G);
+    if (prof) {
+        float ms = 0.f;
+        for (auto& kt : kern_t) {
+            HP_CHECK(hipEventElapsedTime(&ms, kt.first, kt.second));
+            st.local_ms += ms;
+        }
+        if (up0 && up1 && hipEventElapsedTime(&ms, up0, up1) == hipSuccess) st.h2d_ms += ms;
+        if (dn0 && dn1 && hipEventElapsedTime(&ms, dn0, dn1) == hipSuccess) st.d2h_ms += ms;
+    }
+    for (hipEvent_t e : evs) (void)hipEventDestroy(e);
+}
+
+}  // namespace engine
+}  // namespace costa

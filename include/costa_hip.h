@@ -204,11 +204,21 @@ typedef struct {
     int64_t pack_bytes, local_bytes, unpack_bytes; /* algorithmic HBM bytes */
     int64_t transforms;
     int64_t plan_hits, plan_misses;
+    int64_t host_groups; /* tile groups moved by the pipelined host staging */
 } costa_stats_t;
 int costa_hip_set_profiling(int on);
 int costa_hip_get_stats(costa_stats_t* out, int reset);
 /* drop cached plans and device workspaces of this process */
 int costa_hip_release_caches(void);
+
+/* ---- host-resident layouts ----
+ * How a transform whose layouts live in host memory reaches HBM (the reference's path starts
+ * and ends in each rank's host buffers).  1 (default; env COSTA_HOST_STAGING): pipelined --
+ * single-rank calls move the local tiles in 32 MiB groups through pinned/device slot rings,
+ * host gather -> H2D -> tile kernels -> D2H -> host scatter, both copy directions at once;
+ * other calls fall back to 0.  0: mirror -- every byte range the layouts span is uploaded, the
+ * kernels run on the mirror, the target ranges are copied back.  Results are identical. */
+int costa_hip_set_host_staging(int mode);
 
 #ifdef __cplusplus
 }
