@@ -21,10 +21,13 @@
 // profiles/r07/pcie_probe.log).  Device memory needed: the ring, not a mirror of A and C.
 // Only C bytes the ops write are ever stored to the caller's memory.  The host threads move
 // bytes only (strided memcpy); every element's transform runs in the tile kernels.
+#include <emmintrin.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -47,13 +50,46 @@ namespace engine {
 
 namespace {
 
-constexpr size_t kSlot = size_t(32) << 20;    // source (and target) bytes per group
+// source (and target) bytes per group; COSTA_HOST_SLOT_MIB overrides (tuning)
+const size_t kSlot = [] {
+    const char* s = std::getenv("COSTA_HOST_SLOT_MIB");
+    const long v = s ? std::atol(s) : 32;
+    return size_t(std::max(1L, std::min(1024L, v))) << 20;
+}();
 constexpr int kRing = 4;                      // slots in flight
-constexpr int kLag = 2;                       // scatter of group g runs at step g + kLag
+constexpr int kLag = 3;                       // scatter of group g runs at step g + kLag
+static_assert(kLag < kRing, "a pinned target slot is scattered before its reuse");
 constexpr size_t kItemBytes = size_t(256) << 10;  // host copy work item
 constexpr size_t kAlign = 256;
 
 size_t align_up(size_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
+
+// Copy n bytes, storing whole 16-byte blocks of the destination with streaming (non-temporal)
+// stores: neither the pinned packages nor the caller's C are read again by this host, and a
+// streaming store skips the read-for-ownership of the line.  The caller fences.
+inline void copy_nt(char* dst, const char* src, size_t n) {
+    if (n < 256) {
+        std::memcpy(dst, src, n);
+        return;
+    }
+    const size_t head = (16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15;
+    std::memcpy(dst, src, head);
+    dst += head;
+    src += head;
+    n -= head;
+    const size_t body = n & ~size_t(63);
+    for (size_t i = 0; i < body; i += 64) {
+        const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
+        const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 16));
+        const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 32));
+        const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 48));
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), a);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 32), c);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 48), d);
+    }
+    std::memcpy(dst + body, src + body, n - body);
+}
 
 // ---------------------------------------------------------------- host thread pool
 class pool {
@@ -353,86 +389,109 @@ void run_host_pipeline(host_pipeline& hp, int device, void* main_stream, const v
         HP_CHECK(hipEventRecord(R.down_done[k], R.down));
     }
 
-    auto gather = [&](const host_pipeline::group& g, char* pin) {
-        P.run(g.gather.size(), [&](size_t i) {
-            const auto& it = g.gather[i];
-            const auto& h = hp.hops[it.k];
-            const size_t run = size_t(h.op.nf) * E;
-            const char* src = reinterpret_cast<const char*>(h.op.src);
-            char* dst = pin + h.in_off;
-            for (int64_t s = it.lo; s < it.hi; ++s)
-                std::memcpy(dst + size_t(s) * run, src + size_t(s) * size_t(h.op.lds) * E, run);
-        });
-        if (!g.reads_old) return;
-        P.run(g.scatter.size(), [&](size_t i) {  // old target values, for beta != 0 ops only
-            const auto& it = g.scatter[i];
-            const auto& h = hp.hops[it.k];
-            if (((h.op.flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT) != COSTA_SCALE_AXPBY) return;
-            int64_t run, runs;
-            target_shape(h.op, run, runs);
-            const size_t rb = size_t(run) * E;
-            const char* src = reinterpret_cast<const char*>(h.op.dst);
-            char* dst = pin + kSlot + h.out_off;
-            for (int64_t r = it.lo; r < it.hi; ++r)
-                std::memcpy(dst + size_t(r) * rb, src + size_t(r) * size_t(h.op.ldd) * E, rb);
-        });
-    };
-    auto scatter = [&](const host_pipeline::group& g, const char* pin) {
-        P.run(g.scatter.size(), [&](size_t i) {
-            const auto& it = g.scatter[i];
-            const auto& h = hp.hops[it.k];
-            int64_t run, runs;
-            target_shape(h.op, run, runs);
-            const size_t rb = size_t(run) * E;
-            char* dst = reinterpret_cast<char*>(h.op.dst);
-            const char* src = pin + h.out_off;
-            for (int64_t r = it.lo; r < it.hi; ++r)
-                std::memcpy(dst + size_t(r) * size_t(h.op.ldd) * E, src + size_t(r) * rb, rb);
+    // Host copy work of one step: the source gather of group t (plus its old target values
+    // when an op reads C) and the target scatter of group t - kLag, in one parallel pass.
+    auto host_step = [&](const host_pipeline::group* g, char* pin, const host_pipeline::group* o,
+                         const char* pout) {
+        const size_t ng = g ? g->gather.size() : 0;
+        const size_t nold = g && g->reads_old ? g->scatter.size() : 0;
+        const size_t ns = o ? o->scatter.size() : 0;
+        P.run(ng + nold + ns, [&](size_t i) {
+            if (i < ng) {  // source tile columns -> dense package
+                const auto& it = g->gather[i];
+                const auto& h = hp.hops[it.k];
+                const size_t run = size_t(h.op.nf) * E;
+                const char* src = reinterpret_cast<const char*>(h.op.src);
+                char* dst = pin + h.in_off;
+                for (int64_t s = it.lo; s < it.hi; ++s)
+                    copy_nt(dst + size_t(s) * run, src + size_t(s) * size_t(h.op.lds) * E, run);
+            } else if (i < ng + nold) {  // old target values, for beta != 0 ops only
+                const auto& it = g->scatter[i - ng];
+                const auto& h = hp.hops[it.k];
+                if (((h.op.flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT) != COSTA_SCALE_AXPBY)
+                    return;
+                int64_t run, runs;
+                target_shape(h.op, run, runs);
+                const size_t rb = size_t(run) * E;
+                const char* src = reinterpret_cast<const char*>(h.op.dst);
+                char* dst = pin + kSlot + h.out_off;
+                for (int64_t r = it.lo; r < it.hi; ++r)
+                    copy_nt(dst + size_t(r) * rb, src + size_t(r) * size_t(h.op.ldd) * E, rb);
+            } else {  // dense target package -> the caller's C
+                const auto& it = o->scatter[i - ng - nold];
+                const auto& h = hp.hops[it.k];
+                int64_t run, runs;
+                target_shape(h.op, run, runs);
+                const size_t rb = size_t(run) * E;
+                char* dst = reinterpret_cast<char*>(h.op.dst);
+                const char* src = pout + h.out_off;
+                for (int64_t r = it.lo; r < it.hi; ++r)
+                    copy_nt(dst + size_t(r) * size_t(h.op.ldd) * E, src + size_t(r) * rb, rb);
+            }
+            _mm_sfence();  // streaming stores globally visible before the DMA / the caller
         });
     };
 
+    // COSTA_HOST_PIPE_TRACE=1: host-side time split (copies / waits / issue) on stderr
+    static const bool trace = std::getenv("COSTA_HOST_PIPE_TRACE") != nullptr;
+    double t_copy = 0, t_wait_up = 0, t_wait_down = 0, t_issue = 0;
+    auto now = [] {
+        return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    };
+    const double t_begin = now();
     for (size_t t = 0; t < G + kLag; ++t) {
-        if (t < G) {
-            const auto& g = hp.groups[t];
-            const int k = int(t % kRing);
-            char* pin = R.pin_in + size_t(k) * 2 * kSlot;
-            char* dev = R.dev + size_t(k) * 2 * kSlot;
-            // the pinned slot is free once its previous upload has landed
-            HP_CHECK(hipEventSynchronize(R.up_done[k]));
-            gather(g, pin);
-            // the device slot is free once its previous target package has been copied out
-            HP_CHECK(hipStreamWaitEvent(R.up, R.down_done[k], 0));
-            if (prof && !up0) up0 = ev(R.up);
-            HP_CHECK(hipMemcpyAsync(dev, pin, g.in_bytes, hipMemcpyHostToDevice, R.up));
-            if (g.reads_old)
-                HP_CHECK(hipMemcpyAsync(dev + kSlot, pin + kSlot, g.out_bytes, hipMemcpyHostToDevice, R.up));
-            HP_CHECK(hipEventRecord(R.up_done[k], R.up));
-            if (prof && t + 1 == G) up1 = ev(R.up);
-            HP_CHECK(hipStreamWaitEvent(comp, R.up_done[k], 0));
-            hipEvent_t k0 = prof ? ev(comp) : nullptr;
-            launch_tiles(hp.dtype,
-                         make_launch(g.split,
-                                     static_cast<const costa_tile_op_t*>(hp.d_ops) + g.ord_first,
-                                     static_cast<const uint64_t*>(hp.d_work) + g.work_first, dev,
-                                     dev + kSlot, d_scalars, g.any_tr),
-                         comp);
-            if (prof) kern_t.push_back({k0, ev(comp)});
-            HP_CHECK(hipEventRecord(R.kern_done[k], comp));
-            // the pinned target slot was scattered at step t - kRing + kLag < t
-            HP_CHECK(hipStreamWaitEvent(R.down, R.kern_done[k], 0));
-            if (prof && !dn0) dn0 = ev(R.down);
-            HP_CHECK(hipMemcpyAsync(R.pin_out + size_t(k) * kSlot, dev + kSlot, g.out_bytes,
-                                    hipMemcpyDeviceToHost, R.down));
-            HP_CHECK(hipEventRecord(R.down_done[k], R.down));
-            if (prof && t + 1 == G) dn1 = ev(R.down);
-        }
-        if (t >= size_t(kLag)) {
-            const size_t u = t - kLag;
-            const int k = int(u % kRing);
-            HP_CHECK(hipEventSynchronize(R.down_done[k]));
-            scatter(hp.groups[u], R.pin_out + size_t(k) * kSlot);
-        }
+        const int k = int(t % kRing);
+        const host_pipeline::group* g = t < G ? &hp.groups[t] : nullptr;
+        const host_pipeline::group* o = t >= size_t(kLag) ? &hp.groups[t - kLag] : nullptr;
+        const int ko = int((t + kRing - kLag) % kRing);  // slot of group t - kLag
+        char* pin = R.pin_in + size_t(k) * 2 * kSlot;
+        char* dev = R.dev + size_t(k) * 2 * kSlot;
+        double t0 = now();
+        // the pinned source slot is free once its previous upload has landed
+        if (g) HP_CHECK(hipEventSynchronize(R.up_done[k]));
+        double t1 = now();
+        // group t - kLag's target package has landed in its pinned slot
+        if (o) HP_CHECK(hipEventSynchronize(R.down_done[ko]));
+        double t2 = now();
+        host_step(g, pin, o, R.pin_out + size_t(ko) * kSlot);
+        double t3 = now();
+        t_wait_up += t1 - t0;
+        t_wait_down += t2 - t1;
+        t_copy += t3 - t2;
+        if (!g) continue;
+        // the device slot is free once its previous target package has been copied out
+        HP_CHECK(hipStreamWaitEvent(R.up, R.down_done[k], 0));
+        if (prof && !up0) up0 = ev(R.up);
+        HP_CHECK(hipMemcpyAsync(dev, pin, g->in_bytes, hipMemcpyHostToDevice, R.up));
+        if (g->reads_old)
+            HP_CHECK(hipMemcpyAsync(dev + kSlot, pin + kSlot, g->out_bytes, hipMemcpyHostToDevice, R.up));
+        HP_CHECK(hipEventRecord(R.up_done[k], R.up));
+        if (prof && t + 1 == G) up1 = ev(R.up);
+        HP_CHECK(hipStreamWaitEvent(comp, R.up_done[k], 0));
+        hipEvent_t k0 = prof ? ev(comp) : nullptr;
+        launch_tiles(hp.dtype,
+                     make_launch(g->split, static_cast<const costa_tile_op_t*>(hp.d_ops) + g->ord_first,
+                                 static_cast<const uint64_t*>(hp.d_work) + g->work_first, dev,
+                                 dev + kSlot, d_scalars, g->any_tr),
+                     comp);
+        if (prof) kern_t.push_back({k0, ev(comp)});
+        HP_CHECK(hipEventRecord(R.kern_done[k], comp));
+        // the pinned target slot's previous group (t - kRing) was scattered at step
+        // t - kRing + kLag < t
+        HP_CHECK(hipStreamWaitEvent(R.down, R.kern_done[k], 0));
+        if (prof && !dn0) dn0 = ev(R.down);
+        HP_CHECK(hipMemcpyAsync(R.pin_out + size_t(k) * kSlot, dev + kSlot, g->out_bytes,
+                                hipMemcpyDeviceToHost, R.down));
+        HP_CHECK(hipEventRecord(R.down_done[k], R.down));
+        if (prof && t + 1 == G) dn1 = ev(R.down);
+        t_issue += now() - t3;
     }
+    if (trace)
+        std::fprintf(stderr,
+                     "[costa host pipe] groups %zu slot %zu MiB threads %d: total %.2f ms, "
+                     "copies %.2f, wait-up %.2f, wait-down %.2f, issue %.2f\n",
+                     G, kSlot >> 20, host_threads(), (now() - t_begin) * 1e3, t_copy * 1e3,
+                     t_wait_up * 1e3, t_wait_down * 1e3, t_issue * 1e3);
     HP_CHECK(hipStreamSynchronize(R.up));
     HP_CHECK(hipStreamSynchronize(comp));
     HP_CHECK(hipStreamSynchronize(R.down));

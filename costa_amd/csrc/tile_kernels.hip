@@ -353,7 +353,8 @@ __global__ __launch_bounds__(S::NT) void tile_kernel(const costa_tile_op_t* __re
 // TB/s at 2 against 2.95 at 4; copies 3.40 at 8 against 3.36 at 4.
 constexpr int TINY_WAVES_TR = 2;
 constexpr int TINY_WAVES_COPY = 8;
-constexpr int TINY_BYTES = 64;  // bytes in flight per lane per pass
+constexpr int TINY_BYTES = 64;  // bytes in flight per lane per pass (96: -3 %, 128: -35 % on
+                                // cfg 5, profiles/r07/c5_bytes.log)
 
 template <typename T>
 struct lin {  // (f, s) of linear element index e = f + s*n, stepped by 64
