@@ -219,6 +219,12 @@ bool any_transpose(const std::vector<costa_tile_op_t>& ops) {
     return false;
 }
 
+bool any_axpby(const std::vector<costa_tile_op_t>& ops) {
+    for (const auto& op : ops)
+        if (((op.flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT) == COSTA_SCALE_AXPBY) return true;
+    return false;
+}
+
 // Work classes.  An op goes to the large shape (a 1024-thread workgroup per sub-tile) when it
 // holds at least half a large sub-tile of data; every other op runs on the wavefront path
 // (tiny_kernel): ops over a wavefront's budget are first cut, here on the host, into
@@ -343,7 +349,8 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
 }
 
 launch_args make_launch(const work_split& w, const void* d_ordered, const void* d_work,
-                        const char* src_base, char* dst_base, const void* d_scalars, bool transpose) {
+                        const char* src_base, char* dst_base, const void* d_scalars, bool transpose,
+                        bool axpby) {
     launch_args a;
     a.ops = static_cast<const costa_tile_op_t*>(d_ordered);
     a.work = static_cast<const uint64_t*>(d_work);
@@ -355,6 +362,7 @@ launch_args make_launch(const work_split& w, const void* d_ordered, const void* 
     a.dst_base = dst_base;
     a.scalars = d_scalars;
     a.any_transpose = transpose;
+    a.any_axpby = axpby;
     return a;
 }
 
@@ -483,6 +491,7 @@ struct cached_plan {
     dbuf d_local, d_pack, d_unpack, w_local, w_pack, w_unpack, d_scal;
     work_split l_local, l_pack, l_unpack;  // how each work list splits over the kernel shapes
     bool tr_local = true, tr_unpack = true;          // any op of the list transposes
+    bool ax_local = true, ax_unpack = true;          // any op of the list reads C
     std::vector<unsigned char> scal_host;
     std::shared_ptr<host_pipeline> pipe;  // host-resident single-rank calls (host_pipe.cpp)
 };
@@ -679,6 +688,8 @@ cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
     }
     cp->tr_local = any_transpose(p.local_ops);
     cp->tr_unpack = any_transpose(p.unpack_ops);
+    cp->ax_local = any_axpby(p.local_ops);
+    cp->ax_unpack = any_axpby(p.unpack_ops);
     std::vector<costa_tile_op_t> ord_l, ord_p, ord_u;
     std::vector<uint64_t> w_l, w_p, w_u;
     cp->l_local = build_work(p.dtype, p.local_ops, ord_l, w_l);
@@ -847,7 +858,7 @@ void transform(const std::vector<job>& jobs, comm* c, void* user_stream, bool as
         tm.start(PH_LOCAL, ls);
         launch_tiles(p.dtype,
                      make_launch(cp.l_local, cp.d_local.p, cp.w_local.p, nullptr, nullptr,
-                                 cp.d_scal.p, cp.tr_local),
+                                 cp.d_scal.p, cp.tr_local, cp.ax_local),
                      ls);
         tm.stop();
     }
@@ -862,7 +873,7 @@ void transform(const std::vector<job>& jobs, comm* c, void* user_stream, bool as
             tm.start(PH_PACK, dc.main);
             launch_tiles(p.dtype,
                          make_launch(cp.l_pack, cp.d_pack.p, cp.w_pack.p, nullptr, sb, cp.d_scal.p,
-                                     false),
+                                     false, false),
                          dc.main);
             tm.stop();
         }
@@ -888,7 +899,7 @@ void transform(const std::vector<job>& jobs, comm* c, void* user_stream, bool as
             tm.start(PH_UNPACK, dc.main);
             launch_tiles(p.dtype,
                          make_launch(cp.l_unpack, cp.d_unpack.p, cp.w_unpack.p, rb, nullptr,
-                                     cp.d_scal.p, cp.tr_unpack),
+                                     cp.d_scal.p, cp.tr_unpack, cp.ax_unpack),
                          dc.main);
             tm.stop();
         }
@@ -951,7 +962,8 @@ void execute_tiles(costa_dtype_t dtype, const costa_tile_op_t* ops, int64_t n,
     d_scal.upload(sc, dc.main);
     launch_tiles(dtype,
                  make_launch(nl, d_ops.p, d_work.p, static_cast<const char*>(src_base),
-                             static_cast<char*>(dst_base), d_scal.p, any_transpose(v)),
+                             static_cast<char*>(dst_base), d_scal.p, any_transpose(v),
+                             any_axpby(v)),
                  dc.main);
     HIP_CHECK(hipStreamSynchronize(dc.main));
 }

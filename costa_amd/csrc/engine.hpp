@@ -142,8 +142,10 @@ struct launch_args {
     char* dst_base;
     const void* scalars;    // device: n_slots x (alpha, beta) of the dtype
     bool any_transpose;     // false: copy-mode ops only, launch without the LDS tile
+    bool any_axpby;         // false: no op reads its destination (beta == 0 everywhere)
 };
 bool any_transpose(const std::vector<costa_tile_op_t>& ops);
+bool any_axpby(const std::vector<costa_tile_op_t>& ops);
 void launch_tiles(costa_dtype_t dtype, const launch_args& a, void* stream /* hipStream_t */);
 // sub-tile shapes (elements along the source's fast dim, along its slow dim)
 void tile_shapes(costa_dtype_t dtype, int* bf_large, int* bs_large, int* bf_small, int* bs_small);
@@ -159,7 +161,8 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
                       std::vector<costa_tile_op_t>& ordered, std::vector<uint64_t>& work);
 // launch arguments of one ordered op list
 launch_args make_launch(const work_split& w, const void* d_ordered, const void* d_work,
-                        const char* src_base, char* dst_base, const void* d_scalars, bool transpose);
+                        const char* src_base, char* dst_base, const void* d_scalars, bool transpose,
+                        bool axpby);
 
 // ---- host-resident pipeline (host_pipe.cpp) ----
 // Single-rank transforms whose layouts all live in host memory: the local ops in groups of

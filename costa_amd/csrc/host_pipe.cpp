@@ -472,7 +472,7 @@ void run_host_pipeline(host_pipeline& hp, int device, void* main_stream, const v
         launch_tiles(hp.dtype,
                      make_launch(g->split, static_cast<const costa_tile_op_t*>(hp.d_ops) + g->ord_first,
                                  static_cast<const uint64_t*>(hp.d_work) + g->work_first, dev,
-                                 dev + kSlot, d_scalars, g->any_tr),
+                                 dev + kSlot, d_scalars, g->any_tr, g->reads_old),
                      comp);
         if (prof) kern_t.push_back({k0, ev(comp)});
         HP_CHECK(hipEventRecord(R.kern_done[k], comp));

@@ -355,6 +355,9 @@ constexpr int TINY_WAVES_TR = 2;
 constexpr int TINY_WAVES_COPY = 8;
 constexpr int TINY_BYTES = 64;  // bytes in flight per lane per pass (96: -3 %, 128: -35 % on
                                 // cfg 5, profiles/r07/c5_bytes.log)
+// the same for the copy path: 4-byte types 128 (every load of a 2048-element op in flight at
+// once; cfg 5 'N' +3 % over 64 in an interleaved A/B, profiles/r07/c5_copy.log), else 64
+template <typename T> constexpr int tiny_copy_bytes() { return sizeof(T) == 4 ? 128 : 64; }
 
 template <typename T>
 struct lin {  // (f, s) of linear element index e = f + s*n, stepped by 64
@@ -376,8 +379,10 @@ struct lin {  // (f, s) of linear element index e = f + s*n, stepped by 64
 };
 
 // TR = false: the list has no transposing op (the transpose path and its registers are
-// compiled out, so copy-only lists keep a high occupancy)
-template <typename T, int UB, bool TR>
+// compiled out, so copy-only lists keep a high occupancy).  AX = false: no op of the list reads
+// its destination (beta == 0 everywhere), so the copy path holds no old values.  UC: bytes per
+// lane of one copy pass.
+template <typename T, int UB, bool TR, bool AX, int UC>
 __device__ __forceinline__ void tiny_op(const costa_tile_op_t& op, int lane, T* t,
                                         const char* src_base, char* dst_base,
                                         const T* __restrict__ scalars) {
@@ -397,32 +402,44 @@ __device__ __forceinline__ void tiny_op(const costa_tile_op_t& op, int lane, T* 
     constexpr int U = UB / int(sizeof(T)) > 0 ? UB / int(sizeof(T)) : 1;
 
     if (!TR || !(flags & COSTA_TILE_TRANSPOSE)) {
-        // copy mode: dst(f, s) = g(src(f, s)), U independent loads in flight per lane
+        // copy mode: dst(f, s) = g(src(f, s)).  Every load of a pass is issued before the first
+        // store; passes end where the op ends (wave-uniform tests), and the store walk repeats
+        // the load walk instead of keeping every element's address in registers.
+        constexpr int UCE = UC / int(sizeof(T)) > 0 ? UC / int(sizeof(T)) : 1;
         lin<T> p(lane, nf);
-        for (int e0 = 0; e0 < total; e0 += 64 * U) {
-            T x[U], y[U];
-            int fs[U], ss[U];
+        for (int e0 = 0; e0 < total; e0 += 64 * UCE) {
+            T x[UCE];
+            T y[AX ? UCE : 1];
+            const lin<T> q0 = p;
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                x[u] = y[u] = e_zero<T>();
-                fs[u] = p.f;
-                ss[u] = p.s;
-                if (e0 + u * 64 + lane < total) x[u] = src[ss[u] * lds + fs[u]];
+            for (int u = 0; u < UCE; ++u) {
+                if (e0 + u * 64 >= total) break;
+                if (e0 + u * 64 + lane < total) x[u] = src[p.s * lds + p.f];
                 p.step();
             }
-            if (kind == COSTA_SCALE_AXPBY) {
+            if constexpr (AX) {
+                if (kind == COSTA_SCALE_AXPBY) {
+                    lin<T> r = q0;
 #pragma unroll
-                for (int u = 0; u < U; ++u)
-                    if (e0 + u * 64 + lane < total) y[u] = dst[ss[u] * ldd + fs[u]];
+                    for (int u = 0; u < UCE; ++u) {
+                        if (e0 + u * 64 >= total) break;
+                        if (e0 + u * 64 + lane < total) y[u] = dst[r.s * ldd + r.f];
+                        r.step();
+                    }
+                }
             }
+            lin<T> q = q0;
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (e0 + u * 64 + lane >= total) continue;
-                T v = x[u];
-                if (kind != COSTA_SCALE_BITCOPY)
-                    v = scale(v, kind == COSTA_SCALE_AXPBY ? y[u] : e_zero<T>(), kind, conj, alpha,
-                              beta);
-                dst[ss[u] * ldd + fs[u]] = v;
+            for (int u = 0; u < UCE; ++u) {
+                if (e0 + u * 64 >= total) break;
+                if (e0 + u * 64 + lane < total) {
+                    T v = x[u];
+                    if (kind != COSTA_SCALE_BITCOPY)
+                        v = scale(v, AX && kind == COSTA_SCALE_AXPBY ? y[AX ? u : 0] : e_zero<T>(),
+                                  kind, conj, alpha, beta);
+                    dst[q.s * ldd + q.f] = v;
+                }
+                q.step();
             }
         }
         return;
@@ -491,7 +508,7 @@ __device__ __forceinline__ void tiny_op(const costa_tile_op_t& op, int lane, T* 
 // `xcd_remap`: blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup
 // dispatch); renumbering them so that each XCD walks one contiguous slice of the list keeps
 // neighbouring ops (which share partially written cache lines) in one L2.
-template <typename T, int W, int UB, bool TR>
+template <typename T, int W, int UB, bool TR, bool AX, int UC>
 __global__ __launch_bounds__(64 * W) void tiny_kernel(
     const costa_tile_op_t* __restrict__ ops, int64_t n_ops, int k_per_wave, int chunked,
     int xcd_remap, const char* src_base, char* dst_base, const T* __restrict__ scalars,
@@ -515,18 +532,17 @@ __global__ __launch_bounds__(64 * W) void tiny_kernel(
     for (int64_t i = first; i < end; i += step) {
         const costa_tile_op_t op = next;
         if (i + step < end) next = ops[i + step];  // in flight while this op moves its data
-        tiny_op<T, UB, TR>(op, lane, t, src_base, dst_base, scalars);
+        tiny_op<T, UB, TR, AX, UC>(op, lane, t, src_base, dst_base, scalars);
     }
 }
 
 struct tiny_cfg {
     int k = 1;          // ops per wavefront
     int chunked = 0;    // 0: strided assignment, 1: contiguous chunks
-    int waves = 0;      // 0: by list kind (TINY_WAVES_TR / TINY_WAVES_COPY); 4: tuning variant
-    int bytes = TINY_BYTES;
+    int copy_bytes = 0;  // 0: tiny_copy_bytes<T>()
     int xcd = 0;
 };
-const tiny_cfg& tiny_config() {  // COSTA_TINY_{K,CHUNKED,WAVES,BYTES,XCD}: tuning overrides
+const tiny_cfg& tiny_config() {  // COSTA_TINY_{K,CHUNKED,COPY_BYTES,XCD}: tuning overrides
     static tiny_cfg c = [] {
         tiny_cfg x;
         auto env = [](const char* n, int d) {
@@ -535,15 +551,14 @@ const tiny_cfg& tiny_config() {  // COSTA_TINY_{K,CHUNKED,WAVES,BYTES,XCD}: tuni
         };
         x.k = std::max(1, env("COSTA_TINY_K", x.k));
         x.chunked = env("COSTA_TINY_CHUNKED", x.chunked) != 0;
-        x.waves = env("COSTA_TINY_WAVES", x.waves);
-        x.bytes = env("COSTA_TINY_BYTES", x.bytes);
+        x.copy_bytes = env("COSTA_TINY_COPY_BYTES", x.copy_bytes);
         x.xcd = env("COSTA_TINY_XCD", x.xcd) != 0;
         return x;
     }();
     return c;
 }
 
-template <typename T, int W, int UB, bool TR>
+template <typename T, int W, bool TR, bool AX, int UC>
 void launch_tiny_v(const launch_args& a, const tiny_cfg& cfg, hipStream_t stream) {
     const int64_t n = a.n_tiny;
     const int per_wave = a.any_transpose ? int(tiny_lds_bytes / sizeof(T)) : 0;
@@ -551,27 +566,28 @@ void launch_tiny_v(const launch_args& a, const tiny_cfg& cfg, hipStream_t stream
     const int64_t waves = (n + cfg.k - 1) / cfg.k;
     const int64_t blocks = std::min<int64_t>((waves + W - 1) / W, 1LL << 30);
     const int k = int((n + blocks * W - 1) / (blocks * W));  // chunked: covers all ops
-    hipLaunchKernelGGL((tiny_kernel<T, W, UB, TR>), dim3(unsigned(blocks)), dim3(64 * W), lds, stream,
-                       a.ops + a.tiny_first, n, k, cfg.chunked, cfg.xcd, a.src_base, a.dst_base,
-                       static_cast<const T*>(a.scalars), per_wave);
+    hipLaunchKernelGGL((tiny_kernel<T, W, TINY_BYTES, TR, AX, UC>), dim3(unsigned(blocks)),
+                       dim3(64 * W), lds, stream, a.ops + a.tiny_first, n, k, cfg.chunked, cfg.xcd,
+                       a.src_base, a.dst_base, static_cast<const T*>(a.scalars), per_wave);
+}
+
+template <typename T, int UC>
+void launch_tiny_uc(const launch_args& a, const tiny_cfg& cfg, hipStream_t stream) {
+    // transposing lists: TINY_WAVES_TR wavefronts per workgroup; copy-only: TINY_WAVES_COPY
+    if (a.any_transpose)
+        return a.any_axpby ? launch_tiny_v<T, TINY_WAVES_TR, true, true, UC>(a, cfg, stream)
+                           : launch_tiny_v<T, TINY_WAVES_TR, true, false, UC>(a, cfg, stream);
+    a.any_axpby ? launch_tiny_v<T, TINY_WAVES_COPY, false, true, UC>(a, cfg, stream)
+                : launch_tiny_v<T, TINY_WAVES_COPY, false, false, UC>(a, cfg, stream);
 }
 
 template <typename T>
 void launch_tiny(const launch_args& a, hipStream_t stream) {
     if (a.n_tiny <= 0) return;
     const tiny_cfg& cfg = tiny_config();
-    if constexpr (std::is_same<T, float>::value) {  // tuning variants (cfg 5 is fp32)
-        const bool tr = a.any_transpose;
-        if (cfg.waves == 4 && cfg.bytes == 64)
-            return tr ? launch_tiny_v<T, 4, 64, true>(a, cfg, stream)
-                      : launch_tiny_v<T, 4, 64, false>(a, cfg, stream);
-        if (cfg.waves == 4 && cfg.bytes == 32)
-            return tr ? launch_tiny_v<T, 4, 32, true>(a, cfg, stream)
-                      : launch_tiny_v<T, 4, 32, false>(a, cfg, stream);
-    }
-    // transposing lists: TINY_WAVES_TR wavefronts per workgroup; copy-only: TINY_WAVES_COPY
-    if (a.any_transpose) return launch_tiny_v<T, TINY_WAVES_TR, TINY_BYTES, true>(a, cfg, stream);
-    launch_tiny_v<T, TINY_WAVES_COPY, TINY_BYTES, false>(a, cfg, stream);
+    if constexpr (std::is_same<T, float>::value)  // tuning variant (cfg 5 is fp32)
+        if (cfg.copy_bytes == 64) return launch_tiny_uc<T, 64>(a, cfg, stream);
+    launch_tiny_uc<T, tiny_copy_bytes<T>()>(a, cfg, stream);
 }
 
 template <typename T, typename S>

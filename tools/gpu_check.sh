@@ -51,16 +51,4 @@ if [ "${CFG5:-1}" = "1" ]; then
         fi
     done
 fi
-if [ "${KNOBS:-0}" = "1" ]; then  # repeated A/B of wavefront-path variants on cfg 5
-    for rep in 1 2; do
-        for v in "T 4 64 0" "T 2 64 1" "T 2 64 0" "T 4 64 1" "N 4 64 0" "N 8 64 0" "N 8 64 1" "N 2 64 1"; do
-            set -- $v
-            COSTA_TINY_WAVES=$2 COSTA_TINY_BYTES=$3 COSTA_TINY_XCD=$4 timeout -k 10 300 python3 bench.py \
-                --workload cfg5 --cfg5-op $1 --steps 20 --warmup 3 --no-cpu-baseline --no-e2e \
-                > "$OUT/knob.log" 2>&1 || { echo "knob run failed"; exit 3; }
-            python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(sys.argv[2], d['value'], d['kernel_node_GBps'])" \
-                "$OUT/knob.log" "rep$rep op=$1 waves=$2 bytes=$3 xcd=$4" | tee -a "$OUT/c5_knobs.log"
-        done
-    done
-fi
 echo "done"
