@@ -482,6 +482,99 @@ __global__ __launch_bounds__(512) void v_glds(const op_t* ops, const uint64_t* w
     }
 }
 
+// V8: persistent LDS-DMA ring.  One workgroup per CU walks sub-tiles i = blockIdx.x + k*grid;
+// each source column of a BF x BS sub-tile (BF = 128 fp64 = 1 KiB) arrives by one
+// global_load_lds_dwordx4 wave instruction straight into an LDS row (pitch BF + 2); NB buffers,
+// NB - 1 sub-tiles of loads in flight.  The wait before reading sub-tile i counts only the loads
+// of sub-tile i: the stores of earlier sub-tiles and the loads of later ones stay in flight
+// (vmcnt counts in issue order).  Store: lane pairs swap halves so every lane writes 16 B
+// along s (BS s-values per row pair, 64 / BS row pairs per instruction).
+template <int BS, int NT, int NB, int NTL>
+__global__ __launch_bounds__(NT) void v_ring(const op_t* ops, const uint64_t* work, int64_t n) {
+    constexpr int BF = 128, P = BF + 2;
+    constexpr int NW = NT / 64;
+    constexpr int CPW = BS / NW;             // load instructions (columns) per wave per sub-tile
+    constexpr int RPI = 64 / BS;             // row pairs per store instruction
+    constexpr int SI = (BF / 2) / RPI;       // store instructions per sub-tile
+    constexpr int PS = SI / NW;              // per wave
+    static_assert(BS % NW == 0 && SI % NW == 0 && CPW >= 1 && PS >= 1, "mapping");
+    constexpr int WAIT = (NB - 1) * PS + (NB - 2) * CPW;  // vmcnt allowed while sub-tile i lands
+    static_assert(WAIT < 64, "vmcnt range");
+    extern __shared__ __attribute__((aligned(16))) double lds_buf[];  // NB x BS x P
+    const int lane = threadIdx.x % 64;
+    const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / 64);
+    auto geo = [&](int64_t wi, const double*& src, double*& dst, int& ld_s, int& ld_d) {
+        const uint64_t w = work[wi];
+        const op_t op = ops[w >> 32];
+        const uint32_t sub = uint32_t(w);
+        const int nbf = op.nf / BF;
+        const int f0 = int(sub % nbf) * BF, s0 = int(sub / nbf) * BS;
+        src = reinterpret_cast<const double*>(op.src) + int64_t(s0) * op.lds + f0;
+        dst = reinterpret_cast<double*>(op.dst) + int64_t(f0) * op.ldd + s0;
+        ld_s = op.lds;
+        ld_d = op.ldd;
+    };
+    auto issue = [&](int64_t wi, int b) {
+        const double* src;
+        double* dst;
+        int ls, ld;
+        geo(wi, src, dst, ls, ld);
+#pragma unroll
+        for (int k = 0; k < CPW; ++k) {
+            const int c = wave + NW * k;
+            __builtin_amdgcn_global_load_lds(
+                (__attribute__((address_space(1))) void*)(src + int64_t(c) * ls + 2 * lane),
+                (__attribute__((address_space(3))) void*)(&lds_buf[(b * BS + c) * P]), 16, 0,
+                NTL ? 2 : 0);
+        }
+    };
+    const int64_t G = gridDim.x;
+    int64_t i = blockIdx.x;
+    if (i >= n) return;
+    // prologue: NB - 1 sub-tiles in flight
+#pragma unroll
+    for (int q = 0; q < NB - 1; ++q)
+        if (i + q * G < n) issue(i + q * G, q);
+    int b = 0;
+    const bool odd = lane & 1;
+    const int sl = lane % BS, rq = lane / BS;  // s of this lane, row pair within the instruction
+    for (int64_t it = 0;; ++it) {
+        const int64_t cur = i + it * G;
+        if (cur >= n) break;
+        // loads of sub-tile `cur` done; later loads and earlier stores may stay in flight.
+        // Near the end fewer later loads exist: wait for everything then.
+        // (the first NB - 1 sub-tiles have fewer stores behind them: wait for everything)
+        if (it >= NB - 1 && cur + (NB - 2) * G < n)
+            __builtin_amdgcn_s_waitcnt((WAIT & 0xF) | ((WAIT >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+        else
+            __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();  // every wave's DMA into this buffer landed; the oldest buffer is free
+        const int64_t nxt = cur + (NB - 1) * G;
+        if (nxt < n) issue(nxt, (b + NB - 1) % NB);
+        const double* src;
+        double* cdst;
+        int ls, cld;
+        geo(cur, src, cdst, ls, cld);
+        const double* t = &lds_buf[b * BS * P];
+        d2 y[PS];
+#pragma unroll
+        for (int k = 0; k < PS; ++k) {
+            const int rp = (wave + NW * k) * RPI + rq;
+            y[k] = *reinterpret_cast<const d2*>(&t[sl * P + 2 * rp]);
+        }
+#pragma unroll
+        for (int k = 0; k < PS; ++k) {
+            const int rp = (wave + NW * k) * RPI + rq;
+            d2 v = y[k];
+            double got = __shfl_xor(odd ? v.x : v.y, 1);
+            d2 o;
+            if (!odd) { o.x = v.x; o.y = got; } else { o.x = got; o.y = v.y; }
+            *reinterpret_cast<d2*>(cdst + int64_t(2 * rp + (odd ? 1 : 0)) * cld + (sl & ~1)) = o;
+        }
+        b = (b + 1) % NB;
+    }
+}
+
 // ----------------------------------------------------------------------------------
 // ceiling: flat 16-B copy of the same bytes (grid-stride)
 __global__ __launch_bounds__(256) void v_copy(const d2* a, d2* c, int64_t n) {
@@ -635,6 +728,24 @@ int main(int argc, char** argv) {
         CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&v_glds<1>), hipFuncAttributeMaxDynamicSharedMemorySize, glds_bytes));
         V.push_back({"glds 128x64 t512 x1", [&, glds_bytes] { hipLaunchKernelGGL((v_glds<0>), dim3(cus), dim3(512), glds_bytes, 0, d_ops, g128x64.first, g128x64.second); }, true, {}});
         V.push_back({"glds 128x64 t512 x1 nt-load", [&, glds_bytes] { hipLaunchKernelGGL((v_glds<1>), dim3(cus), dim3(512), glds_bytes, 0, d_ops, g128x64.first, g128x64.second); }, true, {}});
+    }
+    {
+        auto ring = [&](auto kern, const char* name, int bs, int nt, int nb) {
+            const int bytes = nb * bs * 130 * 8;
+            CK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+            auto w = bs == 64 ? g128x64 : g128x32;
+            V.push_back({name, [=] { hipLaunchKernelGGL(kern, dim3(cus), dim3(nt), bytes, 0, d_ops,
+                                                        w.first, w.second); }, true, {}});
+        };
+        ring(&v_ring<64, 512, 2, 0>, "ring 128x64 t512 nb2", 64, 512, 2);
+        ring(&v_ring<64, 512, 2, 1>, "ring 128x64 t512 nb2 nt", 64, 512, 2);
+        ring(&v_ring<64, 1024, 2, 0>, "ring 128x64 t1024 nb2", 64, 1024, 2);
+        ring(&v_ring<64, 1024, 2, 1>, "ring 128x64 t1024 nb2 nt", 64, 1024, 2);
+        ring(&v_ring<32, 512, 4, 0>, "ring 128x32 t512 nb4", 32, 512, 4);
+        ring(&v_ring<32, 512, 4, 1>, "ring 128x32 t512 nb4 nt", 32, 512, 4);
+        ring(&v_ring<32, 256, 4, 1>, "ring 128x32 t256 nb4 nt", 32, 256, 4);
+        ring(&v_ring<32, 512, 3, 1>, "ring 128x32 t512 nb3 nt", 32, 512, 3);
     }
     const int64_t n2 = int64_t(n) * n / 2;
     for (int g : {2, 4, 8, 32}) {
