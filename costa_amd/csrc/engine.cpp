@@ -13,7 +13,9 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -558,6 +560,14 @@ cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
         }
     }
     g_stats.plan_misses++;
+    // COSTA_PLAN_TRACE=1: where a plan-cache miss spends its host time (stderr)
+    static const bool trace = std::getenv("COSTA_PLAN_TRACE") != nullptr;
+    auto now = [] {
+        return std::chrono::duration<double, std::milli>(
+                   std::chrono::steady_clock::now().time_since_epoch()).count();
+    };
+    const double t0 = now();
+    double t_resid = 0, t_plan = 0, t_work = 0;
 
     auto cp = std::make_unique<cached_plan>();
     cp->device = c->device;
@@ -621,20 +631,25 @@ cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
                 }
             }
         }
-        // Pipelined staging (host_pipe.cpp) when every layout is host-resident, there is no
-        // exchange, no range holds both source and target data (in-place) and no target
-        // range is shared by two jobs (their updates would have to be applied in order).
-        bool pipe_ok = host_staging_mode() == 1 && c->size == 1 && !c->nccl &&
+        // Pipelined staging (host_pipe.cpp) when every layout is host-resident, no range holds
+        // both source and target data (in-place) and no target range is shared by two jobs
+        // (their updates would have to be applied in order).
+        bool pipe_ok = host_staging_mode() == 1 &&
                        std::none_of(on_dev.begin(), on_dev.end(), [](bool d) { return d; });
         for (uint8_t f : range_flags)
             if ((f & 3) == 3 || (f & 4)) pipe_ok = false;
         if (pipe_ok) {
-            cp->staged = false;
-            cp->p = make_plan(jobs, c->rank, c->size, 0);  // host addresses
-            cp->pipe = make_host_pipeline(cp->p->dtype, cp->p->local_ops);
-            g_plans.emplace_front(h.h, std::move(cp));
-            while (g_plans.size() > kMaxPlans) g_plans.pop_back();
-            return g_plans.front().second.get();
+            auto hplan = make_plan(jobs, c->rank, c->size,  // host addresses
+                                   c->size == 1 && c->nccl ? loopback_exchange() : 0);
+            if (host_pipeline_accepts(hplan->dtype, hplan->pack_ops)) {
+                cp->staged = false;
+                cp->p = std::move(hplan);
+                cp->pipe = make_host_pipeline(cp->p->dtype, cp->p->pack_ops, cp->p->local_ops,
+                                              cp->p->unpack_ops);
+                g_plans.emplace_front(h.h, std::move(cp));
+                while (g_plans.size() > kMaxPlans) g_plans.pop_back();
+                return g_plans.front().second.get();
+            }
         }
         cp->stage.reserve(std::max<size_t>(off, 256));
         staged_ranges = ranges;
@@ -651,8 +666,10 @@ cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
             }
         }
     }
+    t_resid = now() - t0;
     cp->p = make_plan(pj, c->rank, c->size, c->size == 1 && c->nccl ? loopback_exchange() : 0);
     const plan& p = *cp->p;
+    t_plan = now() - t0 - t_resid;
     if (cp->staged) {
         // A C-only range needs no upload when the kernels overwrite every byte of it: one job's
         // C blocks only, no op reading C (beta = 0), and the ops' writes (disjoint: each C
@@ -695,6 +712,7 @@ cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
     cp->l_local = build_work(p.dtype, p.local_ops, ord_l, w_l);
     cp->l_pack = build_work(p.dtype, p.pack_ops, ord_p, w_p);
     cp->l_unpack = build_work(p.dtype, p.unpack_ops, ord_u, w_u);
+    t_work = now() - t0 - t_resid - t_plan;
     cp->d_local.upload(ord_l, dc.main);
     cp->w_local.upload(w_l, dc.main);
     cp->d_pack.upload(ord_p, dc.main);
@@ -702,6 +720,12 @@ cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
     cp->d_unpack.upload(ord_u, dc.main);
     cp->w_unpack.upload(w_u, dc.main);
     HIP_CHECK(hipStreamSynchronize(dc.main));  // host vectors above are temporaries
+    if (trace)
+        std::fprintf(stderr,
+                     "[costa plan] %zu local / %zu pack / %zu unpack ops: residency %.2f ms, "
+                     "planning %.2f, work lists %.2f, upload %.2f, total %.2f\n",
+                     p.local_ops.size(), p.pack_ops.size(), p.unpack_ops.size(), t_resid, t_plan,
+                     t_work, now() - t0 - t_resid - t_plan - t_work, now() - t0);
 
     g_plans.emplace_front(h.h, std::move(cp));
     while (g_plans.size() > kMaxPlans) g_plans.pop_back();
@@ -811,6 +835,29 @@ void synchronize(comm* c) {
     dc.resolve();
 }
 
+namespace {
+// The exchange: one RCCL group of ncclSend / ncclRecv, one pair per peer, at the reference's
+// displacements (communication_data.cpp:152-154).  Each peer's package moves as pieces of at
+// most max_message_bytes(): RCCL was measured to lose the second half of a single >1 GiB self
+// send/recv (tools/loopback_probe.py); pieces to one peer match in issue order on both sides.
+void issue_exchange(comm* c, const plan& p, char* sb, char* rb, hipStream_t s) {
+    const size_t E = dtype_size(p.dtype);
+    const size_t piece = max_message_bytes();
+    NCCL_CHECK(ncclGroupStart());
+    for (int r = 0; r < c->size; ++r) {
+        const size_t sbytes = size_t(p.send_counts[size_t(r)]) * E;
+        const size_t rbytes = size_t(p.recv_counts[size_t(r)]) * E;
+        for (size_t o = 0; o < sbytes; o += piece)
+            NCCL_CHECK(ncclSend(sb + size_t(p.send_displs[size_t(r)]) * E + o,
+                                std::min(piece, sbytes - o), ncclUint8, r, c->nccl, s));
+        for (size_t o = 0; o < rbytes; o += piece)
+            NCCL_CHECK(ncclRecv(rb + size_t(p.recv_displs[size_t(r)]) * E + o,
+                                std::min(piece, rbytes - o), ncclUint8, r, c->nccl, s));
+    }
+    NCCL_CHECK(ncclGroupEnd());
+}
+}  // namespace
+
 void transform(const std::vector<job>& jobs, comm* c, void* user_stream, bool async) {
     std::lock_guard<std::recursive_mutex> lk(g_mutex);
     if (!c) throw error(COSTA_ERR_ARG, "costa: null communicator");
@@ -830,8 +877,21 @@ void transform(const std::vector<job>& jobs, comm* c, void* user_stream, bool as
         HIP_CHECK(hipStreamWaitEvent(dc.main, dc.ev_user, 0));
     }
     upload_scalars(cp, jobs, dc.main);
-    if (cp.pipe) {  // host-resident, single rank: pipelined H2D -> kernels -> D2H
-        run_host_pipeline(*cp.pipe, c->device, dc.main, cp.d_scal.p);
+    if (cp.pipe) {  // host-resident: pipelined gather -> H2D -> [exchange] -> kernels -> D2H
+        const bool xchg = c->nccl != nullptr && (p.send_elems > 0 || p.recv_elems > 0);
+        char *sb = nullptr, *rb = nullptr;
+        std::function<void(void*)> fn;
+        if (xchg) {
+            dc.send.reserve(size_t(p.send_elems) * E + 256);
+            dc.recv.reserve(size_t(p.recv_elems) * E + 256);
+            sb = static_cast<char*>(dc.send.p);
+            rb = static_cast<char*>(dc.recv.p);
+            fn = [&](void* s) { issue_exchange(c, p, sb, rb, static_cast<hipStream_t>(s)); };
+        }
+        // tile kernels on the aux stream, behind the scalars uploaded on main; the exchange on main
+        HIP_CHECK(hipEventRecord(dc.ev_ready, dc.main));
+        HIP_CHECK(hipStreamWaitEvent(dc.aux, dc.ev_ready, 0));
+        run_host_pipeline(*cp.pipe, c->device, dc.aux, dc.main, sb, rb, fn, cp.d_scal.p);
         g_stats.transforms++;
         return;
     }
@@ -878,22 +938,7 @@ void transform(const std::vector<job>& jobs, comm* c, void* user_stream, bool as
             tm.stop();
         }
         tm.start(PH_EXCHANGE, dc.main);
-        NCCL_CHECK(ncclGroupStart());
-        // each peer's package moves as pieces of at most max_message_bytes(): RCCL was measured
-        // to lose the second half of a single >1 GiB self send/recv (tools/loopback_probe.py);
-        // pieces to one peer match in issue order on both sides
-        const size_t piece = max_message_bytes();
-        for (int r = 0; r < c->size; ++r) {
-            const size_t sbytes = size_t(p.send_counts[size_t(r)]) * E;
-            const size_t rbytes = size_t(p.recv_counts[size_t(r)]) * E;
-            for (size_t o = 0; o < sbytes; o += piece)
-                NCCL_CHECK(ncclSend(sb + size_t(p.send_displs[size_t(r)]) * E + o,
-                                    std::min(piece, sbytes - o), ncclUint8, r, c->nccl, dc.main));
-            for (size_t o = 0; o < rbytes; o += piece)
-                NCCL_CHECK(ncclRecv(rb + size_t(p.recv_displs[size_t(r)]) * E + o,
-                                    std::min(piece, rbytes - o), ncclUint8, r, c->nccl, dc.main));
-        }
-        NCCL_CHECK(ncclGroupEnd());
+        issue_exchange(c, p, sb, rb, dc.main);
         tm.stop();
         if (cp.l_unpack.n_items()) {
             tm.start(PH_UNPACK, dc.main);

@@ -6,6 +6,7 @@
 
 #include <array>
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <string>
 #include <vector>
@@ -165,14 +166,23 @@ launch_args make_launch(const work_split& w, const void* d_ordered, const void* 
                         bool axpby);
 
 // ---- host-resident pipeline (host_pipe.cpp) ----
-// Single-rank transforms whose layouts all live in host memory: the local ops in groups of
-// dense packages moving through a pinned/device slot ring (H2D, kernels and D2H overlap).
+// Transforms whose layouts all live in host memory: pack, local and unpack ops in groups of
+// dense packages moving through a pinned/device slot ring (H2D, kernels, the exchange and D2H
+// overlap).
 struct host_pipeline;
+// false when a pack op's column exceeds a pipeline slot (the mirror scheme is used then)
+bool host_pipeline_accepts(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& pack_ops);
 std::shared_ptr<host_pipeline> make_host_pipeline(costa_dtype_t dtype,
-                                                  const std::vector<costa_tile_op_t>& ops);
+                                                  const std::vector<costa_tile_op_t>& pack_ops,
+                                                  const std::vector<costa_tile_op_t>& local_ops,
+                                                  const std::vector<costa_tile_op_t>& unpack_ops);
 size_t host_pipeline_groups(const host_pipeline& hp);
-// blocking: returns when every target byte is back in host memory
-void run_host_pipeline(host_pipeline& hp, int device, void* main_stream, const void* d_scalars);
+// Blocking: returns when every target byte is back in host memory.  Tile kernels run on
+// `compute_stream`; `exchange` (empty without one) is called once, with `exchange_stream`, when
+// the send package is in `send_buf`; the unpack kernels read `recv_buf` after it.
+void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void* exchange_stream,
+                       char* send_buf, char* recv_buf, const std::function<void(void*)>& exchange,
+                       const void* d_scalars);
 void release_host_rings();
 // host staging of host-resident layouts: 0 = mirror (every spanned range up, kernels, target
 // ranges down), 1 = pipelined (default; falls back to the mirror where it does not apply)

@@ -3,14 +3,14 @@
 // The reference's path starts and ends in host memory (each rank's local matrix buffer).  The
 // mirror scheme of engine.cpp uploads every byte range a layout spans, runs the kernels, and
 // copies the target ranges back: one direction at a time, so a call costs H2D + D2H.  Here the
-// local tile ops are cut into groups of at most kSlot bytes of source and target data, and each
-// group moves through a ring of slots:
+// tile ops are cut into groups of at most kSlot bytes of source and target data, and each group
+// moves through a ring of slots:
 //
 //   host threads : gather the group's source tiles (and, for beta != 0, its old target tiles)
 //                  densely into a pinned slot                         [the reference's PACK
 //                  format, communication_data.cpp:191-217: stored shape, dense]
 //   copy stream 1: pinned slot -> device slot (H2D)
-//   main stream  : the tile kernels, rewritten to read the dense source package and write a
+//   compute      : the tile kernels, rewritten to read the dense source package and write a
 //                  dense target package (copy_and_transform of every tile, on the GPU)
 //   copy stream 2: device target package -> pinned slot (D2H)
 //   host threads : scatter the target package into the caller's C
@@ -21,6 +21,14 @@
 // profiles/r07/pcie_probe.log).  Device memory needed: the ring, not a mirror of A and C.
 // Only C bytes the ops write are ever stored to the caller's memory.  The host threads move
 // bytes only (strided memcpy); every element's transform runs in the tile kernels.
+//
+// With an exchange (several ranks, the ScaLAPACK situation) the groups come in three kinds, in
+// this order (the reference's exchange_async, transform.cpp:46-128):
+//   PACK   the host gather IS the pack (a bit copy into the dense package): it goes straight
+//          into the device send buffer; after the last pack group the RCCL group starts
+//   LOCAL  as above, on the compute stream, overlapping the exchange
+//   UNPACK the unpack kernels read the receive buffer once the exchange is done and write dense
+//          target packages, copied back and scattered like LOCAL ones
 #include <emmintrin.h>
 #include <hip/hip_runtime.h>
 
@@ -53,7 +61,7 @@ namespace {
 // source (and target) bytes per group; COSTA_HOST_SLOT_MIB overrides (tuning)
 const size_t kSlot = [] {
     const char* s = std::getenv("COSTA_HOST_SLOT_MIB");
-    const long v = s ? std::atol(s) : 32;
+    const long v = s ? std::atol(s) : 64;
     return size_t(std::max(1L, std::min(1024L, v))) << 20;
 }();
 constexpr int kRing = 4;                      // slots in flight
@@ -175,6 +183,7 @@ struct ring {
     char* pin_out = nullptr;  // kRing x kSlot: target package
     char* dev = nullptr;      // kRing x 2*kSlot: [source package | target package]
     hipEvent_t up_done[kRing]{}, kern_done[kRing]{}, down_done[kRing]{};
+    hipEvent_t packed = nullptr, exchanged = nullptr;  // send buffer uploaded / exchange done
     explicit ring(int d) : device(d) {
         HP_CHECK(hipStreamCreateWithFlags(&up, hipStreamNonBlocking));
         HP_CHECK(hipStreamCreateWithFlags(&down, hipStreamNonBlocking));
@@ -184,6 +193,8 @@ struct ring {
         for (int k = 0; k < kRing; ++k)
             for (hipEvent_t* e : {&up_done[k], &kern_done[k], &down_done[k]})
                 HP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+        HP_CHECK(hipEventCreateWithFlags(&packed, hipEventDisableTiming));
+        HP_CHECK(hipEventCreateWithFlags(&exchanged, hipEventDisableTiming));
     }
     ~ring() {
         (void)hipSetDevice(device);
@@ -191,6 +202,8 @@ struct ring {
         (void)hipStreamSynchronize(down);
         for (int k = 0; k < kRing; ++k)
             for (hipEvent_t e : {up_done[k], kern_done[k], down_done[k]}) (void)hipEventDestroy(e);
+        (void)hipEventDestroy(packed);
+        (void)hipEventDestroy(exchanged);
         (void)hipFree(dev);
         (void)hipHostFree(pin_in);
         (void)hipHostFree(pin_out);
@@ -217,6 +230,7 @@ void release_host_rings() { rings().clear(); }
 
 // ---------------------------------------------------------------- the pipeline of one plan
 struct host_pipeline {
+    enum kind_t { PACK, LOCAL, UNPACK };
     struct hop {          // one op (or piece of one) with its host addresses
         costa_tile_op_t op;
         uint64_t in_off, out_off;  // offsets in the group's source / target packages
@@ -226,8 +240,10 @@ struct host_pipeline {
         int32_t lo, hi;
     };
     struct group {
+        kind_t kind = LOCAL;
         size_t first = 0, count = 0;  // hops
         size_t in_bytes = 0, out_bytes = 0;
+        uint64_t send_off = 0;        // PACK: the group's byte range starts here in the send buffer
         bool reads_old = false;
         std::vector<item> gather, scatter;  // scatter items double as old-target gathers
         work_split split;
@@ -238,7 +254,8 @@ struct host_pipeline {
     costa_dtype_t dtype = COSTA_DOUBLE;
     size_t E = 8;
     std::vector<hop> hops;
-    std::vector<group> groups;
+    std::vector<group> groups;  // PACK groups, then LOCAL, then UNPACK
+    size_t n_pack_groups = 0;
     void* d_ops = nullptr;   // every group's ordered device ops (package offsets)
     void* d_work = nullptr;
     ~host_pipeline() {
@@ -263,61 +280,107 @@ void add_items(std::vector<host_pipeline::item>& v, uint32_t k, int64_t run_byte
         v.push_back({k, int32_t(lo), int32_t(std::min(runs, lo + per))});
 }
 
+// cut an op into pieces of at most one slot (a sub-rectangle of a tile op is a tile op); pack
+// ops are cut into whole columns only, so that every piece stays one contiguous range of the
+// dense send package
+void cut(const costa_tile_op_t& op, size_t E, bool whole_columns, std::vector<costa_tile_op_t>& out) {
+    if (op.nf <= 0 || op.ns <= 0) return;
+    if (align_up(size_t(op.nf) * size_t(op.ns) * E) <= kSlot) {
+        out.push_back(op);
+        return;
+    }
+    const int64_t cap = int64_t((kSlot - kAlign) / E);  // elements per piece
+    const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
+    const int64_t cf = std::min<int64_t>(op.nf, cap);
+    if (whole_columns && cf < op.nf) throw error(COSTA_ERR_INTERNAL, "costa: pack column over a slot");
+    const int64_t cs = std::max<int64_t>(1, cap / cf);
+    for (int64_t f0 = 0; f0 < op.nf; f0 += cf)
+        for (int64_t s0 = 0; s0 < op.ns; s0 += cs) {
+            costa_tile_op_t p = op;
+            p.nf = int32_t(std::min<int64_t>(cf, op.nf - f0));
+            p.ns = int32_t(std::min<int64_t>(cs, op.ns - s0));
+            p.src = op.src + uint64_t((s0 * op.lds + f0) * int64_t(E));
+            p.dst = op.dst + uint64_t((tr ? f0 * op.ldd + s0 : s0 * op.ldd + f0) * int64_t(E));
+            out.push_back(p);
+        }
+}
+
 }  // namespace
 
+bool host_pipeline_accepts(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& pack_ops) {
+    const size_t E = dtype_size(dtype);
+    for (const auto& op : pack_ops)
+        if (size_t(op.nf) * E > kSlot - kAlign) return false;
+    return true;
+}
+
 std::shared_ptr<host_pipeline> make_host_pipeline(costa_dtype_t dtype,
-                                                  const std::vector<costa_tile_op_t>& ops) {
-    auto hp = std::make_shared<host_pipeline>();
+                                                  const std::vector<costa_tile_op_t>& pack_ops,
+                                                  const std::vector<costa_tile_op_t>& local_ops,
+                                                  const std::vector<costa_tile_op_t>& unpack_ops) {
+    using hpl = host_pipeline;
+    auto hp = std::make_shared<hpl>();
     hp->dtype = dtype;
     const size_t E = dtype_size(dtype);
     hp->E = E;
-    const int64_t cap = int64_t(kSlot / E);  // elements per piece
-    // cut ops over a slot into pieces (a sub-rectangle of a tile op is a tile op)
-    std::vector<costa_tile_op_t> pieces;
-    pieces.reserve(ops.size());
-    for (const auto& op : ops) {
-        if (op.nf <= 0 || op.ns <= 0) continue;
-        if (align_up(size_t(op.nf) * size_t(op.ns) * E) <= kSlot) {
-            pieces.push_back(op);
-            continue;
-        }
-        const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
-        const int64_t cf = std::min<int64_t>(op.nf, cap - int64_t(kAlign / E));
-        const int64_t cs = std::max<int64_t>(1, (cap - int64_t(kAlign / E)) / cf);
-        for (int64_t f0 = 0; f0 < op.nf; f0 += cf)
-            for (int64_t s0 = 0; s0 < op.ns; s0 += cs) {
-                costa_tile_op_t p = op;
-                p.nf = int32_t(std::min<int64_t>(cf, op.nf - f0));
-                p.ns = int32_t(std::min<int64_t>(cs, op.ns - s0));
-                p.src = op.src + uint64_t((s0 * op.lds + f0) * int64_t(E));
-                p.dst = op.dst + uint64_t((tr ? f0 * op.ldd + s0 : s0 * op.ldd + f0) * int64_t(E));
-                pieces.push_back(p);
-            }
-    }
-    // groups in list order (the planner's target-key order: for block-cyclic layouts a group
-    // is a band of target rows, read from a band of source columns)
-    host_pipeline::group g;
+
+    // groups in list order (the planner's key order: for block-cyclic layouts a local group is
+    // a band of target rows read from a band of source columns; pack groups are consecutive
+    // ranges of the send package)
+    hpl::group g;
     auto close = [&] {
+        const hpl::kind_t k = g.kind;
         if (g.count) hp->groups.push_back(std::move(g));
-        g = host_pipeline::group{};
+        g = hpl::group{};
+        g.kind = k;
         g.first = hp->hops.size();
     };
-    g.first = 0;
-    for (const auto& p : pieces) {
-        const size_t bytes = align_up(size_t(p.nf) * size_t(p.ns) * E);
-        if (g.in_bytes + bytes > kSlot || g.out_bytes + bytes > kSlot) close();
-        hp->hops.push_back({p, g.in_bytes, g.out_bytes});
-        g.in_bytes += bytes;
-        g.out_bytes += bytes;
-        ++g.count;
+    for (int kind = hpl::PACK; kind <= hpl::UNPACK; ++kind) {
+        const auto& ops = kind == hpl::PACK ? pack_ops : kind == hpl::LOCAL ? local_ops : unpack_ops;
+        std::vector<costa_tile_op_t> pieces;
+        pieces.reserve(ops.size());
+        for (const auto& op : ops) cut(op, E, kind == hpl::PACK, pieces);
+        close();
+        g.kind = hpl::kind_t(kind);
+        for (const auto& p : pieces) {
+            const size_t bytes = size_t(p.nf) * size_t(p.ns) * E;
+            if (kind == hpl::PACK) {  // dense and contiguous in package order
+                if (g.count && g.in_bytes + bytes > kSlot) close();
+                if (!g.count) g.send_off = p.dst;
+                if (p.dst != g.send_off + g.in_bytes)
+                    throw error(COSTA_ERR_INTERNAL, "costa: pack package not contiguous");
+                hp->hops.push_back({p, p.dst - g.send_off, 0});
+                g.in_bytes += bytes;
+            } else {
+                const size_t ab = align_up(bytes);
+                const size_t in = kind == hpl::LOCAL ? ab : 0;
+                if (g.count && (g.in_bytes + in > kSlot || g.out_bytes + ab > kSlot)) close();
+                hp->hops.push_back({p, g.in_bytes, g.out_bytes});
+                g.in_bytes += in;
+                g.out_bytes += ab;
+            }
+            ++g.count;
+        }
+        close();
+        if (kind == hpl::PACK) hp->n_pack_groups = hp->groups.size();
     }
-    close();
 
-    // device op lists: every op reads the dense source package (lds = nf) and writes the
-    // dense target package (ldd = contiguous run of the target); bases are added at launch
+    // device op lists (LOCAL / UNPACK): every op writes the dense target package (ldd = the
+    // contiguous run of the target); LOCAL ops read the dense source package (lds = nf),
+    // UNPACK ops keep their receive-buffer offsets.  Bases are added at launch.
     std::vector<costa_tile_op_t> all_ord;
     std::vector<uint64_t> all_work;
     for (auto& gr : hp->groups) {
+        for (size_t i = gr.first; i < gr.first + gr.count; ++i) {
+            const uint32_t k = uint32_t(i);
+            const auto& h = hp->hops[i];
+            if (gr.kind != hpl::UNPACK) add_items(gr.gather, k, int64_t(h.op.nf) * int64_t(E), h.op.ns);
+            if (gr.kind == hpl::PACK) continue;
+            int64_t run, runs;
+            target_shape(h.op, run, runs);
+            add_items(gr.scatter, k, run * int64_t(E), runs);
+        }
+        if (gr.kind == hpl::PACK) continue;
         std::vector<costa_tile_op_t> dev_ops;
         dev_ops.reserve(gr.count);
         for (size_t i = gr.first; i < gr.first + gr.count; ++i) {
@@ -325,21 +388,20 @@ std::shared_ptr<host_pipeline> make_host_pipeline(costa_dtype_t dtype,
             costa_tile_op_t d = h.op;
             int64_t run, runs;
             target_shape(d, run, runs);
-            d.src = h.in_off;
-            d.lds = d.nf;
+            if (gr.kind == hpl::LOCAL) {
+                d.src = h.in_off;
+                d.lds = d.nf;
+            }
             d.dst = h.out_off;
             d.ldd = int32_t(run);
             d.flags &= ~uint32_t(COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST);
-            if ((int64_t(d.lds) * int64_t(E)) % 16 == 0) d.flags |= COSTA_TILE_VEC_SRC;
+            if (d.src % 16 == 0 && (int64_t(d.lds) * int64_t(E)) % 16 == 0) d.flags |= COSTA_TILE_VEC_SRC;
             if ((int64_t(d.ldd) * int64_t(E)) % 16 == 0) d.flags |= COSTA_TILE_VEC_DST;
             dev_ops.push_back(d);
             const uint32_t kind = (d.flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT;
             if (kind == COSTA_SCALE_AXPBY) gr.reads_old = true;
             const int64_t n = int64_t(d.nf) * d.ns;
             gr.alg_bytes += int64_t(E) * n * (1 + (kind != COSTA_SCALE_ZERO) + (kind == COSTA_SCALE_AXPBY));
-            const uint32_t k = uint32_t(i);
-            add_items(gr.gather, k, int64_t(d.nf) * int64_t(E), d.ns);
-            add_items(gr.scatter, k, run * int64_t(E), runs);
         }
         gr.any_tr = any_transpose(dev_ops);
         std::vector<costa_tile_op_t> ord;
@@ -365,14 +427,19 @@ std::shared_ptr<host_pipeline> make_host_pipeline(costa_dtype_t dtype,
 
 size_t host_pipeline_groups(const host_pipeline& hp) { return hp.groups.size(); }
 
-void run_host_pipeline(host_pipeline& hp, int device, void* main_stream, const void* d_scalars) {
+void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void* exchange_stream,
+                       char* send_buf, char* recv_buf, const std::function<void(void*)>& exchange,
+                       const void* d_scalars) {
+    using hpl = host_pipeline;
     ring& R = ring_of(device);
-    hipStream_t comp = static_cast<hipStream_t>(main_stream);
+    hipStream_t comp = static_cast<hipStream_t>(compute_stream);
+    hipStream_t xs = static_cast<hipStream_t>(exchange_stream);
     pool& P = thread_pool();
     const size_t E = hp.E;
     const size_t G = hp.groups.size();
     const bool prof = profiling();
-    // timing brackets (profiling only): per group kernel, and the spans of both copy streams
+    // timing brackets (profiling only): per group kernel, the exchange, and the spans of both
+    // copy streams
     std::vector<hipEvent_t> evs;
     auto ev = [&](hipStream_t s) {
         hipEvent_t e;
@@ -381,18 +448,35 @@ void run_host_pipeline(host_pipeline& hp, int device, void* main_stream, const v
         HP_CHECK(hipEventRecord(e, s));
         return e;
     };
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> kern_t;
-    hipEvent_t up0 = nullptr, up1 = nullptr, dn0 = nullptr, dn1 = nullptr;
+    struct kbracket {
+        hipEvent_t a, b;
+        bool unpack;
+    };
+    std::vector<kbracket> kern_t;
+    hipEvent_t up0 = nullptr, up1 = nullptr, dn0 = nullptr, dn1 = nullptr, x0 = nullptr, x1 = nullptr;
     // every slot starts free: the ring's events are recorded on idle streams
     for (int k = 0; k < kRing; ++k) {
         HP_CHECK(hipEventRecord(R.up_done[k], R.up));
         HP_CHECK(hipEventRecord(R.down_done[k], R.down));
     }
+    // the exchange starts once the whole send package is in HBM (after the last pack group's
+    // upload, or at once when there is nothing to send); LOCAL groups overlap it
+    bool exchanged = false;
+    auto issue_exchange = [&] {
+        if (!exchange || exchanged) return;
+        HP_CHECK(hipEventRecord(R.packed, R.up));
+        HP_CHECK(hipStreamWaitEvent(xs, R.packed, 0));
+        if (prof) x0 = ev(xs);
+        exchange(xs);
+        if (prof) x1 = ev(xs);
+        HP_CHECK(hipEventRecord(R.exchanged, xs));
+        exchanged = true;
+    };
+    if (hp.n_pack_groups == 0) issue_exchange();
 
     // Host copy work of one step: the source gather of group t (plus its old target values
     // when an op reads C) and the target scatter of group t - kLag, in one parallel pass.
-    auto host_step = [&](const host_pipeline::group* g, char* pin, const host_pipeline::group* o,
-                         const char* pout) {
+    auto host_step = [&](const hpl::group* g, char* pin, const hpl::group* o, const char* pout) {
         const size_t ng = g ? g->gather.size() : 0;
         const size_t nold = g && g->reads_old ? g->scatter.size() : 0;
         const size_t ns = o ? o->scatter.size() : 0;
@@ -441,8 +525,9 @@ void run_host_pipeline(host_pipeline& hp, int device, void* main_stream, const v
     const double t_begin = now();
     for (size_t t = 0; t < G + kLag; ++t) {
         const int k = int(t % kRing);
-        const host_pipeline::group* g = t < G ? &hp.groups[t] : nullptr;
-        const host_pipeline::group* o = t >= size_t(kLag) ? &hp.groups[t - kLag] : nullptr;
+        const hpl::group* g = t < G ? &hp.groups[t] : nullptr;
+        const hpl::group* o = t >= size_t(kLag) ? &hp.groups[t - kLag] : nullptr;
+        if (o && o->kind == hpl::PACK) o = nullptr;  // nothing comes back from a pack group
         const int ko = int((t + kRing - kLag) % kRing);  // slot of group t - kLag
         char* pin = R.pin_in + size_t(k) * 2 * kSlot;
         char* dev = R.dev + size_t(k) * 2 * kSlot;
@@ -459,22 +544,40 @@ void run_host_pipeline(host_pipeline& hp, int device, void* main_stream, const v
         t_wait_down += t2 - t1;
         t_copy += t3 - t2;
         if (!g) continue;
+        if (g->kind == hpl::PACK) {  // the host gather is the pack: upload into the send buffer
+            if (prof && !up0) up0 = ev(R.up);
+            HP_CHECK(hipMemcpyAsync(send_buf + g->send_off, pin, g->in_bytes, hipMemcpyHostToDevice,
+                                    R.up));
+            HP_CHECK(hipEventRecord(R.up_done[k], R.up));
+            if (prof) up1 = ev(R.up);
+            if (t + 1 == hp.n_pack_groups) issue_exchange();
+            t_issue += now() - t3;
+            continue;
+        }
+        const bool unpack = g->kind == hpl::UNPACK;
+        if (unpack && !exchanged)
+            throw error(COSTA_ERR_INTERNAL, "costa: unpack group without an exchange");
         // the device slot is free once its previous target package has been copied out
         HP_CHECK(hipStreamWaitEvent(R.up, R.down_done[k], 0));
-        if (prof && !up0) up0 = ev(R.up);
-        HP_CHECK(hipMemcpyAsync(dev, pin, g->in_bytes, hipMemcpyHostToDevice, R.up));
-        if (g->reads_old)
-            HP_CHECK(hipMemcpyAsync(dev + kSlot, pin + kSlot, g->out_bytes, hipMemcpyHostToDevice, R.up));
+        if (g->in_bytes || g->reads_old) {
+            if (prof && !up0) up0 = ev(R.up);
+            if (g->in_bytes) HP_CHECK(hipMemcpyAsync(dev, pin, g->in_bytes, hipMemcpyHostToDevice, R.up));
+            if (g->reads_old)
+                HP_CHECK(hipMemcpyAsync(dev + kSlot, pin + kSlot, g->out_bytes, hipMemcpyHostToDevice,
+                                        R.up));
+            if (prof) up1 = ev(R.up);
+        }
         HP_CHECK(hipEventRecord(R.up_done[k], R.up));
-        if (prof && t + 1 == G) up1 = ev(R.up);
         HP_CHECK(hipStreamWaitEvent(comp, R.up_done[k], 0));
+        if (unpack) HP_CHECK(hipStreamWaitEvent(comp, R.exchanged, 0));
         hipEvent_t k0 = prof ? ev(comp) : nullptr;
         launch_tiles(hp.dtype,
                      make_launch(g->split, static_cast<const costa_tile_op_t*>(hp.d_ops) + g->ord_first,
-                                 static_cast<const uint64_t*>(hp.d_work) + g->work_first, dev,
-                                 dev + kSlot, d_scalars, g->any_tr, g->reads_old),
+                                 static_cast<const uint64_t*>(hp.d_work) + g->work_first,
+                                 unpack ? recv_buf : dev, dev + kSlot, d_scalars, g->any_tr,
+                                 g->reads_old),
                      comp);
-        if (prof) kern_t.push_back({k0, ev(comp)});
+        if (prof) kern_t.push_back({k0, ev(comp), unpack});
         HP_CHECK(hipEventRecord(R.kern_done[k], comp));
         // the pinned target slot's previous group (t - kRing) was scattered at step
         // t - kRing + kLag < t
@@ -483,31 +586,41 @@ void run_host_pipeline(host_pipeline& hp, int device, void* main_stream, const v
         HP_CHECK(hipMemcpyAsync(R.pin_out + size_t(k) * kSlot, dev + kSlot, g->out_bytes,
                                 hipMemcpyDeviceToHost, R.down));
         HP_CHECK(hipEventRecord(R.down_done[k], R.down));
-        if (prof && t + 1 == G) dn1 = ev(R.down);
+        if (prof) dn1 = ev(R.down);
         t_issue += now() - t3;
     }
+    issue_exchange();  // a rank with nothing to upload still takes part in the exchange
     if (trace)
         std::fprintf(stderr,
-                     "[costa host pipe] groups %zu slot %zu MiB threads %d: total %.2f ms, "
-                     "copies %.2f, wait-up %.2f, wait-down %.2f, issue %.2f\n",
-                     G, kSlot >> 20, host_threads(), (now() - t_begin) * 1e3, t_copy * 1e3,
-                     t_wait_up * 1e3, t_wait_down * 1e3, t_issue * 1e3);
+                     "[costa host pipe] groups %zu (%zu pack) slot %zu MiB threads %d: total %.2f "
+                     "ms, copies %.2f, wait-up %.2f, wait-down %.2f, issue %.2f\n",
+                     G, hp.n_pack_groups, kSlot >> 20, host_threads(), (now() - t_begin) * 1e3,
+                     t_copy * 1e3, t_wait_up * 1e3, t_wait_down * 1e3, t_issue * 1e3);
     HP_CHECK(hipStreamSynchronize(R.up));
+    HP_CHECK(hipStreamSynchronize(xs));
     HP_CHECK(hipStreamSynchronize(comp));
     HP_CHECK(hipStreamSynchronize(R.down));
 
     auto& st = stats();
-    for (const auto& g : hp.groups) st.local_bytes += g.alg_bytes;
-    st.local_launches += int64_t(G);
+    for (const auto& gr : hp.groups) {
+        if (gr.kind == hpl::LOCAL) {
+            st.local_bytes += gr.alg_bytes;
+            st.local_launches++;
+        } else if (gr.kind == hpl::UNPACK) {
+            st.unpack_bytes += gr.alg_bytes;
+            st.unpack_launches++;
+        }
+    }
     st.host_groups += int64_t(G);
     if (prof) {
         float ms = 0.f;
-        for (auto& kt : kern_t) {
-            HP_CHECK(hipEventElapsedTime(&ms, kt.first, kt.second));
-            st.local_ms += ms;
+        for (auto& x : kern_t) {
+            HP_CHECK(hipEventElapsedTime(&ms, x.a, x.b));
+            (x.unpack ? st.unpack_ms : st.local_ms) += ms;
         }
         if (up0 && up1 && hipEventElapsedTime(&ms, up0, up1) == hipSuccess) st.h2d_ms += ms;
         if (dn0 && dn1 && hipEventElapsedTime(&ms, dn0, dn1) == hipSuccess) st.d2h_ms += ms;
+        if (x0 && x1 && hipEventElapsedTime(&ms, x0, x1) == hipSuccess) st.exchange_ms += ms;
     }
     for (hipEvent_t e : evs) (void)hipEventDestroy(e);
 }

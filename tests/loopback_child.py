@@ -1,7 +1,9 @@
 """Child process of test_gpu_loopback.py (run with COSTA_LOOPBACK=1 or 2): every single-rank
 golden case and a 12288^2 fp64 'T' case go through PACK -> ncclSend/ncclRecv to self -> UNPACK
 (mode 2: half of the tiles, the rest through the concurrent LOCAL launch), then a loop of
-stream-ordered async transforms with A updated on torch's stream between them.
+stream-ordered async transforms with A updated on torch's stream between them, then the golden
+cases and a 3000 x 2500 'T' alpha/beta case from host memory through both host staging schemes
+(pipelined: pack groups gathered into the send buffer, unpack groups scattered back).
 Prints one line per failure and a final 'OK <cases> <pack> <unpack> <local launches>'."""
 import os
 import sys
@@ -62,6 +64,45 @@ def main():
     torch.cuda.synchronize()
     if not torch.equal(Cm.view(m, m), A.view(m, m).t()):
         bad.append(f"{m}^2 fp64 T async")
+    # host-resident layouts (the ScaLAPACK situation): the pipelined staging gathers the pack
+    # groups into the send buffer, exchanges with itself over RCCL and brings the unpack groups
+    # back to host memory; the mirror scheme (mode 0) as a cross-check
+    host_groups = 0
+    for hmode in (1, 0):
+        costa.set_host_staging(hmode)
+        g0 = costa.get_stats()["host_groups"]
+        for case in all_cases():
+            if case.P != 1:
+                continue
+            bufs = [case.inputs(k, 0) for k in range(len(case.pairs))]
+            As = [p.A.make_layout(0, bufs[k][0].ctypes.data, 1, case.dtype)
+                  for k, p in enumerate(case.pairs)]
+            Cs = [p.C.make_layout(0, bufs[k][1].ctypes.data, 1, case.dtype)
+                  for k, p in enumerate(case.pairs)]
+            eff = [case.effective(k) for k in range(len(case.pairs))]
+            costa.transform_batch(As, Cs, comm, [e[0] for e in eff], [e[1] for e in eff],
+                                  [e[2] for e in eff])
+            fx = load(case.name)
+            for k in range(len(case.pairs)):
+                if not matches(fx, f"C{k}_r0", bufs[k][1]):
+                    bad.append(f"host mode {hmode} {case.name} C{k}")
+        hm, hn = 3000, 2500  # many groups, ops cut over a slot when COSTA_HOST_SLOT_MIB is small
+        rng = np.random.default_rng(3)
+        ha = rng.standard_normal(hm * hn)
+        c0 = rng.standard_normal(hn * hm)
+        hc = c0.copy()
+        HA = costa.block_cyclic_layout(hm, hn, 512, 384, 1, 1, hm, hn, 1, 1, "R", 0, 0, ha, hm, "C", 0)
+        HC = costa.block_cyclic_layout(hn, hm, 384, 512, 1, 1, hn, hm, 1, 1, "R", 0, 0, hc, hn, "C", 0)
+        costa.transform(HA, HC, comm, "T", -0.75, 1.5)
+        exp = 1.5 * c0 + -0.75 * ha.reshape(hn, hm).T.copy().reshape(-1)
+        if not np.array_equal(hc.view(np.uint64), exp.view(np.uint64)):
+            bad.append(f"host mode {hmode} {hm}x{hn} T axpby")
+        groups = costa.get_stats()["host_groups"] - g0
+        if (groups > 0) != (hmode == 1):
+            bad.append(f"host mode {hmode}: {groups} pipeline groups")
+        host_groups += groups
+    costa.set_host_staging(1)
+    print("HOST", host_groups)
     st = costa.get_stats()
     for b in bad:
         print("FAIL", b)

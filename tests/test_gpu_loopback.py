@@ -14,16 +14,22 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("mode", ["1", "2"])
-def test_loopback_exchange_matches_golden(mode):
+@pytest.mark.parametrize("mode,slot", [("1", None), ("2", None), ("2", "1")])
+def test_loopback_exchange_matches_golden(mode, slot):
+    """slot "1": 1 MiB host pipeline slots (many groups, ops cut into pieces)"""
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "loopback_child.py")
-    r = subprocess.run([sys.executable, child], env=dict(os.environ, COSTA_LOOPBACK=mode),
-                       capture_output=True, text=True, timeout=600)
+    env = dict(os.environ, COSTA_LOOPBACK=mode)
+    if slot:
+        env["COSTA_HOST_SLOT_MIB"] = slot
+    r = subprocess.run([sys.executable, child], env=env, capture_output=True, text=True,
+                       timeout=600)
     out = r.stdout.strip().splitlines()
     assert r.returncode == 0 and out and out[-1].startswith("OK"), r.stdout + r.stderr
+    host = [l for l in out if l.startswith("HOST")]
+    assert host and int(host[-1].split()[1]) > 0, "pipelined host staging did not run"
     _, n, packs, unpacks, locals_ = out[-1].split()
     assert int(packs) >= int(n) and int(unpacks) >= int(n), out[-1]  # every case exchanged
     if mode == "1":
