@@ -401,7 +401,7 @@ def main():
         e2e = dict(res[1])
         e2e["mirror"] = res[0]
         e2e["note"] = ("pageable host A and C (numpy), 2 x 2 GiB over PCIe. Pipelined (default): "
-                       "32 MiB tile groups, host gather -> H2D -> tile kernels -> D2H -> host "
+                       "64 MiB tile groups, host gather -> H2D -> tile kernels -> D2H -> host "
                        "scatter, both copy directions at once (h2d_ms/d2h_ms = span of each "
                        "copy stream). mirror: H2D of A's range, kernel, D2H of C's range "
                        "(C not uploaded: beta=0 and every byte of it is overwritten)")

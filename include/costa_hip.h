@@ -214,10 +214,12 @@ int costa_hip_release_caches(void);
 /* ---- host-resident layouts ----
  * How a transform whose layouts live in host memory reaches HBM (the reference's path starts
  * and ends in each rank's host buffers).  1 (default; env COSTA_HOST_STAGING): pipelined --
- * single-rank calls move the local tiles in 32 MiB groups through pinned/device slot rings,
- * host gather -> H2D -> tile kernels -> D2H -> host scatter, both copy directions at once;
- * other calls fall back to 0.  0: mirror -- every byte range the layouts span is uploaded, the
- * kernels run on the mirror, the target ranges are copied back.  Results are identical. */
+ * the tiles move in 64 MiB groups through pinned/device slot rings: host gather -> H2D ->
+ * tile kernels -> D2H -> host scatter, both copy directions at once; with several ranks the
+ * host gather writes the send package, the RCCL exchange follows, and the unpack kernels'
+ * output comes back the same way.  0: mirror -- every byte range the layouts span is uploaded,
+ * the kernels run on the mirror, the target ranges are copied back.  Mode 1 falls back to 0
+ * for in-place layouts and target ranges shared by two batched jobs.  Results are identical. */
 int costa_hip_set_host_staging(int mode);
 
 #ifdef __cplusplus

@@ -35,7 +35,8 @@ def child():
         costa.transform(A, C, comm, "T", 1.0, 0.0)
         ts.append(time.perf_counter() - t0)
     t = min(ts)
-    print(json.dumps({"mode": mode, "slot_mib": os.environ.get("COSTA_HOST_SLOT_MIB", "64"),
+    print(json.dumps({"mode": mode, "loopback": os.environ.get("COSTA_LOOPBACK", "0"),
+                      "slot_mib": os.environ.get("COSTA_HOST_SLOT_MIB", "64"),
                       "threads": os.environ.get("COSTA_HOST_THREADS", "16"),
                       "ms_best": round(t * 1e3, 2), "ms_all": [round(x * 1e3, 2) for x in ts],
                       "GBps_alg": round(2 * ha.nbytes / t / 1e9, 2), "verified": ok}), flush=True)
@@ -43,8 +44,11 @@ def child():
 
 def main():
     settings = [{"PROBE_MODE": "0"}]
-    for slot, th in (("16", "16"), ("32", "16"), ("64", "16"), ("32", "8"), ("64", "8")):
+    for slot, th in (("32", "16"), ("64", "16"), ("128", "16")):
         settings.append({"PROBE_MODE": "1", "COSTA_HOST_SLOT_MIB": slot, "COSTA_HOST_THREADS": th})
+    # the exchange path on one GPU: every tile packed, sent to itself over RCCL and unpacked
+    for mode in ("0", "1"):
+        settings.append({"PROBE_MODE": mode, "COSTA_LOOPBACK": "1"})
     for s in settings:
         env = dict(os.environ, COSTA_HOST_PIPE_TRACE="1", **s)
         r = subprocess.run([sys.executable, os.path.abspath(__file__), "child"], env=env,
