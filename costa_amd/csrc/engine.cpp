@@ -86,8 +86,18 @@ struct device_ctx {
         hipEvent_t a, b;
     };
     int device = 0;
-    hipStream_t main = nullptr, aux = nullptr;
+    hipStream_t main = nullptr, aux = nullptr, xch = nullptr;  // xch: the RCCL exchange rounds
     hipEvent_t ev_ready = nullptr, ev_local = nullptr, ev_user = nullptr, ev_done = nullptr;
+    std::vector<hipEvent_t> ev_packed, ev_moved;  // per exchange round
+    void round_events(size_t n) {
+        while (ev_packed.size() < n) {
+            hipEvent_t a, b;
+            HIP_CHECK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
+            HIP_CHECK(hipEventCreateWithFlags(&b, hipEventDisableTiming));
+            ev_packed.push_back(a);
+            ev_moved.push_back(b);
+        }
+    }
     std::vector<hipEvent_t> free_events;  // timing events ready for reuse
     std::deque<timed> pending;            // recorded phase brackets not yet read
     dbuf send, recv;
@@ -96,6 +106,7 @@ struct device_ctx {
         // blocking streams: they order after work on the legacy default stream
         HIP_CHECK(hipStreamCreate(&main));
         HIP_CHECK(hipStreamCreate(&aux));
+        HIP_CHECK(hipStreamCreate(&xch));
         for (hipEvent_t* e : {&ev_ready, &ev_local, &ev_user, &ev_done})
             HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
@@ -103,6 +114,9 @@ struct device_ctx {
         (void)hipSetDevice(device);
         (void)hipStreamSynchronize(main);
         (void)hipStreamSynchronize(aux);
+        (void)hipStreamSynchronize(xch);
+        for (auto e : ev_packed) (void)hipEventDestroy(e);
+        for (auto e : ev_moved) (void)hipEventDestroy(e);
         for (auto& t : pending) {
             (void)hipEventDestroy(t.a);
             (void)hipEventDestroy(t.b);
@@ -111,6 +125,7 @@ struct device_ctx {
         for (hipEvent_t e : {ev_ready, ev_local, ev_user, ev_done}) (void)hipEventDestroy(e);
         (void)hipStreamDestroy(main);
         (void)hipStreamDestroy(aux);
+        (void)hipStreamDestroy(xch);
     }
     hipEvent_t take_event();
     void resolve(size_t max_n = size_t(-1));  // read finished brackets into the statistics
@@ -203,6 +218,47 @@ size_t max_message_bytes() {
     }();
     return v;
 }
+
+// Exchange rounds: a peer's package of at least kRoundMinBytes moves in exchange_rounds() equal
+// parts, each its own RCCL group on the exchange stream, so that packing part r+1, moving part
+// r and unpacking part r-1 overlap.  Both sides of a pair derive the parts from the pair's
+// element count alone, so they agree on every message.
+constexpr size_t kRoundMinBytes = size_t(16) << 20;
+int exchange_rounds() {
+    static const int v = [] {
+        const char* s = std::getenv("COSTA_EXCHANGE_ROUNDS");  // tuning / reproduction override
+        const int x = s ? std::atoi(s) : 4;
+        return std::max(1, std::min(16, x));
+    }();
+    return v;
+}
+
+namespace {
+int parts_of(int64_t n, size_t E, int R) { return size_t(n) * E >= kRoundMinBytes ? R : 1; }
+// element range [lo, hi) of round r of a package of n elements (empty past its parts)
+void round_range(int64_t n, size_t E, int R, int r, int64_t& lo, int64_t& hi) {
+    const int parts = parts_of(n, E, R);
+    if (r >= parts) {
+        lo = hi = n;
+        return;
+    }
+    lo = n * r / parts;
+    hi = n * (r + 1) / parts;
+}
+// round holding element o (0 <= o < n) of a package of n elements
+int round_of(int64_t o, int64_t n, size_t E, int R) {
+    const int parts = parts_of(n, E, R);
+    int r = int(o * parts / n);
+    while (r > 0 && o < n * r / parts) --r;
+    while (r + 1 < parts && o >= n * (r + 1) / parts) ++r;
+    return r;
+}
+// the peer whose package holds element o of a buffer laid out by displs / counts
+size_t peer_of(const std::vector<int64_t>& displs, int64_t o) {
+    const auto it = std::upper_bound(displs.begin(), displs.end(), o);
+    return size_t(it - displs.begin()) - 1;
+}
+}  // namespace
 
 int comm_rank(const comm* c) { return c->rank; }
 int comm_size(const comm* c) { return c->size; }
@@ -490,10 +546,16 @@ struct cached_plan {
     std::vector<hrange> h2d_ranges, d2h_ranges;  // uploaded / copied back
     dbuf stage;
     // device copies of the op lists and work lists
-    dbuf d_local, d_pack, d_unpack, w_local, w_pack, w_unpack, d_scal;
-    work_split l_local, l_pack, l_unpack;  // how each work list splits over the kernel shapes
-    bool tr_local = true, tr_unpack = true;          // any op of the list transposes
-    bool ax_local = true, ax_unpack = true;          // any op of the list reads C
+    dbuf d_local, w_local, d_scal;
+    work_split l_local;                     // how the work list splits over the kernel shapes
+    bool tr_local = true, ax_local = true;  // any op of the list transposes / reads C
+    struct xround {  // one exchange round: its pack ops (by their first element) and unpack
+                     // ops (by their last element)
+        dbuf d_pack, w_pack, d_unpack, w_unpack;
+        work_split l_pack, l_unpack;
+        bool tr_unpack = false, ax_unpack = false;
+    };
+    std::vector<std::unique_ptr<xround>> rounds;
     std::vector<unsigned char> scal_host;
     std::shared_ptr<host_pipeline> pipe;  // host-resident single-rank calls (host_pipe.cpp)
 };
@@ -704,21 +766,49 @@ cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
         }
     }
     cp->tr_local = any_transpose(p.local_ops);
-    cp->tr_unpack = any_transpose(p.unpack_ops);
     cp->ax_local = any_axpby(p.local_ops);
-    cp->ax_unpack = any_axpby(p.unpack_ops);
-    std::vector<costa_tile_op_t> ord_l, ord_p, ord_u;
-    std::vector<uint64_t> w_l, w_p, w_u;
+    std::vector<costa_tile_op_t> ord_l;
+    std::vector<uint64_t> w_l;
     cp->l_local = build_work(p.dtype, p.local_ops, ord_l, w_l);
-    cp->l_pack = build_work(p.dtype, p.pack_ops, ord_p, w_p);
-    cp->l_unpack = build_work(p.dtype, p.unpack_ops, ord_u, w_u);
+    // exchange rounds: pack ops go to the round of their first element (every element a round
+    // sends is packed by then), unpack ops to the round of their last (every element they read
+    // has arrived)
+    const int R = c->nccl ? exchange_rounds() : 1;
+    std::vector<std::vector<costa_tile_op_t>> pk(static_cast<size_t>(R)), up(static_cast<size_t>(R));
+    {
+        const size_t E = dtype_size(p.dtype);
+        for (const auto& op : p.pack_ops) {
+            const int64_t o = int64_t(op.dst / E);
+            const size_t q = peer_of(p.send_displs, o);
+            pk[size_t(round_of(o - p.send_displs[q], p.send_counts[q], E, R))].push_back(op);
+        }
+        for (const auto& op : p.unpack_ops) {
+            const int64_t first = int64_t(op.src / E);
+            const int64_t last = first + int64_t(op.nf) * op.ns - 1;
+            const size_t q = peer_of(p.recv_displs, first);
+            up[size_t(round_of(last - p.recv_displs[q], p.recv_counts[q], E, R))].push_back(op);
+        }
+    }
+    std::vector<std::vector<costa_tile_op_t>> ord_p(static_cast<size_t>(R)), ord_u(static_cast<size_t>(R));
+    std::vector<std::vector<uint64_t>> w_p(static_cast<size_t>(R)), w_u(static_cast<size_t>(R));
+    for (int r = 0; r < R; ++r) {
+        auto x = std::make_unique<cached_plan::xround>();
+        x->tr_unpack = any_transpose(up[size_t(r)]);
+        x->ax_unpack = any_axpby(up[size_t(r)]);
+        x->l_pack = build_work(p.dtype, pk[size_t(r)], ord_p[size_t(r)], w_p[size_t(r)]);
+        x->l_unpack = build_work(p.dtype, up[size_t(r)], ord_u[size_t(r)], w_u[size_t(r)]);
+        cp->rounds.push_back(std::move(x));
+    }
     t_work = now() - t0 - t_resid - t_plan;
     cp->d_local.upload(ord_l, dc.main);
     cp->w_local.upload(w_l, dc.main);
-    cp->d_pack.upload(ord_p, dc.main);
-    cp->w_pack.upload(w_p, dc.main);
-    cp->d_unpack.upload(ord_u, dc.main);
-    cp->w_unpack.upload(w_u, dc.main);
+    for (int r = 0; r < R; ++r) {
+        auto& x = *cp->rounds[size_t(r)];
+        x.d_pack.upload(ord_p[size_t(r)], dc.main);
+        x.w_pack.upload(w_p[size_t(r)], dc.main);
+        x.d_unpack.upload(ord_u[size_t(r)], dc.main);
+        x.w_unpack.upload(w_u[size_t(r)], dc.main);
+    }
     HIP_CHECK(hipStreamSynchronize(dc.main));  // host vectors above are temporaries
     if (trace)
         std::fprintf(stderr,
@@ -832,6 +922,7 @@ void synchronize(comm* c) {
     device_ctx& dc = ctx(c->device);
     HIP_CHECK(hipStreamSynchronize(dc.main));
     HIP_CHECK(hipStreamSynchronize(dc.aux));
+    HIP_CHECK(hipStreamSynchronize(dc.xch));
     dc.resolve();
 }
 
@@ -840,19 +931,23 @@ namespace {
 // displacements (communication_data.cpp:152-154).  Each peer's package moves as pieces of at
 // most max_message_bytes(): RCCL was measured to lose the second half of a single >1 GiB self
 // send/recv (tools/loopback_probe.py); pieces to one peer match in issue order on both sides.
-void issue_exchange(comm* c, const plan& p, char* sb, char* rb, hipStream_t s) {
+// Round `round` of `rounds` (exchange_rounds(); rounds = 1: everything at once).
+void issue_exchange(comm* c, const plan& p, char* sb, char* rb, hipStream_t s, int round = 0,
+                    int rounds = 1) {
     const size_t E = dtype_size(p.dtype);
     const size_t piece = max_message_bytes();
     NCCL_CHECK(ncclGroupStart());
-    for (int r = 0; r < c->size; ++r) {
-        const size_t sbytes = size_t(p.send_counts[size_t(r)]) * E;
-        const size_t rbytes = size_t(p.recv_counts[size_t(r)]) * E;
+    for (int q = 0; q < c->size; ++q) {
+        int64_t slo, shi, rlo, rhi;
+        round_range(p.send_counts[size_t(q)], E, rounds, round, slo, shi);
+        round_range(p.recv_counts[size_t(q)], E, rounds, round, rlo, rhi);
+        const size_t sbytes = size_t(shi - slo) * E, rbytes = size_t(rhi - rlo) * E;
+        char* sp = sb + size_t(p.send_displs[size_t(q)] + slo) * E;
+        char* rp = rb + size_t(p.recv_displs[size_t(q)] + rlo) * E;
         for (size_t o = 0; o < sbytes; o += piece)
-            NCCL_CHECK(ncclSend(sb + size_t(p.send_displs[size_t(r)]) * E + o,
-                                std::min(piece, sbytes - o), ncclUint8, r, c->nccl, s));
+            NCCL_CHECK(ncclSend(sp + o, std::min(piece, sbytes - o), ncclUint8, q, c->nccl, s));
         for (size_t o = 0; o < rbytes; o += piece)
-            NCCL_CHECK(ncclRecv(rb + size_t(p.recv_displs[size_t(r)]) * E + o,
-                                std::min(piece, rbytes - o), ncclUint8, r, c->nccl, s));
+            NCCL_CHECK(ncclRecv(rp + o, std::min(piece, rbytes - o), ncclUint8, q, c->nccl, s));
     }
     NCCL_CHECK(ncclGroupEnd());
 }
@@ -924,31 +1019,46 @@ void transform(const std::vector<job>& jobs, comm* c, void* user_stream, bool as
     }
 
     if (exchange) {
-        HIP_CHECK(hipEventRecord(dc.ev_local, dc.aux));
         dc.send.reserve(size_t(p.send_elems) * E + 256);
         dc.recv.reserve(size_t(p.recv_elems) * E + 256);
         char* sb = static_cast<char*>(dc.send.p);
         char* rb = static_cast<char*>(dc.recv.p);
-        if (cp.l_pack.n_items()) {
-            tm.start(PH_PACK, dc.main);
+        // main: pack round r -> the exchange stream moves round r -> aux (after LOCAL): unpack
+        // round r; so packing r+1, moving r and unpacking r-1 overlap
+        const int R = int(cp.rounds.size());
+        dc.round_events(size_t(R));
+        for (int r = 0; r < R; ++r) {
+            const auto& x = *cp.rounds[size_t(r)];
+            if (x.l_pack.n_items()) {
+                tm.start(PH_PACK, dc.main);
+                launch_tiles(p.dtype,
+                             make_launch(x.l_pack, x.d_pack.p, x.w_pack.p, nullptr, sb, cp.d_scal.p,
+                                         false, false),
+                             dc.main);
+                tm.stop();
+            }
+            HIP_CHECK(hipEventRecord(dc.ev_packed[size_t(r)], dc.main));
+            HIP_CHECK(hipStreamWaitEvent(dc.xch, dc.ev_packed[size_t(r)], 0));
+            tm.start(PH_EXCHANGE, dc.xch);
+            issue_exchange(c, p, sb, rb, dc.xch, r, R);
+            tm.stop();
+            HIP_CHECK(hipEventRecord(dc.ev_moved[size_t(r)], dc.xch));
+        }
+        for (int r = 0; r < R; ++r) {
+            const auto& x = *cp.rounds[size_t(r)];
+            if (!x.l_unpack.n_items()) continue;
+            HIP_CHECK(hipStreamWaitEvent(dc.aux, dc.ev_moved[size_t(r)], 0));
+            tm.start(PH_UNPACK, dc.aux);
             launch_tiles(p.dtype,
-                         make_launch(cp.l_pack, cp.d_pack.p, cp.w_pack.p, nullptr, sb, cp.d_scal.p,
-                                     false, false),
-                         dc.main);
+                         make_launch(x.l_unpack, x.d_unpack.p, x.w_unpack.p, rb, nullptr,
+                                     cp.d_scal.p, x.tr_unpack, x.ax_unpack),
+                         dc.aux);
             tm.stop();
         }
-        tm.start(PH_EXCHANGE, dc.main);
-        issue_exchange(c, p, sb, rb, dc.main);
-        tm.stop();
-        if (cp.l_unpack.n_items()) {
-            tm.start(PH_UNPACK, dc.main);
-            launch_tiles(p.dtype,
-                         make_launch(cp.l_unpack, cp.d_unpack.p, cp.w_unpack.p, rb, nullptr,
-                                     cp.d_scal.p, cp.tr_unpack, cp.ax_unpack),
-                         dc.main);
-            tm.stop();
-        }
+        // the call ends on main once LOCAL, every unpack and every round of the exchange are done
+        HIP_CHECK(hipEventRecord(dc.ev_local, dc.aux));
         HIP_CHECK(hipStreamWaitEvent(dc.main, dc.ev_local, 0));
+        HIP_CHECK(hipStreamWaitEvent(dc.main, dc.ev_moved[size_t(R - 1)], 0));
     }
 
     // D2H of the target data
@@ -966,12 +1076,12 @@ void transform(const std::vector<job>& jobs, comm* c, void* user_stream, bool as
         g_stats.local_launches++;
         g_stats.local_bytes += p.local_bytes;
     }
-    if (exchange && cp.l_pack.n_items()) {
-        g_stats.pack_launches++;
+    if (exchange) {
+        for (const auto& x : cp.rounds) {
+            g_stats.pack_launches += x->l_pack.n_items() ? 1 : 0;
+            g_stats.unpack_launches += x->l_unpack.n_items() ? 1 : 0;
+        }
         g_stats.pack_bytes += p.pack_bytes;
-    }
-    if (exchange && cp.l_unpack.n_items()) {
-        g_stats.unpack_launches++;
         g_stats.unpack_bytes += p.unpack_bytes;
     }
 

@@ -92,6 +92,10 @@ int loopback_exchange();
 // largest single ncclSend/ncclRecv of the exchange (COSTA_MAX_MSG_BYTES, default 256 MiB)
 size_t max_message_bytes();
 
+// parts a peer's package (of at least 16 MiB) is exchanged in, each its own RCCL group, so that
+// pack, exchange and unpack overlap (COSTA_EXCHANGE_ROUNDS, default 4; every rank must agree)
+int exchange_rounds();
+
 // normalise one copy_and_transform call (memory_utils.hpp:339-412) into a tile op
 costa_tile_op_t make_tile_op(int n_rows, int n_cols, uint64_t src, int src_stride, bool src_cm,
                              uint64_t dst, int dst_stride, bool dst_cm, bool transpose, bool conj,
