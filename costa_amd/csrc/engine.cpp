@@ -260,6 +260,24 @@ size_t peer_of(const std::vector<int64_t>& displs, int64_t o) {
 }
 }  // namespace
 
+void exchange_round_of_ops(const plan& p, int rounds, std::vector<int>& pack_round,
+                           std::vector<int>& unpack_round) {
+    const size_t E = dtype_size(p.dtype);
+    pack_round.clear();
+    unpack_round.clear();
+    for (const auto& op : p.pack_ops) {
+        const int64_t o = int64_t(op.dst / E);
+        const size_t q = peer_of(p.send_displs, o);
+        pack_round.push_back(round_of(o - p.send_displs[q], p.send_counts[q], E, rounds));
+    }
+    for (const auto& op : p.unpack_ops) {
+        const int64_t first = int64_t(op.src / E);
+        const int64_t last = first + int64_t(op.nf) * op.ns - 1;
+        const size_t q = peer_of(p.recv_displs, first);
+        unpack_round.push_back(round_of(last - p.recv_displs[q], p.recv_counts[q], E, rounds));
+    }
+}
+
 int comm_rank(const comm* c) { return c->rank; }
 int comm_size(const comm* c) { return c->size; }
 void comm_destroy(comm* c) { delete c; }
@@ -706,8 +724,11 @@ cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
             if (host_pipeline_accepts(hplan->dtype, hplan->pack_ops)) {
                 cp->staged = false;
                 cp->p = std::move(hplan);
+                const int R = c->nccl ? exchange_rounds() : 1;
+                std::vector<int> pr, ur;
+                exchange_round_of_ops(*cp->p, R, pr, ur);
                 cp->pipe = make_host_pipeline(cp->p->dtype, cp->p->pack_ops, cp->p->local_ops,
-                                              cp->p->unpack_ops);
+                                              cp->p->unpack_ops, pr, ur, R);
                 g_plans.emplace_front(h.h, std::move(cp));
                 while (g_plans.size() > kMaxPlans) g_plans.pop_back();
                 return g_plans.front().second.get();
@@ -776,18 +797,10 @@ cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
     const int R = c->nccl ? exchange_rounds() : 1;
     std::vector<std::vector<costa_tile_op_t>> pk(static_cast<size_t>(R)), up(static_cast<size_t>(R));
     {
-        const size_t E = dtype_size(p.dtype);
-        for (const auto& op : p.pack_ops) {
-            const int64_t o = int64_t(op.dst / E);
-            const size_t q = peer_of(p.send_displs, o);
-            pk[size_t(round_of(o - p.send_displs[q], p.send_counts[q], E, R))].push_back(op);
-        }
-        for (const auto& op : p.unpack_ops) {
-            const int64_t first = int64_t(op.src / E);
-            const int64_t last = first + int64_t(op.nf) * op.ns - 1;
-            const size_t q = peer_of(p.recv_displs, first);
-            up[size_t(round_of(last - p.recv_displs[q], p.recv_counts[q], E, R))].push_back(op);
-        }
+        std::vector<int> pr, ur;
+        exchange_round_of_ops(p, R, pr, ur);
+        for (size_t i = 0; i < p.pack_ops.size(); ++i) pk[size_t(pr[i])].push_back(p.pack_ops[i]);
+        for (size_t i = 0; i < p.unpack_ops.size(); ++i) up[size_t(ur[i])].push_back(p.unpack_ops[i]);
     }
     std::vector<std::vector<costa_tile_op_t>> ord_p(static_cast<size_t>(R)), ord_u(static_cast<size_t>(R));
     std::vector<std::vector<uint64_t>> w_p(static_cast<size_t>(R)), w_u(static_cast<size_t>(R));
@@ -975,13 +988,16 @@ void transform(const std::vector<job>& jobs, comm* c, void* user_stream, bool as
     if (cp.pipe) {  // host-resident: pipelined gather -> H2D -> [exchange] -> kernels -> D2H
         const bool xchg = c->nccl != nullptr && (p.send_elems > 0 || p.recv_elems > 0);
         char *sb = nullptr, *rb = nullptr;
-        std::function<void(void*)> fn;
+        std::function<void(void*, int)> fn;
         if (xchg) {
             dc.send.reserve(size_t(p.send_elems) * E + 256);
             dc.recv.reserve(size_t(p.recv_elems) * E + 256);
             sb = static_cast<char*>(dc.send.p);
             rb = static_cast<char*>(dc.recv.p);
-            fn = [&](void* s) { issue_exchange(c, p, sb, rb, static_cast<hipStream_t>(s)); };
+            const int R = exchange_rounds();
+            fn = [&, R](void* s, int r) {
+                issue_exchange(c, p, sb, rb, static_cast<hipStream_t>(s), r, R);
+            };
         }
         // tile kernels on the aux stream, behind the scalars uploaded on main; the exchange on main
         HIP_CHECK(hipEventRecord(dc.ev_ready, dc.main));

@@ -176,17 +176,24 @@ launch_args make_launch(const work_split& w, const void* d_ordered, const void* 
 struct host_pipeline;
 // false when a pack op's column exceeds a pipeline slot (the mirror scheme is used then)
 bool host_pipeline_accepts(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& pack_ops);
+// pack_round / unpack_round: each op's exchange round (exchange_round_of_ops) of `rounds`
 std::shared_ptr<host_pipeline> make_host_pipeline(costa_dtype_t dtype,
                                                   const std::vector<costa_tile_op_t>& pack_ops,
                                                   const std::vector<costa_tile_op_t>& local_ops,
-                                                  const std::vector<costa_tile_op_t>& unpack_ops);
+                                                  const std::vector<costa_tile_op_t>& unpack_ops,
+                                                  const std::vector<int>& pack_round,
+                                                  const std::vector<int>& unpack_round, int rounds);
 size_t host_pipeline_groups(const host_pipeline& hp);
 // Blocking: returns when every target byte is back in host memory.  Tile kernels run on
-// `compute_stream`; `exchange` (empty without one) is called once, with `exchange_stream`, when
-// the send package is in `send_buf`; the unpack kernels read `recv_buf` after it.
+// `compute_stream`; `exchange(stream, r)` (empty without one) is called once per round r, with
+// `exchange_stream`, when round r's part of the send package is in `send_buf`; the unpack
+// kernels of round r read `recv_buf` after it.
 void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void* exchange_stream,
-                       char* send_buf, char* recv_buf, const std::function<void(void*)>& exchange,
-                       const void* d_scalars);
+                       char* send_buf, char* recv_buf,
+                       const std::function<void(void*, int)>& exchange, const void* d_scalars);
+// the exchange round of every pack op (by its first element) and unpack op (by its last)
+void exchange_round_of_ops(const struct plan& p, int rounds, std::vector<int>& pack_round,
+                           std::vector<int>& unpack_round);
 void release_host_rings();
 // host staging of host-resident layouts: 0 = mirror (every spanned range up, kernels, target
 // ranges down), 1 = pipelined (default; falls back to the mirror where it does not apply)

@@ -25,10 +25,12 @@
 // With an exchange (several ranks, the ScaLAPACK situation) the groups come in three kinds, in
 // this order (the reference's exchange_async, transform.cpp:46-128):
 //   PACK   the host gather IS the pack (a bit copy into the dense package): it goes straight
-//          into the device send buffer; after the last pack group the RCCL group starts
+//          into the device send buffer; after a round's last pack group its RCCL group starts
 //   LOCAL  as above, on the compute stream, overlapping the exchange
-//   UNPACK the unpack kernels read the receive buffer once the exchange is done and write dense
-//          target packages, copied back and scattered like LOCAL ones
+//   UNPACK the unpack kernels read the receive buffer once their round has arrived and write
+//          dense target packages, copied back and scattered like LOCAL ones
+// in the order PACK(0), LOCAL, PACK(1), UNPACK(0), ..., UNPACK(R-1) over the exchange rounds
+// (engine.cpp exchange_rounds()), so uploads of later rounds overlap downloads of earlier ones.
 #include <emmintrin.h>
 #include <hip/hip_runtime.h>
 
@@ -69,6 +71,7 @@ constexpr int kLag = 3;                       // scatter of group g runs at step
 static_assert(kLag < kRing, "a pinned target slot is scattered before its reuse");
 constexpr size_t kItemBytes = size_t(256) << 10;  // host copy work item
 constexpr size_t kAlign = 256;
+constexpr int kMaxRounds = 16;                // exchange rounds (engine.cpp exchange_rounds())
 
 size_t align_up(size_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
 
@@ -183,7 +186,8 @@ struct ring {
     char* pin_out = nullptr;  // kRing x kSlot: target package
     char* dev = nullptr;      // kRing x 2*kSlot: [source package | target package]
     hipEvent_t up_done[kRing]{}, kern_done[kRing]{}, down_done[kRing]{};
-    hipEvent_t packed = nullptr, exchanged = nullptr;  // send buffer uploaded / exchange done
+    hipEvent_t packed[kMaxRounds]{}, moved[kMaxRounds]{};  // per exchange round: its part of
+                                                             // the send buffer uploaded / moved
     explicit ring(int d) : device(d) {
         HP_CHECK(hipStreamCreateWithFlags(&up, hipStreamNonBlocking));
         HP_CHECK(hipStreamCreateWithFlags(&down, hipStreamNonBlocking));
@@ -193,8 +197,10 @@ struct ring {
         for (int k = 0; k < kRing; ++k)
             for (hipEvent_t* e : {&up_done[k], &kern_done[k], &down_done[k]})
                 HP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-        HP_CHECK(hipEventCreateWithFlags(&packed, hipEventDisableTiming));
-        HP_CHECK(hipEventCreateWithFlags(&exchanged, hipEventDisableTiming));
+        for (int r = 0; r < kMaxRounds; ++r) {
+            HP_CHECK(hipEventCreateWithFlags(&packed[r], hipEventDisableTiming));
+            HP_CHECK(hipEventCreateWithFlags(&moved[r], hipEventDisableTiming));
+        }
     }
     ~ring() {
         (void)hipSetDevice(device);
@@ -202,8 +208,10 @@ struct ring {
         (void)hipStreamSynchronize(down);
         for (int k = 0; k < kRing; ++k)
             for (hipEvent_t e : {up_done[k], kern_done[k], down_done[k]}) (void)hipEventDestroy(e);
-        (void)hipEventDestroy(packed);
-        (void)hipEventDestroy(exchanged);
+        for (int r = 0; r < kMaxRounds; ++r) {
+            (void)hipEventDestroy(packed[r]);
+            (void)hipEventDestroy(moved[r]);
+        }
         (void)hipFree(dev);
         (void)hipHostFree(pin_in);
         (void)hipHostFree(pin_out);
@@ -241,6 +249,7 @@ struct host_pipeline {
     };
     struct group {
         kind_t kind = LOCAL;
+        int round = 0;                // PACK / UNPACK: its exchange round
         size_t first = 0, count = 0;  // hops
         size_t in_bytes = 0, out_bytes = 0;
         uint64_t send_off = 0;        // PACK: the group's byte range starts here in the send buffer
@@ -254,8 +263,12 @@ struct host_pipeline {
     costa_dtype_t dtype = COSTA_DOUBLE;
     size_t E = 8;
     std::vector<hop> hops;
-    std::vector<group> groups;  // PACK groups, then LOCAL, then UNPACK
-    size_t n_pack_groups = 0;
+    // execution order: PACK(0), LOCAL, then PACK(r), UNPACK(r-1) for r = 1..R-1, UNPACK(R-1):
+    // uploads of later rounds overlap the downloads of earlier ones
+    std::vector<group> groups;
+    int rounds = 1;
+    int rounds_before = 0;            // exchange rounds issued before the first group
+    std::vector<int> rounds_after;    // ... issued once group t is enqueued (cumulative)
     void* d_ops = nullptr;   // every group's ordered device ops (package offsets)
     void* d_work = nullptr;
     ~host_pipeline() {
@@ -317,38 +330,51 @@ bool host_pipeline_accepts(costa_dtype_t dtype, const std::vector<costa_tile_op_
 std::shared_ptr<host_pipeline> make_host_pipeline(costa_dtype_t dtype,
                                                   const std::vector<costa_tile_op_t>& pack_ops,
                                                   const std::vector<costa_tile_op_t>& local_ops,
-                                                  const std::vector<costa_tile_op_t>& unpack_ops) {
+                                                  const std::vector<costa_tile_op_t>& unpack_ops,
+                                                  const std::vector<int>& pack_round,
+                                                  const std::vector<int>& unpack_round, int rounds) {
     using hpl = host_pipeline;
+    if (rounds < 1 || rounds > kMaxRounds) throw error(COSTA_ERR_ARG, "costa: exchange rounds out of range");
     auto hp = std::make_shared<hpl>();
     hp->dtype = dtype;
+    hp->rounds = rounds;
     const size_t E = dtype_size(dtype);
     hp->E = E;
 
-    // groups in list order (the planner's key order: for block-cyclic layouts a local group is
-    // a band of target rows read from a band of source columns; pack groups are consecutive
-    // ranges of the send package)
+    // segments in execution order; groups in list order inside a segment (the planner's key
+    // order: for block-cyclic layouts a local group is a band of target rows read from a band
+    // of source columns; pack groups are contiguous ranges of the send package)
+    std::vector<std::pair<hpl::kind_t, int>> segs{{hpl::PACK, 0}, {hpl::LOCAL, 0}};
+    for (int r = 1; r < rounds; ++r) {
+        segs.push_back({hpl::PACK, r});
+        segs.push_back({hpl::UNPACK, r - 1});
+    }
+    segs.push_back({hpl::UNPACK, rounds - 1});
     hpl::group g;
     auto close = [&] {
         const hpl::kind_t k = g.kind;
+        const int rd = g.round;
         if (g.count) hp->groups.push_back(std::move(g));
         g = hpl::group{};
         g.kind = k;
+        g.round = rd;
         g.first = hp->hops.size();
     };
-    for (int kind = hpl::PACK; kind <= hpl::UNPACK; ++kind) {
+    for (const auto& sg : segs) {
+        const hpl::kind_t kind = sg.first;
         const auto& ops = kind == hpl::PACK ? pack_ops : kind == hpl::LOCAL ? local_ops : unpack_ops;
+        const auto* rd = kind == hpl::PACK ? &pack_round : kind == hpl::UNPACK ? &unpack_round : nullptr;
         std::vector<costa_tile_op_t> pieces;
-        pieces.reserve(ops.size());
-        for (const auto& op : ops) cut(op, E, kind == hpl::PACK, pieces);
+        for (size_t i = 0; i < ops.size(); ++i)
+            if (!rd || (*rd)[i] == sg.second) cut(ops[i], E, kind == hpl::PACK, pieces);
         close();
-        g.kind = hpl::kind_t(kind);
+        g.kind = kind;
+        g.round = sg.second;
         for (const auto& p : pieces) {
             const size_t bytes = size_t(p.nf) * size_t(p.ns) * E;
-            if (kind == hpl::PACK) {  // dense and contiguous in package order
-                if (g.count && g.in_bytes + bytes > kSlot) close();
+            if (kind == hpl::PACK) {  // dense; a group is one contiguous range of the package
+                if (g.count && (g.in_bytes + bytes > kSlot || p.dst != g.send_off + g.in_bytes)) close();
                 if (!g.count) g.send_off = p.dst;
-                if (p.dst != g.send_off + g.in_bytes)
-                    throw error(COSTA_ERR_INTERNAL, "costa: pack package not contiguous");
                 hp->hops.push_back({p, p.dst - g.send_off, 0});
                 g.in_bytes += bytes;
             } else {
@@ -362,7 +388,19 @@ std::shared_ptr<host_pipeline> make_host_pipeline(costa_dtype_t dtype,
             ++g.count;
         }
         close();
-        if (kind == hpl::PACK) hp->n_pack_groups = hp->groups.size();
+    }
+    // round r of the exchange is issued once every pack group of rounds <= r is enqueued
+    std::vector<int> last_pack(size_t(rounds), -1);
+    for (size_t t = 0; t < hp->groups.size(); ++t)
+        if (hp->groups[t].kind == hpl::PACK) last_pack[size_t(hp->groups[t].round)] = int(t);
+    hp->rounds_after.assign(hp->groups.size(), 0);
+    int upto = -1;
+    for (int r = 0; r < rounds; ++r) {
+        upto = std::max(upto, last_pack[size_t(r)]);
+        if (upto < 0)
+            hp->rounds_before = r + 1;
+        else
+            for (size_t t = size_t(upto); t < hp->groups.size(); ++t) hp->rounds_after[t] = r + 1;
     }
 
     // device op lists (LOCAL / UNPACK): every op writes the dense target package (ldd = the
@@ -428,8 +466,8 @@ std::shared_ptr<host_pipeline> make_host_pipeline(costa_dtype_t dtype,
 size_t host_pipeline_groups(const host_pipeline& hp) { return hp.groups.size(); }
 
 void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void* exchange_stream,
-                       char* send_buf, char* recv_buf, const std::function<void(void*)>& exchange,
-                       const void* d_scalars) {
+                       char* send_buf, char* recv_buf,
+                       const std::function<void(void*, int)>& exchange, const void* d_scalars) {
     using hpl = host_pipeline;
     ring& R = ring_of(device);
     hipStream_t comp = static_cast<hipStream_t>(compute_stream);
@@ -459,20 +497,20 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
         HP_CHECK(hipEventRecord(R.up_done[k], R.up));
         HP_CHECK(hipEventRecord(R.down_done[k], R.down));
     }
-    // the exchange starts once the whole send package is in HBM (after the last pack group's
-    // upload, or at once when there is nothing to send); LOCAL groups overlap it
-    bool exchanged = false;
-    auto issue_exchange = [&] {
-        if (!exchange || exchanged) return;
-        HP_CHECK(hipEventRecord(R.packed, R.up));
-        HP_CHECK(hipStreamWaitEvent(xs, R.packed, 0));
-        if (prof) x0 = ev(xs);
-        exchange(xs);
-        if (prof) x1 = ev(xs);
-        HP_CHECK(hipEventRecord(R.exchanged, xs));
-        exchanged = true;
+    // exchange round r starts once its part of the send package is in HBM (after the last pack
+    // group of rounds <= r); LOCAL groups and the pack groups of later rounds overlap it
+    int issued = 0;
+    auto issue_rounds = [&](int upto) {
+        for (; issued < upto && exchange; ++issued) {
+            HP_CHECK(hipEventRecord(R.packed[issued], R.up));
+            HP_CHECK(hipStreamWaitEvent(xs, R.packed[issued], 0));
+            if (prof && !x0) x0 = ev(xs);
+            exchange(xs, issued);
+            if (prof) x1 = ev(xs);
+            HP_CHECK(hipEventRecord(R.moved[issued], xs));
+        }
     };
-    if (hp.n_pack_groups == 0) issue_exchange();
+    issue_rounds(hp.rounds_before);
 
     // Host copy work of one step: the source gather of group t (plus its old target values
     // when an op reads C) and the target scatter of group t - kLag, in one parallel pass.
@@ -550,13 +588,13 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
                                     R.up));
             HP_CHECK(hipEventRecord(R.up_done[k], R.up));
             if (prof) up1 = ev(R.up);
-            if (t + 1 == hp.n_pack_groups) issue_exchange();
+            issue_rounds(hp.rounds_after[t]);
             t_issue += now() - t3;
             continue;
         }
         const bool unpack = g->kind == hpl::UNPACK;
-        if (unpack && !exchanged)
-            throw error(COSTA_ERR_INTERNAL, "costa: unpack group without an exchange");
+        if (unpack && (!exchange || issued <= g->round))
+            throw error(COSTA_ERR_INTERNAL, "costa: unpack group before its exchange round");
         // the device slot is free once its previous target package has been copied out
         HP_CHECK(hipStreamWaitEvent(R.up, R.down_done[k], 0));
         if (g->in_bytes || g->reads_old) {
@@ -569,7 +607,7 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
         }
         HP_CHECK(hipEventRecord(R.up_done[k], R.up));
         HP_CHECK(hipStreamWaitEvent(comp, R.up_done[k], 0));
-        if (unpack) HP_CHECK(hipStreamWaitEvent(comp, R.exchanged, 0));
+        if (unpack) HP_CHECK(hipStreamWaitEvent(comp, R.moved[g->round], 0));
         hipEvent_t k0 = prof ? ev(comp) : nullptr;
         launch_tiles(hp.dtype,
                      make_launch(g->split, static_cast<const costa_tile_op_t*>(hp.d_ops) + g->ord_first,
@@ -587,14 +625,15 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
                                 hipMemcpyDeviceToHost, R.down));
         HP_CHECK(hipEventRecord(R.down_done[k], R.down));
         if (prof) dn1 = ev(R.down);
+        issue_rounds(hp.rounds_after[t]);
         t_issue += now() - t3;
     }
-    issue_exchange();  // a rank with nothing to upload still takes part in the exchange
+    issue_rounds(hp.rounds);  // a rank with nothing to upload still takes part in the exchange
     if (trace)
         std::fprintf(stderr,
-                     "[costa host pipe] groups %zu (%zu pack) slot %zu MiB threads %d: total %.2f "
-                     "ms, copies %.2f, wait-up %.2f, wait-down %.2f, issue %.2f\n",
-                     G, hp.n_pack_groups, kSlot >> 20, host_threads(), (now() - t_begin) * 1e3,
+                     "[costa host pipe] groups %zu, %d exchange round(s), slot %zu MiB threads %d: "
+                     "total %.2f ms, copies %.2f, wait-up %.2f, wait-down %.2f, issue %.2f\n",
+                     G, exchange ? hp.rounds : 0, kSlot >> 20, host_threads(), (now() - t_begin) * 1e3,
                      t_copy * 1e3, t_wait_up * 1e3, t_wait_down * 1e3, t_issue * 1e3);
     HP_CHECK(hipStreamSynchronize(R.up));
     HP_CHECK(hipStreamSynchronize(xs));

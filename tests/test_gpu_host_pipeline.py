@@ -54,9 +54,9 @@ def test_golden_host_resident(gpu, case, mode):
         assert st["host_groups"] >= 1, "pipelined staging did not run"
 
 
-# (m, n, mb, nb): many tiles over several 32 MiB groups; one 60 MB block cut into pieces;
+# (m, n, mb, nb): many tiles over several 64 MiB groups; one 96 MB block cut into pieces;
 # ragged small blocks in one group
-SHAPES = [(6000, 5000, 1000, 700), (3000, 2500, 3000, 2500), (1000, 900, 100, 70)]
+SHAPES = [(6000, 5000, 1000, 700), (4000, 3000, 4000, 3000), (1000, 900, 100, 70)]
 
 
 @pytest.mark.parametrize("mode", [1, 0])
@@ -81,7 +81,7 @@ def test_large_host_vs_numpy(gpu, mode, shape, trans, alpha, beta):
     exp = alpha * x if beta == 0 else beta * c0 + alpha * x
     assert np.array_equal(c.view(np.uint64), exp.view(np.uint64))
     if mode == 1:
-        assert st["host_groups"] >= (2 if m * n * 8 > (32 << 20) else 1)
+        assert st["host_groups"] >= (2 if m * n * 8 > (64 << 20) else 1)
 
 
 @pytest.mark.parametrize("mode", [1, 0])
