@@ -29,8 +29,9 @@
 //   LOCAL  as above, on the compute stream, overlapping the exchange
 //   UNPACK the unpack kernels read the receive buffer once their round has arrived and write
 //          dense target packages, copied back and scattered like LOCAL ones
-// in the order PACK(0), LOCAL, PACK(1), UNPACK(0), ..., UNPACK(R-1) over the exchange rounds
-// (engine.cpp exchange_rounds()), so uploads of later rounds overlap downloads of earlier ones.
+// in the order PACK(0) | LOCAL, PACK(1) | UNPACK(0), ..., UNPACK(R-1) over the exchange rounds
+// (engine.cpp exchange_rounds(); "|": alternating group by group), so the uploads of one round
+// and the downloads of the previous one share the ring.
 #include <emmintrin.h>
 #include <hip/hip_runtime.h>
 
@@ -263,8 +264,8 @@ struct host_pipeline {
     costa_dtype_t dtype = COSTA_DOUBLE;
     size_t E = 8;
     std::vector<hop> hops;
-    // execution order: PACK(0), LOCAL, then PACK(r), UNPACK(r-1) for r = 1..R-1, UNPACK(R-1):
-    // uploads of later rounds overlap the downloads of earlier ones
+    // execution order (make_host_pipeline): PACK(0) | LOCAL, PACK(r) | UNPACK(r-1) for
+    // r = 1..R-1, UNPACK(R-1), "|" alternating group by group
     std::vector<group> groups;
     int rounds = 1;
     int rounds_before = 0;            // exchange rounds issued before the first group
@@ -341,26 +342,28 @@ std::shared_ptr<host_pipeline> make_host_pipeline(costa_dtype_t dtype,
     const size_t E = dtype_size(dtype);
     hp->E = E;
 
-    // segments in execution order; groups in list order inside a segment (the planner's key
-    // order: for block-cyclic layouts a local group is a band of target rows read from a band
-    // of source columns; pack groups are contiguous ranges of the send package)
-    std::vector<std::pair<hpl::kind_t, int>> segs{{hpl::PACK, 0}, {hpl::LOCAL, 0}};
-    for (int r = 1; r < rounds; ++r) {
+    // Segments: PACK(r), LOCAL, UNPACK(r); groups in list order inside a segment (the planner's
+    // key order: for block-cyclic layouts a local group is a band of target rows read from a
+    // band of source columns; pack groups are contiguous ranges of the send package).
+    std::vector<std::pair<hpl::kind_t, int>> segs{{hpl::LOCAL, 0}};
+    for (int r = 0; r < rounds; ++r) {
         segs.push_back({hpl::PACK, r});
-        segs.push_back({hpl::UNPACK, r - 1});
+        segs.push_back({hpl::UNPACK, r});
     }
-    segs.push_back({hpl::UNPACK, rounds - 1});
+    std::map<std::pair<int, int>, std::vector<hpl::group>> built;
+    std::vector<hpl::group>* dest = nullptr;
     hpl::group g;
     auto close = [&] {
         const hpl::kind_t k = g.kind;
         const int rd = g.round;
-        if (g.count) hp->groups.push_back(std::move(g));
+        if (g.count) dest->push_back(std::move(g));
         g = hpl::group{};
         g.kind = k;
         g.round = rd;
         g.first = hp->hops.size();
     };
     for (const auto& sg : segs) {
+        dest = &built[{int(sg.first), sg.second}];
         const hpl::kind_t kind = sg.first;
         const auto& ops = kind == hpl::PACK ? pack_ops : kind == hpl::LOCAL ? local_ops : unpack_ops;
         const auto* rd = kind == hpl::PACK ? &pack_round : kind == hpl::UNPACK ? &unpack_round : nullptr;
@@ -389,6 +392,20 @@ std::shared_ptr<host_pipeline> make_host_pipeline(costa_dtype_t dtype,
         }
         close();
     }
+    // Execution order: PACK(0) alternating with LOCAL, then PACK(r) alternating with UNPACK(r-1)
+    // for r = 1..R-1, then UNPACK(R-1): uploads and downloads alternate through the ring, so
+    // both copy directions stay busy (PCIe duplex)
+    auto interleave = [&](std::vector<hpl::group>& a, std::vector<hpl::group>& b) {
+        for (size_t i = 0; i < std::max(a.size(), b.size()); ++i) {
+            if (i < a.size()) hp->groups.push_back(std::move(a[i]));
+            if (i < b.size()) hp->groups.push_back(std::move(b[i]));
+        }
+    };
+    interleave(built[{int(hpl::PACK), 0}], built[{int(hpl::LOCAL), 0}]);
+    for (int r = 1; r < rounds; ++r)
+        interleave(built[{int(hpl::PACK), r}], built[{int(hpl::UNPACK), r - 1}]);
+    std::vector<hpl::group> none;
+    interleave(built[{int(hpl::UNPACK), rounds - 1}], none);
     // round r of the exchange is issued once every pack group of rounds <= r is enqueued
     std::vector<int> last_pack(size_t(rounds), -1);
     for (size_t t = 0; t < hp->groups.size(); ++t)
