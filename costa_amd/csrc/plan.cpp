@@ -54,7 +54,7 @@ elayout erase(const grid_layout<T>& L) {
         throw error(COSTA_ERR_ARG, "costa: layouts must not be left transposed by the caller");
     e.rows_split = g.grid().rows_split;
     e.cols_split = g.grid().cols_split;
-    e.owners = g.owners_row_major();
+    e.owners = g.reordered_owners_row_major();  // with a rank relabelling applied
     e.n_ranks = g.num_ranks();
     e.ordering = L.ordering;
     e.blocks.reserve(size_t(L.blocks.num_blocks()));

@@ -111,13 +111,28 @@ class assigned_grid2D {
             throw std::runtime_error("costa::assigned_grid2D: owners size mismatch");
     }
 
-    // owner of block (i, j) in the CURRENT (possibly transposed) orientation
+    // owner of block (i, j) in the CURRENT (possibly transposed) orientation, relabelled when
+    // reorder_ranks was called (reference grid2D.hpp:186)
     int owner(int i, int j) const {
         int r = transposed_ ? j : i;
         int c = transposed_ ? i : j;
         int stored_cols = transposed_ ? g_.n_rows : g_.n_cols;
-        return owners_[size_t(r) * size_t(stored_cols) + size_t(c)];
+        return reordered_rank(owners_[size_t(r) * size_t(stored_cols) + size_t(c)]);
     }
+    // rank relabelling (reference grid2D.hpp:75-79, 219-233): rank k of the grid becomes
+    // reordering[k] (costa::optimal_reordering proposes one)
+    void reorder_ranks(const std::vector<int>& reordering) {
+        if (!reordering.empty() && int(reordering.size()) < n_ranks_)
+            throw std::runtime_error("costa::assigned_grid2D: reordering shorter than the ranks");
+        for (int k : reordering)
+            if (k < 0 || k >= std::max(n_ranks_, int(reordering.size())))
+                throw std::runtime_error("costa::assigned_grid2D: reordering out of range");
+        reordering_ = reordering;
+    }
+    int reordered_rank(int rank) const {
+        return reordering_.empty() ? rank : reordering_[size_t(rank)];
+    }
+    bool ranks_reordered() const noexcept { return !reordering_.empty(); }
     const grid2D& grid() const noexcept { return g_; }
     int num_ranks() const noexcept { return n_ranks_; }
     interval rows_interval(int i) const { return g_.row_interval(i); }
@@ -132,11 +147,20 @@ class assigned_grid2D {
     int num_blocks_col() const noexcept { return g_.n_cols; }
     int num_rows() const noexcept { return g_.rows_split.empty() ? 0 : g_.rows_split.back(); }
     int num_cols() const noexcept { return g_.cols_split.empty() ? 0 : g_.cols_split.back(); }
+    // stored owners, row-major in the stored (untransposed) orientation, before relabelling
     const std::vector<int>& owners_row_major() const noexcept { return owners_; }
+    // the same with the relabelling applied (what the planner uses)
+    std::vector<int> reordered_owners_row_major() const {
+        if (reordering_.empty()) return owners_;
+        std::vector<int> o(owners_.size());
+        for (size_t k = 0; k < o.size(); ++k) o[k] = reordering_[size_t(owners_[k])];
+        return o;
+    }
 
   private:
     grid2D g_;
     std::vector<int> owners_;
+    std::vector<int> reordering_;  // empty: identity
     int n_ranks_ = 0;
     bool transposed_ = false;
 };
@@ -229,6 +253,10 @@ class grid_layout {
         grid.transpose();
         blocks.transpose();
     }
+    // rank relabelling of the grid (reference grid_layout.hpp:32-42)
+    void reorder_ranks(const std::vector<int>& reordering) { grid.reorder_ranks(reordering); }
+    int reordered_rank(int rank) const { return grid.reordered_rank(rank); }
+    bool ranks_reordered() const { return grid.ranks_reordered(); }
     int num_cols() const noexcept { return grid.num_cols(); }
     int num_rows() const noexcept { return grid.num_rows(); }
     int num_blocks_col() const noexcept { return grid.num_blocks_col(); }

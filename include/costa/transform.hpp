@@ -11,6 +11,7 @@
 // MPI available, <costa/mpi.hpp> adds the reference's exact MPI_Comm signatures on top.
 #pragma once
 
+#include <costa/grid2grid/comm_volume.hpp>
 #include <costa/layout.hpp>
 #include <costa_hip.h>
 
@@ -41,6 +42,13 @@ template <typename T>
 void transform(std::vector<layout_ref<T>>& initial_layouts,
                std::vector<layout_ref<T>>& final_layouts, const char* trans, const T* alpha,
                const T* beta, costa_comm_t comm);
+
+// Elements each rank pair exchanges when g_init is transformed into g_final with op `trans`
+// (reference transform.hpp:44-48 / transform.cpp:9-44): every block of g_init (transposed view
+// for 'T' / 'C') is intersected with the blocks of g_final; edge {a, b} (a <= b) adds the area
+// owned by a in g_init and by b in g_final, relabelled owners included.  Host-only.
+comm_volume communication_volume(assigned_grid2D& g_init, assigned_grid2D& g_final,
+                                 char trans = 'N');
 
 // batches several layout pairs into one exchange (reference transformer.hpp:8-62)
 template <typename T>
@@ -145,6 +153,27 @@ inline costa_comm_t comm_from_mpi(MPI_Comm comm, int device = -1) {
 
 template <typename T>
 transformer<T>::transformer(MPI_Comm c) : comm(comm_from_mpi(c)) {}
+
+// Rank-pair cost factors for comm_volume::apply_topology (reference utils.hpp:12,
+// utils.cpp:30-88): 1 between nodes, 2 for ranks sharing a node (their volume counts half).
+// Collective over `comm`.
+inline std::vector<std::vector<int>> topology_cost(MPI_Comm comm) {
+    int P = 1, rank = 0;
+    MPI_Comm_size(comm, &P);
+    MPI_Comm_rank(comm, &rank);
+    MPI_Comm node;
+    MPI_Comm_split_type(comm, MPI_COMM_TYPE_SHARED, rank, MPI_INFO_NULL, &node);
+    int node_id = rank;  // a node is named by its smallest rank
+    MPI_Allreduce(&rank, &node_id, 1, MPI_INT, MPI_MIN, node);
+    MPI_Comm_free(&node);
+    std::vector<int> node_of(size_t(P), 0);
+    MPI_Allgather(&node_id, 1, MPI_INT, node_of.data(), 1, MPI_INT, comm);
+    std::vector<std::vector<int>> cost(size_t(P), std::vector<int>(size_t(P), 1));
+    for (int i = 0; i < P; ++i)
+        for (int j = 0; j < P; ++j)
+            if (node_of[size_t(i)] == node_of[size_t(j)]) cost[size_t(i)][size_t(j)] = 2;
+    return cost;
+}
 
 template <typename T>
 void transform(grid_layout<T>& A, grid_layout<T>& C, MPI_Comm comm) {

@@ -13,12 +13,20 @@
 //                                        threads: OMP_NUM_THREADS); prints one JSON line.
 //                                        Run by bench.py (cpu_baseline, rank 0, N = 1) on the
 //                                        GPU box as a child process, as the timed baseline.
+//   ref_harness relabel <spec>           rank relabelling of two grids (spec: P, trans, then
+//                                        per grid its row splits, col splits, owners): prints
+//                                        the communication volume, the reference's proposed
+//                                        permutation and the volume after relabelling (JSON)
 #include <costa/layout.hpp>
 #include <costa/grid2grid/transform.hpp>
 #include <costa/grid2grid/transformer.hpp>
 #include <costa/grid2grid/memory_utils.hpp>
 #include <costa/grid2grid/workspace.hpp>
+#include <costa/grid2grid/ranks_reordering.hpp>
 #include <mpi.h>
+
+#include <algorithm>
+#include <tuple>
 
 #include <omp.h>
 
@@ -264,6 +272,55 @@ int run_bench(int m, int n, int nb, double seconds) {
     return ok ? 0 : 1;
 }
 
+// spec: P trans / per grid: n_rs rs... n_cs cs... owners (row-major)
+costa::assigned_grid2D read_grid(std::istream& in, int P) {
+    auto vec = [&]() {
+        int n;
+        in >> n;
+        std::vector<int> v(static_cast<size_t>(n));
+        for (auto& x : v) in >> x;
+        return v;
+    };
+    std::vector<int> rs = vec(), cs = vec();
+    const int nbr = int(rs.size()) - 1, nbc = int(cs.size()) - 1;
+    std::vector<std::vector<int>> own(static_cast<size_t>(nbr), std::vector<int>(static_cast<size_t>(nbc)));
+    for (auto& row : own)
+        for (auto& x : row) in >> x;
+    return costa::assigned_grid2D(costa::grid2D(std::move(rs), std::move(cs)), std::move(own), P);
+}
+
+void print_volume(const char* key, const costa::comm_volume& cv) {
+    std::vector<std::tuple<int, int, size_t>> e;
+    for (const auto& kv : cv.volume)
+        if (kv.second) e.emplace_back(kv.first.src, kv.first.dest, kv.second);
+    std::sort(e.begin(), e.end());
+    std::printf("\"%s\": [", key);
+    for (size_t i = 0; i < e.size(); ++i)
+        std::printf("%s[%d, %d, %zu]", i ? ", " : "", std::get<0>(e[i]), std::get<1>(e[i]), std::get<2>(e[i]));
+    std::printf("]");
+}
+
+int run_relabel(const char* spec) {
+    std::ifstream in(spec);
+    int P;
+    char trans;
+    in >> P >> trans;
+    auto gi = read_grid(in, P);
+    auto gf = read_grid(in, P);
+    auto cv = costa::communication_volume(gi, gf, trans);
+    bool reordered = false;
+    auto perm = costa::optimal_reordering(cv, P, reordered);
+    gf.reorder_ranks(perm);
+    auto cv2 = costa::communication_volume(gi, gf, trans);
+    std::printf("{\"total\": %zu, \"new_total\": %zu, \"reordered\": %s, \"perm\": [", cv.total_volume(),
+                cv2.total_volume(), reordered ? "true" : "false");
+    for (size_t i = 0; i < perm.size(); ++i) std::printf("%s%d", i ? ", " : "", perm[i]);
+    std::printf("], ");
+    print_volume("volume", cv);
+    std::printf("}\n");
+    return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -290,9 +347,12 @@ int main(int argc, char** argv) {
         rc = rank == 0 ? run_bench(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]),
                                    std::atof(argv[5]))
                        : 0;
+    } else if (argc >= 3 && std::string(argv[1]) == "relabel") {
+        rc = rank == 0 ? run_relabel(argv[2]) : 0;
     } else {
         if (rank == 0)
-            std::cerr << "usage: ref_harness kat <out> | case <spec> <out> | bench <m> <n> <nb> <s>\n";
+            std::cerr << "usage: ref_harness kat <out> | case <spec> <out> | bench <m> <n> <nb> <s>"
+                         " | relabel <spec>\n";
     }
     MPI_Finalize();
     return rc;
