@@ -56,9 +56,12 @@ static double a_val(int i, int j) { return 1.0 + i * 7919.0 + j * 0.5; }
 static double c_val(int i, int j) { return -3.0 + i * 0.25 - j * 104729.0; }
 
 // one job on P ranks; make_a / make_c(rank, buffer) build each rank's layout
+// `relabel` (a rank permutation, involution): rank r builds C with the blocks of rank
+// relabel[r] and every C layout gets reorder_ranks(relabel), as README.md:343-362 prescribes
 template <typename MA, typename MC>
 static void run_case(const char* name, int P, MA make_a, MC make_c, size_t a_elems, size_t c_elems,
-                     char op, double alpha, double beta, int loopback = 0) {
+                     char op, double alpha, double beta, int loopback = 0,
+                     const std::vector<int>& relabel = {}) {
     std::vector<std::vector<double>> abuf, cbuf;
     std::vector<grid_layout<double>> la, lc;
     std::vector<elayout> ea, ec;
@@ -68,7 +71,8 @@ static void run_case(const char* name, int P, MA make_a, MC make_c, size_t a_ele
     }
     for (int r = 0; r < P; ++r) {
         la.push_back(make_a(r, abuf[size_t(r)].data()));
-        lc.push_back(make_c(r, cbuf[size_t(r)].data()));
+        lc.push_back(make_c(relabel.empty() ? r : relabel[size_t(r)], cbuf[size_t(r)].data()));
+        if (!relabel.empty()) lc.back().reorder_ranks(relabel);
         la.back().initialize(a_val);
         lc.back().initialize(c_val);
     }
@@ -138,7 +142,8 @@ static std::pair<int, int> local_dims(const bc& g, int rank) {
 
 static int cases = 0;
 
-static void run_bc(const char* name, bc a, bc c, char op, double alpha, double beta, int loop = 0) {
+static void run_bc(const char* name, bc a, bc c, char op, double alpha, double beta, int loop = 0,
+                   const std::vector<int>& relabel = {}) {
     const int P = std::max(a.pm * a.pn, c.pm * c.pn);
     size_t ae = 0, ce = 0;
     for (int r = 0; r < P; ++r) {
@@ -152,7 +157,7 @@ static void run_bc(const char* name, bc a, bc c, char op, double alpha, double b
                                                g.order, 0, 0, p, local_dims(g, r).first, g.ord, r);
         };
     };
-    run_case(name, P, mk(a), mk(c), ae, ce, op, alpha, beta, loop);
+    run_case(name, P, mk(a), mk(c), ae, ce, op, alpha, beta, loop, relabel);
     ++cases;
 }
 
@@ -167,6 +172,8 @@ int main() {
            {190, 257, 40, 24, 1, 1, 190, 257, 3, 2, 'R', 'R'}, 'T', 2.0, 0.5);
     run_bc("row-major source, sub-matrices", {260, 240, 30, 20, 5, 7, 200, 180, 2, 2, 'R', 'R'},
            {190, 210, 16, 48, 3, 2, 180, 200, 1, 4, 'C', 'C'}, 'T', -0.75, 0.0);
+    run_bc("2x2 -> 4x1 relabelled target", {300, 280, 64, 64, 1, 1, 300, 280, 2, 2, 'R', 'C'},
+           {300, 280, 50, 70, 1, 1, 300, 280, 4, 1, 'R', 'C'}, 'N', 1.0, 0.0, 0, {2, 3, 0, 1});
     run_bc("1 rank, loopback all", {200, 150, 32, 48, 1, 1, 200, 150, 1, 1, 'R', 'C'},
            {150, 200, 40, 24, 1, 1, 150, 200, 1, 1, 'R', 'C'}, 'T', 1.0, 0.0, 1);
     run_bc("1 rank, loopback half", {200, 150, 32, 48, 1, 1, 200, 150, 1, 1, 'R', 'C'},
