@@ -182,19 +182,20 @@ pool& thread_pool() {  // never destroyed: its threads outlive static destructio
 // ---------------------------------------------------------------- per-device ring
 struct ring {
     int device = 0;
+    size_t slot = 0;          // bytes of one package; at most kSlot, sized to the largest group
     hipStream_t up = nullptr, down = nullptr;
-    char* pin_in = nullptr;   // kRing x 2*kSlot: [source package | old target package]
-    char* pin_out = nullptr;  // kRing x kSlot: target package
-    char* dev = nullptr;      // kRing x 2*kSlot: [source package | target package]
+    char* pin_in = nullptr;   // kRing x 2*slot: [source package | old target package]
+    char* pin_out = nullptr;  // kRing x slot: target package
+    char* dev = nullptr;      // kRing x 2*slot: [source package | target package]
     hipEvent_t up_done[kRing]{}, kern_done[kRing]{}, down_done[kRing]{};
     hipEvent_t packed[kMaxRounds]{}, moved[kMaxRounds]{};  // per exchange round: its part of
                                                              // the send buffer uploaded / moved
-    explicit ring(int d) : device(d) {
+    ring(int d, size_t slot_bytes) : device(d), slot(slot_bytes) {
         HP_CHECK(hipStreamCreateWithFlags(&up, hipStreamNonBlocking));
         HP_CHECK(hipStreamCreateWithFlags(&down, hipStreamNonBlocking));
-        HP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&pin_in), kRing * 2 * kSlot, hipHostMallocDefault));
-        HP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&pin_out), kRing * kSlot, hipHostMallocDefault));
-        HP_CHECK(hipMalloc(reinterpret_cast<void**>(&dev), kRing * 2 * kSlot));
+        HP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&pin_in), kRing * 2 * slot, hipHostMallocDefault));
+        HP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&pin_out), kRing * slot, hipHostMallocDefault));
+        HP_CHECK(hipMalloc(reinterpret_cast<void**>(&dev), kRing * 2 * slot));
         for (int k = 0; k < kRing; ++k)
             for (hipEvent_t* e : {&up_done[k], &kern_done[k], &down_done[k]})
                 HP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
@@ -226,10 +227,16 @@ std::map<int, std::unique_ptr<ring>>& rings() {  // freed by release_caches(), n
     return *m;
 }
 
-ring& ring_of(int device) {
+// the device's ring, reallocated when a pipeline needs larger slots than it has: a small
+// host-resident call pins a few MiB, not kRing x 3 x kSlot
+ring& ring_of(int device, size_t slot_bytes) {
     auto& m = rings();
     auto it = m.find(device);
-    if (it == m.end()) it = m.emplace(device, std::make_unique<ring>(device)).first;
+    if (it != m.end() && it->second->slot < slot_bytes) {
+        m.erase(it);  // the destructor waits for the ring's copy streams
+        it = m.end();
+    }
+    if (it == m.end()) it = m.emplace(device, std::make_unique<ring>(device, slot_bytes)).first;
     return *it->second;
 }
 
@@ -268,7 +275,8 @@ struct host_pipeline {
     // r = 1..R-1, UNPACK(R-1), "|" alternating group by group
     std::vector<group> groups;
     int rounds = 1;
-    int rounds_before = 0;            // exchange rounds issued before the first group
+    size_t slot_bytes = 0;            // ring slot the largest package needs (<= kSlot)
+    int rounds_before = 0;           // exchange rounds issued before the first group
     std::vector<int> rounds_after;    // ... issued once group t is enqueued (cumulative)
     void* d_ops = nullptr;   // every group's ordered device ops (package offsets)
     void* d_work = nullptr;
@@ -406,6 +414,11 @@ std::shared_ptr<host_pipeline> make_host_pipeline(costa_dtype_t dtype,
         interleave(built[{int(hpl::PACK), r}], built[{int(hpl::UNPACK), r - 1}]);
     std::vector<hpl::group> none;
     interleave(built[{int(hpl::UNPACK), rounds - 1}], none);
+    // ring slot: the largest package, in 2 MiB steps
+    for (const auto& gr : hp->groups)
+        hp->slot_bytes = std::max(hp->slot_bytes, std::max(gr.in_bytes, gr.out_bytes));
+    const size_t step = size_t(2) << 20;
+    hp->slot_bytes = std::min(kSlot, std::max(step, (hp->slot_bytes + step - 1) / step * step));
     // round r of the exchange is issued once every pack group of rounds <= r is enqueued
     std::vector<int> last_pack(size_t(rounds), -1);
     for (size_t t = 0; t < hp->groups.size(); ++t)
@@ -486,7 +499,8 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
                        char* send_buf, char* recv_buf,
                        const std::function<void(void*, int)>& exchange, const void* d_scalars) {
     using hpl = host_pipeline;
-    ring& R = ring_of(device);
+    ring& R = ring_of(device, hp.slot_bytes);
+    const size_t S = R.slot;
     hipStream_t comp = static_cast<hipStream_t>(compute_stream);
     hipStream_t xs = static_cast<hipStream_t>(exchange_stream);
     pool& P = thread_pool();
@@ -553,7 +567,7 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
                 target_shape(h.op, run, runs);
                 const size_t rb = size_t(run) * E;
                 const char* src = reinterpret_cast<const char*>(h.op.dst);
-                char* dst = pin + kSlot + h.out_off;
+                char* dst = pin + S + h.out_off;
                 for (int64_t r = it.lo; r < it.hi; ++r)
                     copy_nt(dst + size_t(r) * rb, src + size_t(r) * size_t(h.op.ldd) * E, rb);
             } else {  // dense target package -> the caller's C
@@ -584,8 +598,8 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
         const hpl::group* o = t >= size_t(kLag) ? &hp.groups[t - kLag] : nullptr;
         if (o && o->kind == hpl::PACK) o = nullptr;  // nothing comes back from a pack group
         const int ko = int((t + kRing - kLag) % kRing);  // slot of group t - kLag
-        char* pin = R.pin_in + size_t(k) * 2 * kSlot;
-        char* dev = R.dev + size_t(k) * 2 * kSlot;
+        char* pin = R.pin_in + size_t(k) * 2 * S;
+        char* dev = R.dev + size_t(k) * 2 * S;
         double t0 = now();
         // the pinned source slot is free once its previous upload has landed
         if (g) HP_CHECK(hipEventSynchronize(R.up_done[k]));
@@ -593,7 +607,7 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
         // group t - kLag's target package has landed in its pinned slot
         if (o) HP_CHECK(hipEventSynchronize(R.down_done[ko]));
         double t2 = now();
-        host_step(g, pin, o, R.pin_out + size_t(ko) * kSlot);
+        host_step(g, pin, o, R.pin_out + size_t(ko) * S);
         double t3 = now();
         t_wait_up += t1 - t0;
         t_wait_down += t2 - t1;
@@ -618,7 +632,7 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
             if (prof && !up0) up0 = ev(R.up);
             if (g->in_bytes) HP_CHECK(hipMemcpyAsync(dev, pin, g->in_bytes, hipMemcpyHostToDevice, R.up));
             if (g->reads_old)
-                HP_CHECK(hipMemcpyAsync(dev + kSlot, pin + kSlot, g->out_bytes, hipMemcpyHostToDevice,
+                HP_CHECK(hipMemcpyAsync(dev + S, pin + S, g->out_bytes, hipMemcpyHostToDevice,
                                         R.up));
             if (prof) up1 = ev(R.up);
         }
@@ -629,7 +643,7 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
         launch_tiles(hp.dtype,
                      make_launch(g->split, static_cast<const costa_tile_op_t*>(hp.d_ops) + g->ord_first,
                                  static_cast<const uint64_t*>(hp.d_work) + g->work_first,
-                                 unpack ? recv_buf : dev, dev + kSlot, d_scalars, g->any_tr,
+                                 unpack ? recv_buf : dev, dev + S, d_scalars, g->any_tr,
                                  g->reads_old),
                      comp);
         if (prof) kern_t.push_back({k0, ev(comp), unpack});
@@ -638,7 +652,7 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
         // t - kRing + kLag < t
         HP_CHECK(hipStreamWaitEvent(R.down, R.kern_done[k], 0));
         if (prof && !dn0) dn0 = ev(R.down);
-        HP_CHECK(hipMemcpyAsync(R.pin_out + size_t(k) * kSlot, dev + kSlot, g->out_bytes,
+        HP_CHECK(hipMemcpyAsync(R.pin_out + size_t(k) * S, dev + S, g->out_bytes,
                                 hipMemcpyDeviceToHost, R.down));
         HP_CHECK(hipEventRecord(R.down_done[k], R.down));
         if (prof) dn1 = ev(R.down);
@@ -650,7 +664,7 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
         std::fprintf(stderr,
                      "[costa host pipe] groups %zu, %d exchange round(s), slot %zu MiB threads %d: "
                      "total %.2f ms, copies %.2f, wait-up %.2f, wait-down %.2f, issue %.2f\n",
-                     G, exchange ? hp.rounds : 0, kSlot >> 20, host_threads(), (now() - t_begin) * 1e3,
+                     G, exchange ? hp.rounds : 0, S >> 20, host_threads(), (now() - t_begin) * 1e3,
                      t_copy * 1e3, t_wait_up * 1e3, t_wait_down * 1e3, t_issue * 1e3);
     HP_CHECK(hipStreamSynchronize(R.up));
     HP_CHECK(hipStreamSynchronize(xs));
