@@ -318,11 +318,26 @@ def main():
         costa.set_profiling(False)
         return el, st
 
-    # first call on these layouts: host planning + descriptor upload + kernels (plan-cache miss)
+    # first call on these layouts: planning + descriptor upload + kernels (plan-cache miss)
+    costa.get_stats(reset=True)
     barrier()
     t0 = time.perf_counter()
     step_blocking()
     first_call_ms = max_over_ranks(time.perf_counter() - t0) * 1e3
+    st0 = costa.get_stats(reset=True)
+    planning = {"planner": "device" if st0["device_plans"] else "host",
+                "plan_ms": round(st0["plan_ms"], 2)}
+    if world == 1:  # warm plan-cache misses with each planner (the first call pays one-time costs)
+        for mode, key in ((1, "default"), (0, "host"), (2, "device")):
+            costa.set_planner(mode)
+            costa.release_caches()
+            t0 = time.perf_counter()
+            step_blocking()
+            sm = costa.get_stats(reset=True)
+            planning[key] = {"call_ms": round((time.perf_counter() - t0) * 1e3, 2),
+                             "plan_ms": round(sm["plan_ms"], 2),
+                             "planner": "device" if sm["device_plans"] else "host"}
+        costa.set_planner(1)
     repeatable = args.workload != "cfg4"  # beta != 0: only the first call's result is known
     if world == 1 and check and not repeatable:
         check()
@@ -457,6 +472,7 @@ def main():
             "e2e_host": e2e,
             "call_overhead_us": overhead_us,
             "first_call_ms": round(first_call_ms, 2),  # plan-cache miss: planning + upload + kernels
+            "planning": planning,
             "blocking": {"ms_per_step": round(el_block / args.steps * 1e3, 4),
                          "GBps": round(total_bytes / el_block / 1e9, 2),
                          "note": "costa_hip_transform (reference semantics: host waits for C)"},

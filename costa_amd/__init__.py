@@ -96,7 +96,8 @@ class Stats(C.Structure):
                 ("unpack_launches", C.c_int64), ("pack_bytes", C.c_int64),
                 ("local_bytes", C.c_int64), ("unpack_bytes", C.c_int64),
                 ("transforms", C.c_int64), ("plan_hits", C.c_int64),
-                ("plan_misses", C.c_int64), ("host_groups", C.c_int64)]
+                ("plan_misses", C.c_int64), ("host_groups", C.c_int64),
+                ("device_plans", C.c_int64), ("plan_ms", C.c_double)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -153,6 +154,10 @@ def lib():
         "costa_hip_get_stats": (i, [C.POINTER(Stats), i]),
         "costa_hip_release_caches": (i, []),
         "costa_hip_set_host_staging": (i, [i]),
+        "costa_hip_set_planner": (i, [i]),
+        "costa_hip_plan_export_device": (i, [i, i, C.POINTER(vp), C.POINTER(vp), C.c_char_p, vp, vp,
+                                             i, i, C.POINTER(PlanInfo), vp, vp, vp, vp, vp, vp, vp,
+                                             vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -444,8 +449,9 @@ class Plan:
 
 
 def plan_export(As: Sequence[Layout], Cs: Sequence[Layout], rank: int, nranks: int,
-                trans=None, alpha=None, beta=None) -> Plan:
-    """Tile-op lists of `rank` (host only; never touches a GPU)."""
+                trans=None, alpha=None, beta=None, device=None) -> Plan:
+    """Tile-op lists of `rank`: by the host planner (never touches a GPU), or with ``device``
+    set by the GPU planner of that device (costa_hip_plan_export_device)."""
     n = len(As)
     code = As[0].dtype
     trans = list(trans) if trans is not None else ["N"] * n
@@ -458,16 +464,21 @@ def plan_export(As: Sequence[Layout], Cs: Sequence[Layout], rank: int, nranks: i
     tb = "".join(trans).encode()
     info = PlanInfo()
     L = lib()
-    _check(L.costa_hip_plan_export(n, a, c, tb, ab, bb, rank, nranks, C.byref(info), None, None,
-                                   None, None, None, None, None, None))
+    if device is None:
+        export = L.costa_hip_plan_export
+    else:
+        def export(*args):
+            return L.costa_hip_plan_export_device(int(device), *args)
+    _check(export(n, a, c, tb, ab, bb, rank, nranks, C.byref(info), None, None,
+                  None, None, None, None, None, None))
     lo = np.zeros(info.n_local, TILE_OP_DTYPE)
     po = np.zeros(info.n_pack, TILE_OP_DTYPE)
     uo = np.zeros(info.n_unpack, TILE_OP_DTYPE)
     cnt = [np.zeros(nranks, np.int64) for _ in range(4)]
     sc = np.zeros(2 * info.n_slots, _NP[code])
-    _check(L.costa_hip_plan_export(n, a, c, tb, ab, bb, rank, nranks, C.byref(info),
-                                   lo.ctypes.data, po.ctypes.data, uo.ctypes.data,
-                                   *[x.ctypes.data for x in cnt], sc.ctypes.data))
+    _check(export(n, a, c, tb, ab, bb, rank, nranks, C.byref(info),
+                  lo.ctypes.data, po.ctypes.data, uo.ctypes.data,
+                  *[x.ctypes.data for x in cnt], sc.ctypes.data))
     return Plan(lo, po, uo, *cnt, sc, info.send_elems, info.recv_elems, info.local_elems)
 
 
@@ -484,6 +495,12 @@ def get_stats(reset: bool = False) -> dict:
 
 def release_caches():
     _check(lib().costa_hip_release_caches())
+
+
+def set_planner(mode: int):
+    """Planner of plan-cache misses: 1 = the GPU for layout pairs of >= 4096 blocks (default),
+    0 = always the host, 2 = the GPU wherever it applies (costa_hip_set_planner)."""
+    _check(lib().costa_hip_set_planner(int(mode)))
 
 
 def set_host_staging(mode: int):

@@ -87,6 +87,50 @@ std::vector<job> make_jobs(int n, const costa_layout_t* A, const costa_layout_t*
 }
 }  // namespace
 
+namespace {
+// one plan (from `make`) copied out as costa_hip_plan_export documents
+template <typename F>
+int export_plan(F make, int n, const costa_layout_t* A, const costa_layout_t* C, const char* trans,
+                const void* alpha, const void* beta, int rank, int nranks, costa_plan_info_t* info,
+                costa_tile_op_t* local_ops, costa_tile_op_t* pack_ops, costa_tile_op_t* unpack_ops,
+                int64_t* send_counts, int64_t* send_displs, int64_t* recv_counts,
+                int64_t* recv_displs, void* scalars) {
+    return guarded([&] {
+        if (!info || !alpha || !beta) throw costa::engine::error(COSTA_ERR_ARG, "null argument");
+        if (nranks < 1 || rank < 0 || rank >= nranks)
+            throw costa::engine::error(COSTA_ERR_ARG, "bad rank/size");
+        auto jobs = make_jobs(n, A, C, trans, alpha, beta);
+        std::unique_ptr<costa::engine::plan> p = make(jobs);
+        info->n_local = int64_t(p->local_ops.size());
+        info->n_pack = int64_t(p->pack_ops.size());
+        info->n_unpack = int64_t(p->unpack_ops.size());
+        info->send_elems = p->send_elems;
+        info->recv_elems = p->recv_elems;
+        info->local_elems = p->local_elems;
+        info->n_ranks = nranks;
+        info->n_slots = int32_t(p->slots.size());
+        auto cp = [](const auto& v, auto* dst) {
+            if (dst && !v.empty()) std::memcpy(dst, v.data(), v.size() * sizeof(v[0]));
+        };
+        cp(p->local_ops, local_ops);
+        cp(p->pack_ops, pack_ops);
+        cp(p->unpack_ops, unpack_ops);
+        cp(p->send_counts, send_counts);
+        cp(p->send_displs, send_displs);
+        cp(p->recv_counts, recv_counts);
+        cp(p->recv_displs, recv_displs);
+        if (scalars) {
+            const size_t E = dtype_size(p->dtype);
+            auto* out = static_cast<unsigned char*>(scalars);
+            for (size_t t = 0; t < p->slots.size(); ++t) {
+                std::memcpy(out + (2 * t) * E, p->slots[t].alpha.data(), E);
+                std::memcpy(out + (2 * t + 1) * E, p->slots[t].beta.data(), E);
+            }
+        }
+    });
+}
+}  // namespace
+
 extern "C" {
 
 const char* costa_hip_last_error(void) { return g_last_error.c_str(); }
@@ -256,38 +300,36 @@ int costa_hip_plan_export(int n, const costa_layout_t* A, const costa_layout_t* 
                           costa_tile_op_t* pack_ops, costa_tile_op_t* unpack_ops,
                           int64_t* send_counts, int64_t* send_displs, int64_t* recv_counts,
                           int64_t* recv_displs, void* scalars) {
+    return export_plan(
+        [&](const std::vector<job>& jobs) { return costa::engine::make_plan(jobs, rank, nranks); },
+        n, A, C, trans, alpha, beta, rank, nranks, info, local_ops, pack_ops, unpack_ops,
+        send_counts, send_displs, recv_counts, recv_displs, scalars);
+}
+
+int costa_hip_plan_export_device(int device, int n, const costa_layout_t* A, const costa_layout_t* C,
+                                 const char* trans, const void* alpha, const void* beta, int rank,
+                                 int nranks, costa_plan_info_t* info, costa_tile_op_t* local_ops,
+                                 costa_tile_op_t* pack_ops, costa_tile_op_t* unpack_ops,
+                                 int64_t* send_counts, int64_t* send_displs, int64_t* recv_counts,
+                                 int64_t* recv_displs, void* scalars) {
+    return export_plan(
+        [&](const std::vector<job>& jobs) {
+            auto p = costa::engine::make_plan_device(jobs, rank, nranks, 0, device, nullptr);
+            if (!p)
+                throw costa::engine::error(COSTA_ERR_ARG,
+                                           "costa: the device planner does not apply to these "
+                                           "layouts (local blocks are not exactly the rank's grid "
+                                           "cells)");
+            return p;
+        },
+        n, A, C, trans, alpha, beta, rank, nranks, info, local_ops, pack_ops, unpack_ops,
+        send_counts, send_displs, recv_counts, recv_displs, scalars);
+}
+
+int costa_hip_set_planner(int mode) {
     return guarded([&] {
-        if (!info || !alpha || !beta) throw costa::engine::error(COSTA_ERR_ARG, "null argument");
-        if (nranks < 1 || rank < 0 || rank >= nranks)
-            throw costa::engine::error(COSTA_ERR_ARG, "bad rank/size");
-        auto jobs = make_jobs(n, A, C, trans, alpha, beta);
-        auto p = costa::engine::make_plan(jobs, rank, nranks);
-        info->n_local = int64_t(p->local_ops.size());
-        info->n_pack = int64_t(p->pack_ops.size());
-        info->n_unpack = int64_t(p->unpack_ops.size());
-        info->send_elems = p->send_elems;
-        info->recv_elems = p->recv_elems;
-        info->local_elems = p->local_elems;
-        info->n_ranks = nranks;
-        info->n_slots = int32_t(p->slots.size());
-        auto cp = [](const auto& v, auto* dst) {
-            if (dst && !v.empty()) std::memcpy(dst, v.data(), v.size() * sizeof(v[0]));
-        };
-        cp(p->local_ops, local_ops);
-        cp(p->pack_ops, pack_ops);
-        cp(p->unpack_ops, unpack_ops);
-        cp(p->send_counts, send_counts);
-        cp(p->send_displs, send_displs);
-        cp(p->recv_counts, recv_counts);
-        cp(p->recv_displs, recv_displs);
-        if (scalars) {
-            const size_t E = dtype_size(p->dtype);
-            auto* out = static_cast<unsigned char*>(scalars);
-            for (size_t t = 0; t < p->slots.size(); ++t) {
-                std::memcpy(out + (2 * t) * E, p->slots[t].alpha.data(), E);
-                std::memcpy(out + (2 * t + 1) * E, p->slots[t].beta.data(), E);
-            }
-        }
+        if (mode < 0 || mode > 2) throw costa::engine::error(COSTA_ERR_ARG, "mode must be 0, 1 or 2");
+        costa::engine::set_planner_mode(mode);
     });
 }
 

@@ -617,6 +617,44 @@ std::vector<hrange> collect_ranges(const std::vector<const elayout*>& Ls) {
     return m;
 }
 
+}  // namespace
+
+// ---------------------------------------------------------------- planner choice
+namespace {
+int g_planner = -1;                         // costa_hip_set_planner / COSTA_PLANNER
+constexpr size_t kDevicePlanBlocks = 4096;  // smaller layout pairs plan on the host
+}  // namespace
+
+int planner_mode() {
+    if (g_planner < 0) {
+        const char* s = std::getenv("COSTA_PLANNER");
+        g_planner = s ? std::max(0, std::min(2, std::atoi(s))) : 1;
+    }
+    return g_planner;
+}
+
+void set_planner_mode(int mode) {
+    std::lock_guard<std::recursive_mutex> lk(g_mutex);
+    g_planner = mode;
+}
+
+namespace {
+// the plan of a cache miss, built on the GPU when the planner mode asks for it and the layouts
+// allow it (make_plan_device), else on the host; both give the same plan
+std::unique_ptr<plan> plan_jobs(const std::vector<job>& jobs, comm* c, hipStream_t s) {
+    const int lb = c->size == 1 && c->nccl ? loopback_exchange() : 0;
+    const int mode = planner_mode();
+    size_t blocks = 0;
+    for (const job& j : jobs) blocks += j.A->blocks.size() + j.C->blocks.size();
+    if (mode == 2 || (mode == 1 && blocks >= kDevicePlanBlocks)) {
+        if (auto p = make_plan_device(jobs, c->rank, c->size, lb, c->device, s)) {
+            g_stats.device_plans++;
+            return p;
+        }
+    }
+    return make_plan(jobs, c->rank, c->size, lb);
+}
+
 cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
     hasher h;
     h.mix(uint64_t(c->rank));
@@ -719,8 +757,9 @@ cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
         for (uint8_t f : range_flags)
             if ((f & 3) == 3 || (f & 4)) pipe_ok = false;
         if (pipe_ok) {
-            auto hplan = make_plan(jobs, c->rank, c->size,  // host addresses
-                                   c->size == 1 && c->nccl ? loopback_exchange() : 0);
+            const double tp = now();
+            auto hplan = plan_jobs(jobs, c, dc.main);  // host addresses
+            g_stats.plan_ms += now() - tp;
             if (host_pipeline_accepts(hplan->dtype, hplan->pack_ops)) {
                 cp->staged = false;
                 cp->p = std::move(hplan);
@@ -750,9 +789,10 @@ cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
         }
     }
     t_resid = now() - t0;
-    cp->p = make_plan(pj, c->rank, c->size, c->size == 1 && c->nccl ? loopback_exchange() : 0);
+    cp->p = plan_jobs(pj, c, dc.main);
     const plan& p = *cp->p;
     t_plan = now() - t0 - t_resid;
+    g_stats.plan_ms += t_plan;
     if (cp->staged) {
         // A C-only range needs no upload when the kernels overwrite every byte of it: one job's
         // C blocks only, no op reading C (beta = 0), and the ops' writes (disjoint: each C

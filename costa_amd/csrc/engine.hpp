@@ -76,12 +76,29 @@ struct plan {
     int64_t local_bytes = 0, pack_bytes = 0, unpack_bytes = 0;
 };
 
+// per-job transform parameters, validated as the reference's transform does (plan.cpp)
+struct job_params {
+    bool transpose, conj, a_cm, c_cm;
+    uint32_t kind_copy, kind_tr;  // scale kind of ops that copy / transpose
+};
+std::vector<job_params> check_jobs(const std::vector<job>& jobs, int n_ranks, costa_dtype_t& dtype);
+
 // Build the plan of `rank` (of `n_ranks`) for a batch of jobs (host only).  `loopback` (test
 // mode, see loopback_exchange()): 1 = the rank's own tiles all go through pack -> exchange with
 // itself -> unpack instead of the local list; 2 = half of them (by a parity of their target
 // coordinates, the same on both sides), the rest stays local.
 std::unique_ptr<plan> make_plan(const std::vector<job>& jobs, int rank, int n_ranks,
                                 int loopback = 0);
+
+// The same plan built on the GPU (device_plan.hip, on `stream` of `device`): identical op lists,
+// order and exchange geometry.  nullptr when it does not apply (local blocks that are not exactly
+// the rank's grid cells, grids not starting at the same index, more than 2^32 merged cells).
+std::unique_ptr<plan> make_plan_device(const std::vector<job>& jobs, int rank, int n_ranks,
+                                       int loopback, int device, void* stream);
+// planner of plan-cache misses (costa_hip_set_planner, COSTA_PLANNER): 0 host, 1 the GPU for
+// layout pairs of at least 4096 blocks (default), 2 the GPU wherever it applies
+int planner_mode();
+void set_planner_mode(int mode);
 
 // COSTA_LOOPBACK=1 or 2 (test only): a one-rank communicator gets a one-rank RCCL communicator
 // and its transforms route tiles through PACK -> ncclSend/ncclRecv to itself -> UNPACK (all of

@@ -15,6 +15,7 @@
 // The cover is found by binary search instead of the reference's merged linear scan;
 // the resulting tile set and order are identical.
 #include "engine.hpp"
+#include "tile_op.hpp"
 
 #include <algorithm>
 #include <cctype>
@@ -150,12 +151,11 @@ void decompose(const view& sv, const view& dv, int tag, size_t elem, std::vector
                 const interval r(std::max(vr.start, drs[i]), std::min(vr.end, drs[i + 1]));
                 if (r.empty()) continue;
                 // back to the stored orientation of the block (block.cpp:85-99)
-                const interval sr = sv.t ? c : r;
-                const interval sc = sv.t ? r : c;
-                const int64_t dr = sr.start - b.rows.start, dc = sc.start - b.cols.start;
-                const int64_t off = row_major ? dr * b.ld + dc : dc * b.ld + dr;
-                out.push_back({dv.owner(i, j), tag, r, c, b.data + off * int64_t(elem), b.ld,
-                               sr.length(), sc.length()});
+                const tile_side ts = sub_tile(reinterpret_cast<uint64_t>(b.data), b.ld, b.rows.start,
+                                              b.cols.start, row_major, sv.t, r.start, r.end,
+                                              c.start, c.end, elem);
+                out.push_back({dv.owner(i, j), tag, r, c, reinterpret_cast<char*>(ts.ptr), b.ld,
+                               ts.n_rows, ts.n_cols});
             }
         }
     }
@@ -196,57 +196,18 @@ uint32_t scale_kind(costa_dtype_t dtype, const scal& s, bool copy_mode, bool con
 costa_tile_op_t make_tile_op(int n_rows, int n_cols, uint64_t src, int src_stride, bool src_cm,
                              uint64_t dst, int dst_stride, bool dst_cm, bool transpose, bool conj,
                              uint32_t kind, uint32_t slot, size_t elem) {
-    // ordering mismatch is itself a transpose and cancels an explicit one
-    // (memory_utils.hpp:353-367)
-    const bool will_transpose = (transpose && src_cm == dst_cm) || (!transpose && src_cm != dst_cm);
-    // default strides (memory_utils.hpp:330-337, 370-381)
-    if (dst_stride == 0) {
-        int r = will_transpose ? n_cols : n_rows, c = will_transpose ? n_rows : n_cols;
-        dst_stride = dst_cm ? r : c;
-    }
-    if (src_stride == 0) src_stride = src_cm ? n_rows : n_cols;
-    costa_tile_op_t op{};
-    op.src = src;
-    op.dst = dst;
-    op.nf = src_cm ? n_rows : n_cols;  // contiguous extent of the source
-    op.ns = src_cm ? n_cols : n_rows;
-    op.lds = src_stride;
-    op.ldd = dst_stride;
-    if (will_transpose && kind == COSTA_SCALE_BITCOPY) kind = COSTA_SCALE_ALPHA;  // never memcpy
-    op.flags = (will_transpose ? COSTA_TILE_TRANSPOSE : 0u) | (conj ? COSTA_TILE_CONJ : 0u) |
-               (kind << COSTA_SCALE_SHIFT) | (slot << COSTA_SLOT_SHIFT);
-    if (src % 16 == 0 && (uint64_t(src_stride) * elem) % 16 == 0) op.flags |= COSTA_TILE_VEC_SRC;
-    if (dst % 16 == 0 && (uint64_t(dst_stride) * elem) % 16 == 0) op.flags |= COSTA_TILE_VEC_DST;
-    return op;
+    return tile_op(n_rows, n_cols, src, src_stride, src_cm, dst, dst_stride, dst_cm, transpose, conj,
+                   kind, slot, elem);
 }
 
-std::unique_ptr<plan> make_plan(const std::vector<job>& jobs, int rank, int n_ranks,
-                                int loopback) {
-    // loopback test mode: which of the rank's own tiles stay local
-    auto stays_local = [&](const side_tile& m) {
-        if (m.peer != rank) return false;
-        if (loopback == 1) return false;
-        if (loopback == 2) return ((m.rows.start / 7 + m.cols.start / 5) & 1) == 0;
-        return true;
-    };
+std::vector<job_params> check_jobs(const std::vector<job>& jobs, int n_ranks, costa_dtype_t& dtype) {
     if (jobs.empty()) throw error(COSTA_ERR_ARG, "costa::transform: nothing scheduled");
     if (jobs.size() > 0xFFFF) throw error(COSTA_ERR_ARG, "costa::transform: too many layout pairs");
-    auto p = std::make_unique<plan>();
-    p->dtype = jobs[0].A->dtype;
-    p->rank = rank;
-    p->n_ranks = n_ranks;
-    const size_t E = dtype_size(p->dtype);
-    const bool cplx = dtype_is_complex(p->dtype);
-
-    struct tag_info {
-        bool transpose, conj, a_cm, c_cm;
-        uint32_t kind_copy, kind_tr;
-    };
-    std::vector<tag_info> tags;
-    std::vector<side_tile> send, recv;
-    for (size_t t = 0; t < jobs.size(); ++t) {
-        const job& jb = jobs[t];
-        if (jb.A->dtype != p->dtype || jb.C->dtype != p->dtype)
+    dtype = jobs[0].A->dtype;
+    const bool cplx = dtype_is_complex(dtype);
+    std::vector<job_params> out;
+    for (const job& jb : jobs) {
+        if (jb.A->dtype != dtype || jb.C->dtype != dtype)
             throw error(COSTA_ERR_ARG, "costa::transform: all layouts must share one element type");
         for (const elayout* L : {jb.A, jb.C})
             for (int o : L->owners)
@@ -258,10 +219,29 @@ std::unique_ptr<plan> make_plan(const std::vector<job>& jobs, int rank, int n_ra
             throw error(COSTA_ERR_ARG, "costa::transform: trans must be 'N', 'T' or 'C'");
         const bool tr = op != 'N';            // utils.cpp:9 (if_should_transpose)
         const bool cj = op == 'C' && cplx;    // communication_data.cpp:31-33
-        tags.push_back({tr, cj, jb.A->ordering == 'C', jb.C->ordering == 'C',
-                        scale_kind(p->dtype, jb.s, true, cj), scale_kind(p->dtype, jb.s, false, cj)});
-        p->slots.push_back(jb.s);
+        out.push_back({tr, cj, jb.A->ordering == 'C', jb.C->ordering == 'C',
+                       scale_kind(dtype, jb.s, true, cj), scale_kind(dtype, jb.s, false, cj)});
     }
+    return out;
+}
+
+std::unique_ptr<plan> make_plan(const std::vector<job>& jobs, int rank, int n_ranks,
+                                int loopback) {
+    // loopback test mode: which of the rank's own tiles stay local
+    auto stays_local = [&](const side_tile& m) {
+        if (m.peer != rank) return false;
+        if (loopback == 1) return false;
+        if (loopback == 2) return ((m.rows.start / 7 + m.cols.start / 5) & 1) == 0;
+        return true;
+    };
+    auto p = std::make_unique<plan>();
+    p->rank = rank;
+    p->n_ranks = n_ranks;
+    using tag_info = job_params;
+    const std::vector<tag_info> tags = check_jobs(jobs, n_ranks, p->dtype);
+    const size_t E = dtype_size(p->dtype);
+    std::vector<side_tile> send, recv;
+    for (const job& jb : jobs) p->slots.push_back(jb.s);
     // prepare_to_send and prepare_to_recv are independent: the receive side runs on a second
     // thread when there are enough blocks to pay for it
     auto side = [&](bool send_side, std::vector<side_tile>& out) {
@@ -310,11 +290,7 @@ std::unique_ptr<plan> make_plan(const std::vector<job>& jobs, int rank, int n_ra
     auto will_tr = [](const tag_info& ti, bool src_cm, bool dst_cm) {
         return (ti.transpose && src_cm == dst_cm) || (!ti.transpose && src_cm != dst_cm);
     };
-    auto op_bytes = [&](const costa_tile_op_t& op) {
-        const uint32_t k = (op.flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT;
-        const int64_t n = int64_t(op.nf) * op.ns;
-        return int64_t(E) * n * (1 + (k != COSTA_SCALE_ZERO) + (k == COSTA_SCALE_AXPBY));
-    };
+    auto op_bytes = [&](const costa_tile_op_t& op) { return op_alg_bytes(op, E); };
 
     // target coordinates of every op, for the locality hint (costa_tile_op_t::order)
     std::vector<const side_tile*> at_pack, at_unpack, at_local;

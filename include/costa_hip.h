@@ -205,6 +205,8 @@ typedef struct {
     int64_t transforms;
     int64_t plan_hits, plan_misses;
     int64_t host_groups; /* tile groups moved by the pipelined host staging */
+    int64_t device_plans; /* plan-cache misses planned on the GPU (costa_hip_set_planner) */
+    double plan_ms;       /* host wall time spent building plans (cache misses) */
 } costa_stats_t;
 int costa_hip_set_profiling(int on);
 int costa_hip_get_stats(costa_stats_t* out, int reset);
@@ -221,6 +223,22 @@ int costa_hip_release_caches(void);
  * the kernels run on the mirror, the target ranges are copied back.  Mode 1 falls back to 0
  * for in-place layouts and target ranges shared by two batched jobs.  Results are identical. */
 int costa_hip_set_host_staging(int mode);
+
+/* Planner of plan-cache misses (the reference plans on the host at every call, utils.hpp:87-206,
+ * communication_data.cpp:67-164).  1 (default): layout pairs of at least 4096 blocks are planned
+ * on the GPU -- one thread per cell of the merged grid of the two layouts, a stable radix sort by
+ * peer for the message order, scans for the package offsets; 0: always on the host; 2: on the GPU
+ * wherever it applies.  The op lists are identical either way.  Layouts whose local blocks are
+ * not exactly the rank's grid cells are planned on the host in every mode. */
+int costa_hip_set_planner(int mode);
+/* costa_hip_plan_export through the GPU planner of `device` (COSTA_ERR_ARG when it does not
+ * apply to these layouts) */
+int costa_hip_plan_export_device(int device, int n, const costa_layout_t* A, const costa_layout_t* C,
+                                 const char* trans, const void* alpha, const void* beta, int rank,
+                                 int nranks, costa_plan_info_t* info, costa_tile_op_t* local_ops,
+                                 costa_tile_op_t* pack_ops, costa_tile_op_t* unpack_ops,
+                                 int64_t* send_counts, int64_t* send_displs, int64_t* recv_counts,
+                                 int64_t* recv_displs, void* scalars);
 
 #ifdef __cplusplus
 }

@@ -14,9 +14,11 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("mode,slot", [("1", None), ("2", None), ("2", "1")])
-def test_loopback_exchange_matches_golden(mode, slot):
-    """slot "1": 1 MiB host pipeline slots (many groups, ops cut into pieces)"""
+@pytest.mark.parametrize("mode,slot,planner", [("1", None, None), ("2", None, None),
+                                               ("2", "1", None), ("1", None, "2")])
+def test_loopback_exchange_matches_golden(mode, slot, planner):
+    """slot "1": 1 MiB host pipeline slots (many groups, ops cut into pieces); planner "2": every
+    plan (pack / unpack lists, package geometry) built by the device planner"""
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -24,6 +26,8 @@ def test_loopback_exchange_matches_golden(mode, slot):
     env = dict(os.environ, COSTA_LOOPBACK=mode)
     if slot:
         env["COSTA_HOST_SLOT_MIB"] = slot
+    if planner:
+        env["COSTA_PLANNER"] = planner
     r = subprocess.run([sys.executable, child], env=env, capture_output=True, text=True,
                        timeout=600)
     out = r.stdout.strip().splitlines()
