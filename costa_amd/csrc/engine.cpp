@@ -404,7 +404,18 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     const bool hinted = std::any_of(tiny.begin(), tiny.end(),
                                     [](const costa_tile_op_t& o) { return o.order != 0; });
     const int mode = kn.sort == 3 && !hinted ? 2 : kn.sort;
-    if (mode >= 1 && mode <= 3) {  // sort (key, index) pairs: stable, and cheap to move
+    uint32_t top = 0;  // largest hint
+    if (mode == 3)
+        for (const auto& o : tiny) top = std::max(top, o.order);
+    if (mode == 3 && size_t(top) <= 4 * tiny.size() + 1024) {
+        // the planner's hints are ranks within the list: a stable counting sort
+        std::vector<uint32_t> at(size_t(top) + 2, 0);
+        for (const auto& o : tiny) ++at[size_t(o.order) + 1];
+        for (size_t k = 1; k < at.size(); ++k) at[k] += at[k - 1];
+        std::vector<costa_tile_op_t> sorted(tiny.size());
+        for (const auto& o : tiny) sorted[at[o.order]++] = o;
+        tiny.swap(sorted);
+    } else if (mode >= 1 && mode <= 3) {  // sort (key, index) pairs: stable, and cheap to move
         std::vector<std::pair<uint64_t, uint32_t>> key(tiny.size());
         for (size_t i = 0; i < tiny.size(); ++i)
             key[i] = {mode == 1 ? tiny[i].src : mode == 2 ? tiny[i].dst : tiny[i].order,
