@@ -498,7 +498,8 @@ def release_caches():
 
 
 def set_planner(mode: int):
-    """Planner of plan-cache misses: 1 = the GPU for layout pairs of >= 4096 blocks (default),
+    """Planner of plan-cache misses: 1 = the GPU for layout pairs of >= 4096 blocks (>= 100000
+    before the first GPU plan of the process, which loads the planner's kernels; default),
     0 = always the host, 2 = the GPU wherever it applies (costa_hip_set_planner)."""
     _check(lib().costa_hip_set_planner(int(mode)))
 

@@ -634,6 +634,10 @@ std::vector<hrange> collect_ranges(const std::vector<const elayout*>& Ls) {
 namespace {
 int g_planner = -1;                         // costa_hip_set_planner / COSTA_PLANNER
 constexpr size_t kDevicePlanBlocks = 4096;  // smaller layout pairs plan on the host
+// The first GPU plan of a process loads the planner's kernels (about 15 ms on MI355X); before
+// that, only layout pairs whose host planning costs as much go to the GPU.
+constexpr size_t kColdDevicePlanBlocks = 100000;
+bool g_device_planner_warm = false;
 }  // namespace
 
 int planner_mode() {
@@ -657,9 +661,11 @@ std::unique_ptr<plan> plan_jobs(const std::vector<job>& jobs, comm* c, hipStream
     const int mode = planner_mode();
     size_t blocks = 0;
     for (const job& j : jobs) blocks += j.A->blocks.size() + j.C->blocks.size();
-    if (mode == 2 || (mode == 1 && blocks >= kDevicePlanBlocks)) {
+    const size_t need = g_device_planner_warm ? kDevicePlanBlocks : kColdDevicePlanBlocks;
+    if (mode == 2 || (mode == 1 && blocks >= need)) {
         if (auto p = make_plan_device(jobs, c->rank, c->size, lb, c->device, s)) {
             g_stats.device_plans++;
+            g_device_planner_warm = true;
             return p;
         }
     }

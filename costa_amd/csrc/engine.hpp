@@ -96,7 +96,8 @@ std::unique_ptr<plan> make_plan(const std::vector<job>& jobs, int rank, int n_ra
 std::unique_ptr<plan> make_plan_device(const std::vector<job>& jobs, int rank, int n_ranks,
                                        int loopback, int device, void* stream);
 // planner of plan-cache misses (costa_hip_set_planner, COSTA_PLANNER): 0 host, 1 the GPU for
-// layout pairs of at least 4096 blocks (default), 2 the GPU wherever it applies
+// layout pairs of at least 4096 blocks, 100000 before the first GPU plan of the process (default),
+// 2 the GPU wherever it applies
 int planner_mode();
 void set_planner_mode(int mode);
 

@@ -226,7 +226,8 @@ int costa_hip_set_host_staging(int mode);
 
 /* Planner of plan-cache misses (the reference plans on the host at every call, utils.hpp:87-206,
  * communication_data.cpp:67-164).  1 (default): layout pairs of at least 4096 blocks are planned
- * on the GPU -- one thread per cell of the merged grid of the two layouts, a stable radix sort by
+ * on the GPU (100000 before the first GPU plan of the process, which loads the planner's kernels)
+ * -- one thread per cell of the merged grid of the two layouts, a stable radix sort by
  * peer for the message order, scans for the package offsets; 0: always on the host; 2: on the GPU
  * wherever it applies.  The op lists are identical either way.  Layouts whose local blocks are
  * not exactly the rank's grid cells are planned on the host in every mode. */
