@@ -121,6 +121,37 @@ __device__ __forceinline__ void vstore(T* p, const vec<T>& in, int n, bool vec_o
     }
 }
 
+// 16 bytes at 4-byte alignment: one dwordx4 access (the memory pipeline splits one that crosses
+// a cache line); element runs shorter than a vector move element by element
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(4)));
+
+template <typename T>
+__device__ __forceinline__ void uload(vec<T>& out, const T* p, int n) {
+    constexpr int V = vec<T>::V;
+    if (n >= V) {
+        const u32x4u r = *reinterpret_cast<const u32x4u*>(p);
+        __builtin_memcpy(&out, &r, 16);
+    } else {
+#pragma unroll
+        for (int k = 0; k < V; ++k)
+            if (k < n) out.e[k] = p[k];
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void ustore(T* p, const vec<T>& in, int n) {
+    constexpr int V = vec<T>::V;
+    if (n >= V) {
+        u32x4u r;
+        __builtin_memcpy(&r, &in, 16);
+        *reinterpret_cast<u32x4u*>(p) = r;
+    } else {
+#pragma unroll
+        for (int k = 0; k < V; ++k)
+            if (k < n) p[k] = in.e[k];
+    }
+}
+
 // Lanes k = 0..V-1 of an aligned group hold in[.] = row k of a V x V block; afterwards
 // lane k holds column k.  Round r: every lane offers element (k - r) mod V and reads the
 // offer of lane (k + r) mod V.  All indices are compile-time after unrolling.
@@ -378,6 +409,62 @@ struct lin {  // (f, s) of linear element index e = f + s*n, stepped by 64
     }
 };
 
+// Copy mode with 16-byte accesses: lanes walk the op's columns in runs of V elements (a column's
+// last run may be shorter).  Tile columns start at any element, so the accesses are 4-byte
+// aligned dwordx4; per element the arithmetic is the scalar path's.  A wavefront issues 1/V of
+// the scalar path's memory instructions.  Off by default (COSTA_TINY_VCOPY=1): on cfg 5 'N' it
+// reached 3.15 TB/s against 3.35 for 4-byte accesses (profiles/r09/c5v.log), so instruction
+// issue is not what bounds the wavefront path.
+template <typename T, bool AX, int UC>
+__device__ __forceinline__ void tiny_copy_vec(const T* src, T* dst, int nf, int ns, int64_t lds,
+                                              int64_t ldd, int lane, uint32_t kind, bool conj,
+                                              T alpha, T beta) {
+    constexpr int V = vec<T>::V;
+    constexpr int UQ = UC / 16 > 0 ? UC / 16 : 1;  // runs per lane per pass
+    const int nq = (nf + V - 1) / V, total = nq * ns;
+    lin<T> p(lane, nq);
+    for (int e0 = 0; e0 < total; e0 += 64 * UQ) {
+        vec<T> x[UQ];
+        vec<T> y[AX ? UQ : 1];
+        const lin<T> q0 = p;
+#pragma unroll
+        for (int u = 0; u < UQ; ++u) {
+            if (e0 + u * 64 >= total) break;
+            if (e0 + u * 64 + lane < total) uload(x[u], src + p.s * lds + p.f * V, nf - p.f * V);
+            p.step();
+        }
+        if constexpr (AX) {
+            if (kind == COSTA_SCALE_AXPBY) {
+                lin<T> r = q0;
+#pragma unroll
+                for (int u = 0; u < UQ; ++u) {
+                    if (e0 + u * 64 >= total) break;
+                    if (e0 + u * 64 + lane < total)
+                        uload(y[u], dst + r.s * ldd + r.f * V, nf - r.f * V);
+                    r.step();
+                }
+            }
+        }
+        lin<T> q = q0;
+#pragma unroll
+        for (int u = 0; u < UQ; ++u) {
+            if (e0 + u * 64 >= total) break;
+            if (e0 + u * 64 + lane < total) {
+                vec<T> v = x[u];
+                if (kind != COSTA_SCALE_BITCOPY) {
+#pragma unroll
+                    for (int e = 0; e < V; ++e)
+                        v.e[e] = scale(v.e[e],
+                                       AX && kind == COSTA_SCALE_AXPBY ? y[AX ? u : 0].e[e] : e_zero<T>(),
+                                       kind, conj, alpha, beta);
+                }
+                ustore(dst + q.s * ldd + q.f * V, v, nf - q.f * V);
+            }
+            q.step();
+        }
+    }
+}
+
 // TR = false: the list has no transposing op (the transpose path and its registers are
 // compiled out, so copy-only lists keep a high occupancy).  AX = false: no op of the list reads
 // its destination (beta == 0 everywhere), so the copy path holds no old values.  UC: bytes per
@@ -385,7 +472,7 @@ struct lin {  // (f, s) of linear element index e = f + s*n, stepped by 64
 template <typename T, int UB, bool TR, bool AX, int UC>
 __device__ __forceinline__ void tiny_op(const costa_tile_op_t& op, int lane, T* t,
                                         const char* src_base, char* dst_base,
-                                        const T* __restrict__ scalars) {
+                                        const T* __restrict__ scalars, int vcopy) {
     const uint32_t flags = op.flags;
     const uint32_t kind = (flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT;
     const bool conj = flags & COSTA_TILE_CONJ;
@@ -402,6 +489,12 @@ __device__ __forceinline__ void tiny_op(const costa_tile_op_t& op, int lane, T* 
     constexpr int U = UB / int(sizeof(T)) > 0 ? UB / int(sizeof(T)) : 1;
 
     if (!TR || !(flags & COSTA_TILE_TRANSPOSE)) {
+        if constexpr (sizeof(T) <= 8) {
+            if (vcopy) {
+                tiny_copy_vec<T, AX, UC>(src, dst, nf, ns, lds, ldd, lane, kind, conj, alpha, beta);
+                return;
+            }
+        }
         // copy mode: dst(f, s) = g(src(f, s)).  Every load of a pass is issued before the first
         // store; passes end where the op ends (wave-uniform tests), and the store walk repeats
         // the load walk instead of keeping every element's address in registers.
@@ -512,7 +605,7 @@ template <typename T, int W, int UB, bool TR, bool AX, int UC>
 __global__ __launch_bounds__(64 * W) void tiny_kernel(
     const costa_tile_op_t* __restrict__ ops, int64_t n_ops, int k_per_wave, int chunked,
     int xcd_remap, const char* src_base, char* dst_base, const T* __restrict__ scalars,
-    int lds_per_wave) {
+    int lds_per_wave, int vcopy) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = int(threadIdx.x) % 64;
     const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / 64);
@@ -532,7 +625,7 @@ __global__ __launch_bounds__(64 * W) void tiny_kernel(
     for (int64_t i = first; i < end; i += step) {
         const costa_tile_op_t op = next;
         if (i + step < end) next = ops[i + step];  // in flight while this op moves its data
-        tiny_op<T, UB, TR, AX, UC>(op, lane, t, src_base, dst_base, scalars);
+        tiny_op<T, UB, TR, AX, UC>(op, lane, t, src_base, dst_base, scalars, vcopy);
     }
 }
 
@@ -541,6 +634,8 @@ struct tiny_cfg {
     int chunked = 0;    // 0: strided assignment, 1: contiguous chunks
     int copy_bytes = 0;  // 0: tiny_copy_bytes<T>()
     int xcd = 0;
+    int vcopy = 0;  // 1: copy mode with 16-byte accesses (4- and 8-byte types); measured slower
+                    // on cfg 5 'N' (3.15 against 3.35 TB/s, profiles/r09/c5v.log)
 };
 const tiny_cfg& tiny_config() {  // COSTA_TINY_{K,CHUNKED,COPY_BYTES,XCD}: tuning overrides
     static tiny_cfg c = [] {
@@ -553,6 +648,7 @@ const tiny_cfg& tiny_config() {  // COSTA_TINY_{K,CHUNKED,COPY_BYTES,XCD}: tunin
         x.chunked = env("COSTA_TINY_CHUNKED", x.chunked) != 0;
         x.copy_bytes = env("COSTA_TINY_COPY_BYTES", x.copy_bytes);
         x.xcd = env("COSTA_TINY_XCD", x.xcd) != 0;
+        x.vcopy = env("COSTA_TINY_VCOPY", x.vcopy) != 0;
         return x;
     }();
     return c;
@@ -568,7 +664,8 @@ void launch_tiny_v(const launch_args& a, const tiny_cfg& cfg, hipStream_t stream
     const int k = int((n + blocks * W - 1) / (blocks * W));  // chunked: covers all ops
     hipLaunchKernelGGL((tiny_kernel<T, W, TINY_BYTES, TR, AX, UC>), dim3(unsigned(blocks)),
                        dim3(64 * W), lds, stream, a.ops + a.tiny_first, n, k, cfg.chunked, cfg.xcd,
-                       a.src_base, a.dst_base, static_cast<const T*>(a.scalars), per_wave);
+                       a.src_base, a.dst_base, static_cast<const T*>(a.scalars), per_wave,
+                       cfg.vcopy);
 }
 
 template <typename T, int UC>
