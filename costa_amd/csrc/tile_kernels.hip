@@ -393,6 +393,7 @@ template <typename T> constexpr int tiny_copy_bytes() { return sizeof(T) == 4 ? 
 template <typename T>
 struct lin {  // (f, s) of linear element index e = f + s*n, stepped by 64
     int f, s, df, ds, n;
+    __device__ __forceinline__ lin() : f(0), s(0), df(0), ds(0), n(1) {}
     __device__ __forceinline__ lin(int lane, int n_) : n(n_) {
         f = lane % n;
         s = lane / n;
@@ -629,7 +630,101 @@ __global__ __launch_bounds__(64 * W) void tiny_kernel(
     }
 }
 
+// Copy-only lists, NP ops per wavefront moved together: the loads of all NP ops are issued
+// before the first store, so a wavefront keeps NP ops' bytes in flight for one memory round trip
+// instead of one op's (on cfg 5 a wavefront lives one load-to-store round trip and only ~5.5
+// are resident per CU).  Per element the arithmetic is tiny_op's copy mode.
+// Off by default (COSTA_TINY_MULTI=2|4): on cfg 5 'N' 3.14 / 2.66 against 3.36 TB/s with one op
+// per wavefront (profiles/r09/c5m.log).
+template <typename T, int W, bool AX, int UC, int NP>
+__global__ __launch_bounds__(64 * W) void tiny_multi_kernel(const costa_tile_op_t* __restrict__ ops,
+                                                            int64_t n_ops, const char* src_base,
+                                                            char* dst_base,
+                                                            const T* __restrict__ scalars) {
+    const int lane = int(threadIdx.x) % 64;
+    const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / 64);
+    const int64_t first = (int64_t(blockIdx.x) * W + wave) * NP;
+    if (first >= n_ops) return;
+    constexpr int UCE = UC / int(sizeof(T)) > 0 ? UC / int(sizeof(T)) : 1;
+    const T* src[NP];
+    T* dst[NP];
+    int total[NP];
+    int64_t lds[NP], ldd[NP];
+    uint32_t kind[NP];
+    bool conj[NP];
+    T alpha[NP], beta[NP];
+    lin<T> p[NP];
+    int longest = 0;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+        total[j] = 0;
+        if (first + j >= n_ops) continue;
+        const costa_tile_op_t op = ops[first + j];
+        src[j] = reinterpret_cast<const T*>(src_base + op.src);
+        dst[j] = reinterpret_cast<T*>(dst_base + op.dst);
+        total[j] = op.nf * op.ns;
+        lds[j] = op.lds;
+        ldd[j] = op.ldd;
+        kind[j] = (op.flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT;
+        conj[j] = op.flags & COSTA_TILE_CONJ;
+        alpha[j] = beta[j] = e_zero<T>();
+        if (kind[j] >= COSTA_SCALE_ALPHA) {
+            const uint32_t slot = op.flags >> COSTA_SLOT_SHIFT;
+            alpha[j] = scalars[2 * slot];
+            beta[j] = scalars[2 * slot + 1];
+        }
+        p[j] = lin<T>(lane, op.nf);
+        longest = max(longest, total[j]);
+    }
+    for (int e0 = 0; e0 < longest; e0 += 64 * UCE) {
+        T x[NP][UCE];
+        T y[AX ? NP : 1][AX ? UCE : 1];
+        lin<T> q0[NP];
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+            q0[j] = p[j];
+#pragma unroll
+            for (int u = 0; u < UCE; ++u) {
+                if (e0 + u * 64 >= total[j]) break;
+                if (e0 + u * 64 + lane < total[j]) x[j][u] = src[j][p[j].s * lds[j] + p[j].f];
+                p[j].step();
+            }
+        }
+        if constexpr (AX) {
+#pragma unroll
+            for (int j = 0; j < NP; ++j) {
+                if (kind[j] != COSTA_SCALE_AXPBY) continue;
+                lin<T> r = q0[j];
+#pragma unroll
+                for (int u = 0; u < UCE; ++u) {
+                    if (e0 + u * 64 >= total[j]) break;
+                    if (e0 + u * 64 + lane < total[j]) y[j][u] = dst[j][r.s * ldd[j] + r.f];
+                    r.step();
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+            lin<T> q = q0[j];
+#pragma unroll
+            for (int u = 0; u < UCE; ++u) {
+                if (e0 + u * 64 >= total[j]) break;
+                if (e0 + u * 64 + lane < total[j]) {
+                    T v = x[j][u];
+                    if (kind[j] != COSTA_SCALE_BITCOPY)
+                        v = scale(v, AX && kind[j] == COSTA_SCALE_AXPBY ? y[AX ? j : 0][AX ? u : 0]
+                                                                         : e_zero<T>(),
+                                  kind[j], conj[j], alpha[j], beta[j]);
+                    dst[j][q.s * ldd[j] + q.f] = v;
+                }
+                q.step();
+            }
+        }
+    }
+}
+
 struct tiny_cfg {
+    int multi = 0;      // copy-only lists: ops moved together per wavefront (0: tiny_kernel)
     int k = 1;          // ops per wavefront
     int chunked = 0;    // 0: strided assignment, 1: contiguous chunks
     int copy_bytes = 0;  // 0: tiny_copy_bytes<T>()
@@ -644,6 +739,7 @@ const tiny_cfg& tiny_config() {  // COSTA_TINY_{K,CHUNKED,COPY_BYTES,XCD}: tunin
             const char* s = std::getenv(n);
             return s ? std::atoi(s) : d;
         };
+        x.multi = env("COSTA_TINY_MULTI", x.multi);
         x.k = std::max(1, env("COSTA_TINY_K", x.k));
         x.chunked = env("COSTA_TINY_CHUNKED", x.chunked) != 0;
         x.copy_bytes = env("COSTA_TINY_COPY_BYTES", x.copy_bytes);
@@ -668,8 +764,27 @@ void launch_tiny_v(const launch_args& a, const tiny_cfg& cfg, hipStream_t stream
                        cfg.vcopy);
 }
 
+template <typename T, bool AX, int UC, int NP>
+void launch_tiny_multi(const launch_args& a, hipStream_t stream) {
+    constexpr int W = TINY_WAVES_COPY;
+    const int64_t waves = (a.n_tiny + NP - 1) / NP;
+    const int64_t blocks = (waves + W - 1) / W;
+    if (blocks >= (1LL << 31)) throw error(COSTA_ERR_ARG, "costa: tile list too long");
+    hipLaunchKernelGGL((tiny_multi_kernel<T, W, AX, UC, NP>), dim3(unsigned(blocks)), dim3(64 * W), 0,
+                       stream, a.ops + a.tiny_first, a.n_tiny, a.src_base, a.dst_base,
+                       static_cast<const T*>(a.scalars));
+}
+
 template <typename T, int UC>
 void launch_tiny_uc(const launch_args& a, const tiny_cfg& cfg, hipStream_t stream) {
+    if (!a.any_transpose && (cfg.multi == 2 || cfg.multi == 4)) {
+        constexpr int UC4 = UC / 2 >= int(sizeof(T)) ? UC / 2 : int(sizeof(T));
+        if (cfg.multi == 2)
+            return a.any_axpby ? launch_tiny_multi<T, true, UC, 2>(a, stream)
+                               : launch_tiny_multi<T, false, UC, 2>(a, stream);
+        return a.any_axpby ? launch_tiny_multi<T, true, UC4, 4>(a, stream)
+                           : launch_tiny_multi<T, false, UC4, 4>(a, stream);
+    }
     // transposing lists: TINY_WAVES_TR wavefronts per workgroup; copy-only: TINY_WAVES_COPY
     if (a.any_transpose)
         return a.any_axpby ? launch_tiny_v<T, TINY_WAVES_TR, true, true, UC>(a, cfg, stream)
