@@ -122,6 +122,61 @@ def test_device_plan_equals_host_block_cyclic(gpu, name):
     both(c, [A], [C], r, P, [args["trans"]], [args["alpha"]], [args["beta"]])
 
 
+def _random_splits(rng, n):
+    """ragged split points of [0, n), with repeated points (empty block rows / columns)"""
+    s = [0]
+    while s[-1] < n:
+        s.append(min(n, s[-1] + int(rng.integers(1, max(2, n // 3) + 1))))
+        if rng.random() < 0.15:
+            s.append(s[-1])
+    return s
+
+
+def _random_custom(costa, rng, m, n, P, rank, base, dtype, ordering):
+    rs, cs = _random_splits(rng, m), _random_splits(rng, n)
+    own = rng.integers(0, P, (len(rs) - 1, len(cs) - 1))
+    E = 16
+    blocks, off = [], 0
+    for i in range(len(rs) - 1):
+        for j in range(len(cs) - 1):
+            if own[i, j] != rank:
+                continue
+            rows, cols = rs[i + 1] - rs[i], cs[j + 1] - cs[j]
+            ld = (cols if ordering == "R" else rows) + int(rng.integers(0, 3))
+            blocks.append((base + E * off, max(ld, 1), i, j))
+            off += max(ld, 1) * (rows if ordering == "R" else cols) + 8
+    return costa.custom_layout(len(rs) - 1, len(cs) - 1, rs, cs, own, blocks, ordering, dtype)
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_device_plan_equals_host_random(gpu, seed):
+    """random ragged custom layouts (empty block rows / columns, ld padding, both orderings),
+    1-5 ranks, every rank, 1-3 layout pairs per batch, every op and scale kind"""
+    rng = np.random.default_rng(1000 + seed)
+    dtype = int(rng.integers(0, 5))
+    P = int(rng.integers(1, 6))
+    jobs = []
+    for k in range(int(rng.integers(1, 4))):
+        m, n = int(rng.integers(1, 300)), int(rng.integers(1, 300))
+        op = "NTC"[int(rng.integers(0, 3))]
+        cm, cn = (n, m) if op != "N" else (m, n)
+        ab = [(1.0, 0.0), (0.0, 0.0), (-0.5, 0.0), (1.0, 1.0), (2.0, -0.25)][int(rng.integers(0, 5))]
+        if dtype == gpu.INT32:
+            ab = (int(ab[0]), int(ab[1]))
+        jobs.append((m, n, cm, cn, op, ab, "RC"[int(rng.integers(0, 2))], "RC"[int(rng.integers(0, 2))],
+                     int(rng.integers(0, 1 << 30))))
+    for r in range(P):
+        As, Cs = [], []
+        for k, (m, n, cm, cn, op, ab, oa, oc, s) in enumerate(jobs):
+            # the same grids and owners on every rank: the layouts' rng is re-seeded per job
+            As.append(_random_custom(gpu, np.random.default_rng(s), m, n, P, r,
+                                     (1 << 40) + (k << 34), dtype, oa))
+            Cs.append(_random_custom(gpu, np.random.default_rng(s + 1), cm, cn, P, r,
+                                     (1 << 41) + (k << 34), dtype, oc))
+        both(gpu, As, Cs, r, P, [j[4] for j in jobs], [j[5][0] for j in jobs],
+             [j[5][1] for j in jobs])
+
+
 @pytest.mark.parametrize("case", [c for c in all_cases() if c.P == 1], ids=lambda c: c.name)
 def test_transform_with_device_planner(gpu, case):
     """the engine's plan-cache miss through the device planner, end to end"""
