@@ -305,10 +305,22 @@ bool any_axpby(const std::vector<costa_tile_op_t>& ops) {
 // holds at least half a large sub-tile of data; every other op runs on the wavefront path
 // (tiny_kernel): ops over a wavefront's budget are first cut, here on the host, into
 // rectangular sub-ops within it (a sub-rectangle of a tile op is a tile op).  Budgets: copy
-// mode kTinyCopyBytes of data, transpose mode kTinyLdsBytes of staged tile (row pitch nf | 1).
+// mode one wavefront pass of data (tiny_copy_budget), transpose mode kTinyLdsBytes of staged
+// tile (row pitch nf | 1).
+// Copy mode: one pass of the wavefront (64 lanes x tiny_copy_lane_bytes) by default -- an op the
+// wavefront moves in one round trip; cfg 5 'N' 3.52 TB/s at 8 KiB against 3.35 at 16 KiB, 3.44 at
+// 4 KiB (profiles/r09/c5b.log).  COSTA_TINY_COPY_BUDGET (bytes, <= kTinyCopyBytes) overrides.
+static int64_t tiny_copy_budget(int64_t E) {
+    static const int64_t env = [] {
+        const char* s = std::getenv("COSTA_TINY_COPY_BUDGET");
+        return s ? std::max<int64_t>(256, std::min<int64_t>(kTinyCopyBytes, std::atoll(s))) : 0;
+    }();
+    return env ? env : 64 * int64_t(tiny_copy_lane_bytes(size_t(E)));
+}
+
 static bool is_tiny(const costa_tile_op_t& op, int64_t E) {
     if (op.flags & COSTA_TILE_TRANSPOSE) return int64_t(op.nf | 1) * op.ns * E <= kTinyLdsBytes;
-    return int64_t(op.nf) * op.ns * E <= kTinyCopyBytes;
+    return int64_t(op.nf) * op.ns * E <= tiny_copy_budget(E);
 }
 
 static uint32_t vec_flags(uint64_t src, int64_t lds, uint64_t dst, int64_t ldd, int64_t E) {
@@ -325,7 +337,7 @@ static void split_for_waves(const costa_tile_op_t& op, int64_t E, std::vector<co
         return;
     }
     const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
-    const int64_t budget = (tr ? kTinyLdsBytes : kTinyCopyBytes) / E;  // elements
+    const int64_t budget = (tr ? kTinyLdsBytes : tiny_copy_budget(E)) / E;  // elements
     const int64_t nf = op.nf, ns = op.ns;
     // transpose: near-square pieces (both the source columns and the destination rows stay
     // long); copy: whole columns when one fits, else tall pieces

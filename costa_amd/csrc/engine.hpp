@@ -152,6 +152,8 @@ void execute_tiles(costa_dtype_t dtype, const costa_tile_op_t* ops, int64_t n,
 // data, transpose mode up to kTinyLdsBytes of staged tile (row pitch nf | 1)
 constexpr int kTinyCopyBytes = 16384;
 constexpr int kTinyLdsBytes = 8192;
+// bytes a lane of the wavefront copy path moves per pass (tile_kernels.hip tiny_copy_bytes)
+constexpr int tiny_copy_lane_bytes(size_t elem) { return elem == 4 ? 128 : 64; }
 constexpr int tiny_lds_bytes = kTinyLdsBytes;
 
 struct launch_args {

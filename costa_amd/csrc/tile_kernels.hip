@@ -388,7 +388,7 @@ constexpr int TINY_BYTES = 64;  // bytes in flight per lane per pass (96: -3 %, 
                                 // cfg 5, profiles/r07/c5_bytes.log)
 // the same for the copy path: 4-byte types 128 (every load of a 2048-element op in flight at
 // once; cfg 5 'N' +3 % over 64 in an interleaved A/B, profiles/r07/c5_copy.log), else 64
-template <typename T> constexpr int tiny_copy_bytes() { return sizeof(T) == 4 ? 128 : 64; }
+template <typename T> constexpr int tiny_copy_bytes() { return tiny_copy_lane_bytes(sizeof(T)); }
 
 template <typename T>
 struct lin {  // (f, s) of linear element index e = f + s*n, stepped by 64

@@ -1,6 +1,6 @@
 """GPU parity of one batched tile launch against the oracle, on random op lists that mix every
 work class of the executor: tiny ops (one wavefront each, copy and LDS transpose), small and
-large sub-tile shapes, the class boundaries (engine.hpp kTinyCopyBytes / kTinyLdsBytes), thin
+large sub-tile shapes, the class boundaries (engine.cpp tiny_copy_budget / kTinyLdsBytes), thin
 ops (nf = 1, ns = 1), padded strides, unaligned offsets, and every scale kind.
 
 Each op is the reference's copy_and_transform (memory_utils.hpp:339-412); the oracle executes
@@ -17,7 +17,12 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
-TINY_COPY, TINY_LDS = 16384, 8192  # engine.hpp kTinyCopyBytes / kTinyLdsBytes
+TINY_LDS = 8192  # engine.hpp kTinyLdsBytes
+
+
+def tiny_copy(E):
+    """engine.cpp tiny_copy_budget: one wavefront pass, 64 lanes x tiny_copy_lane_bytes"""
+    return 64 * (128 if E == 4 else 64)
 
 
 @pytest.fixture(scope="module")
@@ -42,7 +47,7 @@ def _shape(rng, E, transpose):
     if pick == 0:  # tiny, ragged
         return int(rng.integers(1, 70)), int(rng.integers(1, 70))
     if pick == 1:  # at the tiny boundary
-        limit = (TINY_LDS if transpose else TINY_COPY) // E
+        limit = (TINY_LDS if transpose else tiny_copy(E)) // E
         nf = int(rng.integers(1, 129))
         ns = max(1, limit // ((nf | 1) if transpose else nf) + int(rng.integers(-1, 2)))
         return nf, ns
