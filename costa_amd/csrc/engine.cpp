@@ -318,8 +318,19 @@ static int64_t tiny_copy_budget(int64_t E) {
     return env ? env : 64 * int64_t(tiny_copy_lane_bytes(size_t(E)));
 }
 
+// Transpose mode: the staged tile, at most the wavefront's kTinyLdsBytes of LDS;
+// COSTA_TINY_LDS_BUDGET (bytes, <= kTinyLdsBytes) cuts smaller pieces (tuning).
+static int64_t tiny_lds_budget() {
+    static const int64_t b = [] {
+        const char* s = std::getenv("COSTA_TINY_LDS_BUDGET");
+        return s ? std::max<int64_t>(256, std::min<int64_t>(kTinyLdsBytes, std::atoll(s)))
+                 : int64_t(kTinyLdsBytes);
+    }();
+    return b;
+}
+
 static bool is_tiny(const costa_tile_op_t& op, int64_t E) {
-    if (op.flags & COSTA_TILE_TRANSPOSE) return int64_t(op.nf | 1) * op.ns * E <= kTinyLdsBytes;
+    if (op.flags & COSTA_TILE_TRANSPOSE) return int64_t(op.nf | 1) * op.ns * E <= tiny_lds_budget();
     return int64_t(op.nf) * op.ns * E <= tiny_copy_budget(E);
 }
 
@@ -337,7 +348,7 @@ static void split_for_waves(const costa_tile_op_t& op, int64_t E, std::vector<co
         return;
     }
     const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
-    const int64_t budget = (tr ? kTinyLdsBytes : tiny_copy_budget(E)) / E;  // elements
+    const int64_t budget = (tr ? tiny_lds_budget() : tiny_copy_budget(E)) / E;  // elements
     const int64_t nf = op.nf, ns = op.ns;
     // transpose: near-square pieces (both the source columns and the destination rows stay
     // long); copy: whole columns when one fits, else tall pieces
