@@ -320,7 +320,7 @@ static int64_t tiny_copy_budget(int64_t E) {
 
 // Transpose mode: the staged tile, at most the wavefront's kTinyLdsBytes of LDS;
 // COSTA_TINY_LDS_BUDGET (bytes, <= kTinyLdsBytes) cuts smaller pieces (tuning).
-static int64_t tiny_lds_budget() {
+int64_t tiny_lds_budget() {
     static const int64_t b = [] {
         const char* s = std::getenv("COSTA_TINY_LDS_BUDGET");
         return s ? std::max<int64_t>(256, std::min<int64_t>(kTinyLdsBytes, std::atoll(s)))

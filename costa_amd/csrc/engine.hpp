@@ -152,6 +152,9 @@ void execute_tiles(costa_dtype_t dtype, const costa_tile_op_t* ops, int64_t n,
 // data, transpose mode up to kTinyLdsBytes of staged tile (row pitch nf | 1)
 constexpr int kTinyCopyBytes = 16384;
 constexpr int kTinyLdsBytes = 8192;
+// staged bytes of one transposing wavefront op (kTinyLdsBytes unless COSTA_TINY_LDS_BUDGET);
+// the launch gives each wavefront that much LDS
+int64_t tiny_lds_budget();
 // bytes a lane of the wavefront copy path moves per pass (tile_kernels.hip tiny_copy_bytes)
 constexpr int tiny_copy_lane_bytes(size_t elem) { return elem == 4 ? 128 : 64; }
 constexpr int tiny_lds_bytes = kTinyLdsBytes;

@@ -753,7 +753,7 @@ const tiny_cfg& tiny_config() {  // COSTA_TINY_{K,CHUNKED,COPY_BYTES,XCD}: tunin
 template <typename T, int W, bool TR, bool AX, int UC>
 void launch_tiny_v(const launch_args& a, const tiny_cfg& cfg, hipStream_t stream) {
     const int64_t n = a.n_tiny;
-    const int per_wave = a.any_transpose ? int(tiny_lds_bytes / sizeof(T)) : 0;
+    const int per_wave = a.any_transpose ? int(tiny_lds_budget() / int64_t(sizeof(T))) : 0;
     const size_t lds = size_t(per_wave) * sizeof(T) * W;
     const int64_t waves = (n + cfg.k - 1) / cfg.k;
     const int64_t blocks = std::min<int64_t>((waves + W - 1) / W, 1LL << 30);
