@@ -402,6 +402,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     ordered.clear();
     work.clear();
     std::vector<costa_tile_op_t> tiny;
+    tiny.reserve(ops.size() + ops.size() / 4);
     std::vector<uint64_t> small;
     const uint32_t vec_both = COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST;
     for (const auto& op : ops) {
@@ -409,7 +410,11 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         const int64_t elems = int64_t(op.nf) * op.ns;
         bool large = 2 * elems >= int64_t(bfl) * bsl;
         if (kn.policy == 2 && (op.flags & vec_both) != vec_both) large = false;
-        if (is_tiny(op, E) || (!large && kn.policy >= 1)) {
+        if (is_tiny(op, E)) {
+            tiny.push_back(op);
+            continue;
+        }
+        if (!large && kn.policy >= 1) {
             split_for_waves(op, E, tiny);
             continue;
         }
@@ -424,21 +429,27 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     }
     // ops are independent (disjoint destinations), so any order is valid; neighbours in
     // memory run at the same time and share the partially used cache lines at their edges
-    const bool hinted = std::any_of(tiny.begin(), tiny.end(),
-                                    [](const costa_tile_op_t& o) { return o.order != 0; });
-    const int mode = kn.sort == 3 && !hinted ? 2 : kn.sort;
-    uint32_t top = 0;  // largest hint
-    if (mode == 3)
-        for (const auto& o : tiny) top = std::max(top, o.order);
+    uint32_t top = 0;  // largest hint (0: none of the ops carries one)
+    for (const auto& o : tiny) top = std::max(top, o.order);
+    const int mode = kn.sort == 3 && top == 0 ? 2 : kn.sort;
+    work_split w;
+    w.n_large = int64_t(work.size());
+    w.n_small = int64_t(small.size());
+    w.tiny_first = int64_t(ordered.size());
+    w.n_tiny = int64_t(tiny.size());
+    work.insert(work.end(), small.begin(), small.end());
     if (mode == 3 && size_t(top) <= 4 * tiny.size() + 1024) {
-        // the planner's hints are ranks within the list: a stable counting sort
+        // the planner's hints are ranks within the list: a stable counting sort, straight into
+        // the ordered list
         std::vector<uint32_t> at(size_t(top) + 2, 0);
         for (const auto& o : tiny) ++at[size_t(o.order) + 1];
         for (size_t k = 1; k < at.size(); ++k) at[k] += at[k - 1];
-        std::vector<costa_tile_op_t> sorted(tiny.size());
-        for (const auto& o : tiny) sorted[at[o.order]++] = o;
-        tiny.swap(sorted);
-    } else if (mode >= 1 && mode <= 3) {  // sort (key, index) pairs: stable, and cheap to move
+        const size_t base = ordered.size();
+        ordered.resize(base + tiny.size());
+        for (const auto& o : tiny) ordered[base + at[o.order]++] = o;
+        return w;
+    }
+    if (mode >= 1 && mode <= 3) {  // sort (key, index) pairs: stable, and cheap to move
         std::vector<std::pair<uint64_t, uint32_t>> key(tiny.size());
         for (size_t i = 0; i < tiny.size(); ++i)
             key[i] = {mode == 1 ? tiny[i].src : mode == 2 ? tiny[i].dst : tiny[i].order,
@@ -448,12 +459,6 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         for (size_t i = 0; i < key.size(); ++i) sorted[i] = tiny[key[i].second];
         tiny.swap(sorted);
     }
-    work_split w;
-    w.n_large = int64_t(work.size());
-    w.n_small = int64_t(small.size());
-    w.tiny_first = int64_t(ordered.size());
-    w.n_tiny = int64_t(tiny.size());
-    work.insert(work.end(), small.begin(), small.end());
     ordered.insert(ordered.end(), tiny.begin(), tiny.end());
     return w;
 }
