@@ -15,7 +15,9 @@ ranks.  value = algorithmic bytes of all ranks / that time (read + 
 element moved, + read of C when beta != 0).  Rank 0 prints ONE JSON line.
 
 roofline: the dominant kernel's algorithmic bytes per launch / its average duration from
-HIP events recorded on the stream it runs on (costa_hip_get_stats), against 8 TB/s.
+HIP events recorded on the stream it runs on (costa_hip_get_stats), against 8 TB/s.  Those
+events are recorded in a second pass of the same K steps: in the `value` pass they are off, as
+they are in the shipped library (each event pair adds ~11 us to a 0.83 ms cfg 2 step).
 cpu_baseline: the oracle's restatement of the reference's OpenMP tile loop (256x256-blocked
 transpose, OpenMP over tiles) on a bounded sample of the same tiles, rank 0 at N = 1.
 """
@@ -302,8 +304,8 @@ def main():
     def step_async():  # stream-ordered: the host queues step k+1 while step k runs
         costa.transform_async(LA, LC, comm, op, al, be)
 
-    def timed(step):
-        costa.set_profiling(True)
+    def timed(step, profile=True):
+        costa.set_profiling(profile)
         costa.get_stats(reset=True)
         barrier()
         torch.cuda.synchronize()
@@ -345,10 +347,15 @@ def main():
         step_blocking()
     if world == 1 and check and repeatable:  # correctness of what we time
         check()
-    el_block, _ = timed(step_blocking)
+    el_block, _ = timed(step_blocking, profile=False)
     for _ in range(args.warmup):
         step_async()
-    el, st = timed(step_async)
+    # value: the product as shipped (phase-timing events off: recording them costs ~11 us per
+    # step on cfg 2, tools/step_gap_probe.py); then the same K steps again with the events on,
+    # for the kernel durations (roofline.avg_launch_ms, phase_ms_per_step)
+    el, st_val = timed(step_async, profile=False)
+    el_ev, st = timed(step_async)
+    assert all(st_val[k] == st[k] for k in ("local_bytes", "pack_bytes", "unpack_bytes"))
     if world == 1 and check and repeatable:
         check()
 
@@ -476,7 +483,13 @@ def main():
             "blocking": {"ms_per_step": round(el_block / args.steps * 1e3, 4),
                          "GBps": round(total_bytes / el_block / 1e9, 2),
                          "note": "costa_hip_transform (reference semantics: host waits for C)"},
-            "value_mode": "costa_hip_transform_async steps, stream-ordered, one sync at the end",
+            "value_mode": ("costa_hip_transform_async steps, stream-ordered, one sync at the end; "
+                           "phase-timing events off (the shipped default)"),
+            "with_phase_events": {"ms_per_step": round(el_ev / args.steps * 1e3, 4),
+                                  "GBps": round(total_bytes / el_ev / 1e9, 2),
+                                  "note": "second pass of the same K steps with a HIP event "
+                                          "pair around every phase: the source of the kernel "
+                                          "durations (roofline.avg_launch_ms)"},
             "kernel_node_GBps": round(kernel_node, 2) if kernel_node else None,
             "phase_ms_per_step": {k: round(st[k + "_ms"] / args.steps, 4)
                                   for k in ("pack", "local", "unpack", "exchange")},
