@@ -305,7 +305,7 @@ bool any_axpby(const std::vector<costa_tile_op_t>& ops) {
 // holds at least half a large sub-tile of data; every other op runs on the wavefront path
 // (tiny_kernel): ops over a wavefront's budget are first cut, here on the host, into
 // rectangular sub-ops within it (a sub-rectangle of a tile op is a tile op).  Budgets: copy
-// mode one wavefront pass of data (tiny_copy_budget), transpose mode kTinyLdsBytes of staged
+// mode one wavefront pass of data (tiny_copy_budget), transpose mode tiny_lds_budget() of staged
 // tile (row pitch nf | 1).
 // Copy mode: one pass of the wavefront (64 lanes x tiny_copy_lane_bytes) by default -- an op the
 // wavefront moves in one round trip; cfg 5 'N' 3.52 TB/s at 8 KiB against 3.35 at 16 KiB, 3.44 at
@@ -318,13 +318,13 @@ static int64_t tiny_copy_budget(int64_t E) {
     return env ? env : 64 * int64_t(tiny_copy_lane_bytes(size_t(E)));
 }
 
-// Transpose mode: the staged tile, at most the wavefront's kTinyLdsBytes of LDS;
-// COSTA_TINY_LDS_BUDGET (bytes, <= kTinyLdsBytes) cuts smaller pieces (tuning).
+// Transpose mode: the staged tile, kTinyLdsDefault bytes of LDS per wavefront;
+// COSTA_TINY_LDS_BUDGET (bytes, <= kTinyLdsBytes) overrides (tuning).
 int64_t tiny_lds_budget() {
     static const int64_t b = [] {
         const char* s = std::getenv("COSTA_TINY_LDS_BUDGET");
         return s ? std::max<int64_t>(256, std::min<int64_t>(kTinyLdsBytes, std::atoll(s)))
-                 : int64_t(kTinyLdsBytes);
+                 : int64_t(kTinyLdsDefault);
     }();
     return b;
 }

@@ -149,14 +149,20 @@ void execute_tiles(costa_dtype_t dtype, const costa_tile_op_t* ops, int64_t n,
 
 // kernel launcher (tile_kernels.hip); `work` and `ops` are device arrays
 // ops small enough for one wavefront each (tiny path): copy mode up to kTinyCopyBytes of
-// data, transpose mode up to kTinyLdsBytes of staged tile (row pitch nf | 1)
+// data, transpose mode up to kTinyLdsBytes of staged tile (row pitch nf | 1); the defaults
+// are smaller (tiny_copy_budget: one pass of the wavefront; kTinyLdsDefault staged)
 constexpr int kTinyCopyBytes = 16384;
 constexpr int kTinyLdsBytes = 8192;
-// staged bytes of one transposing wavefront op (kTinyLdsBytes unless COSTA_TINY_LDS_BUDGET);
+// r11, cfg 5 'T' with the XCD remap and 32 bytes per lane per pass: 3.80 TB/s at 4 KiB
+// against 3.0 at 8 KiB (profiles/r11/tiny_variants*.log)
+constexpr int kTinyLdsDefault = 4096;
+// staged bytes of one transposing wavefront op (kTinyLdsDefault unless COSTA_TINY_LDS_BUDGET);
 // the launch gives each wavefront that much LDS
 int64_t tiny_lds_budget();
 // bytes a lane of the wavefront copy path moves per pass (tile_kernels.hip tiny_copy_bytes)
-constexpr int tiny_copy_lane_bytes(size_t elem) { return elem == 4 ? 128 : 64; }
+// (64 for every type since r11: 4-byte types at 128 gave cfg 5 'N' 3.77 against 4.15 TB/s once
+// the XCD remap was on, profiles/r11/c5_budget.log; fewer VGPRs, more resident wavefronts)
+constexpr int tiny_copy_lane_bytes(size_t) { return 64; }
 constexpr int tiny_lds_bytes = kTinyLdsBytes;
 
 struct launch_args {

@@ -382,12 +382,22 @@ __global__ __launch_bounds__(S::NT) void tile_kernel(const costa_tile_op_t* __re
 // Wavefronts per workgroup: 2 for lists that transpose (8 KiB of LDS per wavefront), 8 for
 // copy-only lists (no LDS).  Measured on cfg 5 (profiles/r06/c5_knobs.log): transposes 3.1-3.3
 // TB/s at 2 against 2.95 at 4; copies 3.40 at 8 against 3.36 at 4.
-constexpr int TINY_WAVES_TR = 2;
-constexpr int TINY_WAVES_COPY = 8;
-constexpr int TINY_BYTES = 64;  // bytes in flight per lane per pass (96: -3 %, 128: -35 % on
-                                // cfg 5, profiles/r07/c5_bytes.log)
-// the same for the copy path: 4-byte types 128 (every load of a 2048-element op in flight at
-// once; cfg 5 'N' +3 % over 64 in an interleaved A/B, profiles/r07/c5_copy.log), else 64
+#ifndef COSTA_TINY_WAVES_TR  // build-time overrides for tuning builds (tools/tiny_variants.sh)
+#define COSTA_TINY_WAVES_TR 2
+#endif
+#ifndef COSTA_TINY_WAVES_COPY
+#define COSTA_TINY_WAVES_COPY 8
+#endif
+#ifndef COSTA_TINY_BYTES
+#define COSTA_TINY_BYTES 32
+#endif
+constexpr int TINY_WAVES_TR = COSTA_TINY_WAVES_TR;
+constexpr int TINY_WAVES_COPY = COSTA_TINY_WAVES_COPY;
+// bytes in flight per lane per pass of the transpose path: 32 since r11 (cfg 5 'T' 3.80 TB/s
+// against 3.51 at 64 and 3.65 at 16, 4 KiB staged, profiles/r11/tiny_variants*.log; before the
+// XCD remap 64 was best: 96 -3 %, 128 -35 %, profiles/r07/c5_bytes.log)
+constexpr int TINY_BYTES = COSTA_TINY_BYTES;
+// the same for the copy path (engine.hpp tiny_copy_lane_bytes): 64 for every type since r11
 template <typename T> constexpr int tiny_copy_bytes() { return tiny_copy_lane_bytes(sizeof(T)); }
 
 template <typename T>
@@ -728,7 +738,8 @@ struct tiny_cfg {
     int k = 1;          // ops per wavefront
     int chunked = 0;    // 0: strided assignment, 1: contiguous chunks
     int copy_bytes = 0;  // 0: tiny_copy_bytes<T>()
-    int xcd = 0;
+    int xcd = 1;  // r11: cfg 5 'N' 3.77 against 3.58 TB/s, 'T' 3.07 against 3.00
+                  // (profiles/r11/c5_order.log, band 0 rows)
     int vcopy = 0;  // 1: copy mode with 16-byte accesses (4- and 8-byte types); measured slower
                     // on cfg 5 'N' (3.15 against 3.35 TB/s, profiles/r09/c5v.log)
 };

@@ -17,12 +17,12 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
-TINY_LDS = 8192  # engine.hpp kTinyLdsBytes
+TINY_LDS = 4096  # engine.hpp kTinyLdsDefault
 
 
 def tiny_copy(E):
     """engine.cpp tiny_copy_budget: one wavefront pass, 64 lanes x tiny_copy_lane_bytes"""
-    return 64 * (128 if E == 4 else 64)
+    return 64 * 64
 
 
 @pytest.fixture(scope="module")

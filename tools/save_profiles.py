@@ -11,7 +11,8 @@ grid are taken, the median per kernel is summed.  One json per workload:
   pmc_cfg5_N.json / pmc_cfg5_T.json
 bench.py's measured_traffic() picks the file whose bytes_per_launch_alg equals its own.
 Caveat written into each file: the x2 FETCH correction is calibrated for 16-B-per-lane loads;
-the wavefront path of cfg 5 uses 4-B loads, for which it is uncalibrated."""
+the wavefront path of cfg 5 uses 4-B loads: calibrated in profiles/r11/calib/calib.json
+(x1.95-1.98 on a line-aligned geometry, so x2 is within 2.5 %)."""
 import csv
 import json
 import os
@@ -66,7 +67,7 @@ def derive(prefix, dtype, out_name):
            "kernels_fetch": fper, "kernels_write": wper,
            "hbm_bytes_per_launch_corrected": int((2 * fk + wk) * 1024),
            "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halving; "
-                         "calibrated for 16-B/lane loads only)"}
+                         "16-B loads exact, 4-B loads within 2.5 %: profiles/r11/calib)"}
     d = bench_line(os.path.join(src, f"{prefix}pmc_fetch.log"))
     if d:
         out["bytes_per_launch_alg"] = d["roofline"]["bytes_per_launch"]
