@@ -307,15 +307,18 @@ bool any_axpby(const std::vector<costa_tile_op_t>& ops) {
 // rectangular sub-ops within it (a sub-rectangle of a tile op is a tile op).  Budgets: copy
 // mode one wavefront pass of data (tiny_copy_budget), transpose mode tiny_lds_budget() of staged
 // tile (row pitch nf | 1).
-// Copy mode: one pass of the wavefront (64 lanes x tiny_copy_lane_bytes) by default -- an op the
-// wavefront moves in one round trip; cfg 5 'N' 3.52 TB/s at 8 KiB against 3.35 at 16 KiB, 3.44 at
-// 4 KiB (profiles/r09/c5b.log).  COSTA_TINY_COPY_BUDGET (bytes, <= kTinyCopyBytes) overrides.
+// Copy mode: three quarters of one wavefront pass (64 lanes x tiny_copy_lane_bytes) by default
+// -- an op the wavefront moves in one round trip, cut a little finer for more wavefronts in
+// flight; cfg 5 'N' 4.26 TB/s at 3 KiB against 4.15 at 4 KiB and 4.25 at 2 KiB with 64-byte
+// lanes and the XCD remap (profiles/r11/c5_budget_uc64.log; r09, 128-byte lanes without the
+// remap: 8 KiB best, profiles/r09/c5b.log).  COSTA_TINY_COPY_BUDGET (bytes, <= kTinyCopyBytes)
+// overrides.
 static int64_t tiny_copy_budget(int64_t E) {
     static const int64_t env = [] {
         const char* s = std::getenv("COSTA_TINY_COPY_BUDGET");
         return s ? std::max<int64_t>(256, std::min<int64_t>(kTinyCopyBytes, std::atoll(s))) : 0;
     }();
-    return env ? env : 64 * int64_t(tiny_copy_lane_bytes(size_t(E)));
+    return env ? env : 48 * int64_t(tiny_copy_lane_bytes(size_t(E)));
 }
 
 // Transpose mode: the staged tile, kTinyLdsDefault bytes of LDS per wavefront;

@@ -21,8 +21,8 @@ TINY_LDS = 4096  # engine.hpp kTinyLdsDefault
 
 
 def tiny_copy(E):
-    """engine.cpp tiny_copy_budget: one wavefront pass, 64 lanes x tiny_copy_lane_bytes"""
-    return 64 * 64
+    """engine.cpp tiny_copy_budget: 3/4 of a wavefront pass, 48 lanes x tiny_copy_lane_bytes"""
+    return 48 * 64
 
 
 @pytest.fixture(scope="module")
