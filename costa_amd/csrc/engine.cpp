@@ -382,8 +382,10 @@ struct wave_knobs {  // defaults, overridable for tuning runs
     int policy = 1;  // COSTA_WAVE_POLICY 0: only ops within the budget take the wave path (the
                      // rest: 256-thread small shape); 1: every op below the large threshold;
                      // 2: also large ops that are not 16-byte aligned on both sides
-    int sort = 3;    // COSTA_TINY_SORT 0: list order, 1: by source, 2: by destination address,
-                     // 3: by the planner's locality hint (costa_tile_op_t::order), else as 2
+    int sort = 4;    // COSTA_TINY_SORT 0: list order, 1: by source, 2: by destination address,
+                     // 3: by the planner's locality hint (costa_tile_op_t::order), 4: 3 for
+                     // copy-only lists, 2 for lists that transpose (cfg 5 'T' 3.88 against
+                     // 3.79 TB/s, 'N' equal; profiles/r11/c5_env.log), else as 2
 };
 const wave_knobs& knobs() {
     static wave_knobs k = [] {
@@ -433,8 +435,12 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     // ops are independent (disjoint destinations), so any order is valid; neighbours in
     // memory run at the same time and share the partially used cache lines at their edges
     uint32_t top = 0;  // largest hint (0: none of the ops carries one)
-    for (const auto& o : tiny) top = std::max(top, o.order);
-    const int mode = kn.sort == 3 && top == 0 ? 2 : kn.sort;
+    bool tr = false;
+    for (const auto& o : tiny) {
+        top = std::max(top, o.order);
+        tr = tr || (o.flags & COSTA_TILE_TRANSPOSE);
+    }
+    const int mode = kn.sort == 4 ? (tr || top == 0 ? 2 : 3) : kn.sort == 3 && top == 0 ? 2 : kn.sort;
     work_split w;
     w.n_large = int64_t(work.size());
     w.n_small = int64_t(small.size());
@@ -450,6 +456,42 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         const size_t base = ordered.size();
         ordered.resize(base + tiny.size());
         for (const auto& o : tiny) ordered[base + at[o.order]++] = o;
+        return w;
+    }
+    if (mode == 2 && !tiny.empty()) {
+        // by destination address: a stable LSD radix sort of the element offsets from the lowest
+        // destination (14-bit digits, only as many passes as the span needs), straight into the
+        // ordered list
+        uint64_t lo = ~uint64_t(0), hi = 0;
+        for (const auto& o : tiny) {
+            lo = std::min(lo, o.dst);
+            hi = std::max(hi, o.dst);
+        }
+        const size_t n = tiny.size();
+        std::vector<uint64_t> key(n), key2(n);
+        std::vector<uint32_t> idx(n), idx2(n);
+        for (size_t i = 0; i < n; ++i) {
+            key[i] = (tiny[i].dst - lo) / uint64_t(E);
+            idx[i] = uint32_t(i);
+        }
+        const uint64_t span = (hi - lo) / uint64_t(E);
+        constexpr int B = 14;
+        std::vector<uint32_t> at((1 << B) + 1);
+        for (int shift = 0; shift == 0 || (shift < 64 && (span >> shift) != 0); shift += B) {
+            std::fill(at.begin(), at.end(), 0u);
+            for (size_t i = 0; i < n; ++i) ++at[((key[i] >> shift) & ((1 << B) - 1)) + 1];
+            for (int d = 1; d <= (1 << B); ++d) at[d] += at[d - 1];
+            for (size_t i = 0; i < n; ++i) {
+                const uint32_t p = at[(key[i] >> shift) & ((1 << B) - 1)]++;
+                key2[p] = key[i];
+                idx2[p] = idx[i];
+            }
+            key.swap(key2);
+            idx.swap(idx2);
+        }
+        const size_t base = ordered.size();
+        ordered.resize(base + n);
+        for (size_t i = 0; i < n; ++i) ordered[base + i] = tiny[idx[i]];
         return w;
     }
     if (mode >= 1 && mode <= 3) {  // sort (key, index) pairs: stable, and cheap to move
