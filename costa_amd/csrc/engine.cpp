@@ -7,6 +7,8 @@
 //   aux stream  : LOCAL kernel, overlapping pack + exchange (the reference overlaps its
 //                 local copy with the MPI messages in flight, transform.cpp:96-101)
 // Plans are cached by layout content (the reference re-plans every call).
+#include <exception>
+#include <thread>
 #include "engine.hpp"
 
 #include <hip/hip_runtime.h>
@@ -344,27 +346,40 @@ static uint32_t vec_flags(uint64_t src, int64_t lds, uint64_t dst, int64_t ldd, 
     return f;
 }
 
-// cut `op` into near-equal rectangles that each fit the wavefront budget
-static void split_for_waves(const costa_tile_op_t& op, int64_t E, std::vector<costa_tile_op_t>& out) {
-    if (is_tiny(op, E)) {
-        out.push_back(op);
-        return;
-    }
+// cut `op` into near-equal rectangles that each fit the wavefront budget: the grid of pieces
+// (nfc x nsc pieces of cf x cs elements at most), then the pieces themselves
+namespace {
+struct wave_grid {
+    int64_t nfc = 1, nsc = 1;
+};
+wave_grid wave_pieces(const costa_tile_op_t& op, int64_t E) {
+    wave_grid g;
+    if (is_tiny(op, E)) return g;
     const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
     const int64_t budget = (tr ? tiny_lds_budget() : tiny_copy_budget(E)) / E;  // elements
     const int64_t nf = op.nf, ns = op.ns;
     // transpose: near-square pieces (both the source columns and the destination rows stay
     // long); copy: whole columns when one fits, else tall pieces
     const int64_t side = tr ? std::max<int64_t>(1, int64_t(std::sqrt(double(budget)))) : budget;
-    const int64_t nfc = (nf + side - 1) / side;
-    const int64_t cf = (nf + nfc - 1) / nfc;
+    g.nfc = (nf + side - 1) / side;
+    const int64_t cf = (nf + g.nfc - 1) / g.nfc;
     const int64_t cs_max = std::max<int64_t>(1, budget / (tr ? (cf | 1) : cf));
-    const int64_t nsc = (ns + cs_max - 1) / cs_max;
+    g.nsc = (ns + cs_max - 1) / cs_max;
+    return g;
+}
+// writes the g.nfc * g.nsc pieces of `op` at `out`
+void emit_pieces(const costa_tile_op_t& op, int64_t E, const wave_grid& g, costa_tile_op_t* out) {
+    if (g.nfc == 1 && g.nsc == 1) {
+        *out = op;
+        return;
+    }
+    const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
+    const int64_t nf = op.nf, ns = op.ns;
     const uint32_t keep = op.flags & ~uint32_t(COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST);
-    for (int64_t i = 0; i < nfc; ++i) {
-        const int64_t f0 = i * nf / nfc, f1 = (i + 1) * nf / nfc;
-        for (int64_t j = 0; j < nsc; ++j) {
-            const int64_t s0 = j * ns / nsc, s1 = (j + 1) * ns / nsc;
+    for (int64_t i = 0; i < g.nfc; ++i) {
+        const int64_t f0 = i * nf / g.nfc, f1 = (i + 1) * nf / g.nfc;
+        for (int64_t j = 0; j < g.nsc; ++j) {
+            const int64_t s0 = j * ns / g.nsc, s1 = (j + 1) * ns / g.nsc;
             costa_tile_op_t sub = op;
             sub.src = op.src + uint64_t((s0 * op.lds + f0) * E);
             sub.dst = op.dst + uint64_t((tr ? f0 * op.ldd + s0 : s0 * op.ldd + f0) * E);
@@ -372,10 +387,32 @@ static void split_for_waves(const costa_tile_op_t& op, int64_t E, std::vector<co
             sub.ns = int32_t(s1 - s0);
             sub.flags = keep | vec_flags(sub.src, op.lds, sub.dst, op.ldd, E);
             if (!is_tiny(sub, E)) throw error(COSTA_ERR_INTERNAL, "costa: wave split over budget");
-            out.push_back(sub);
+            *out++ = sub;
         }
     }
 }
+
+// runs fn(begin, end) over [0, n) on up to 8 host threads (one when n is small)
+template <typename F>
+void host_parallel(size_t n, F fn) {
+    const size_t hw = std::max(1u, std::thread::hardware_concurrency());
+    const size_t T = n < 32768 ? 1 : std::min<size_t>(8, hw);
+    if (T == 1) return fn(size_t(0), n);
+    std::vector<std::thread> th;
+    std::vector<std::exception_ptr> err(T);
+    for (size_t t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            try {
+                fn(n * t / T, n * (t + 1) / T);
+            } catch (...) {
+                err[t] = std::current_exception();
+            }
+        });
+    for (auto& x : th) x.join();
+    for (auto& e : err)
+        if (e) std::rethrow_exception(e);
+}
+}  // namespace
 
 namespace {
 struct wave_knobs {  // defaults, overridable for tuning runs
@@ -406,8 +443,8 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     const wave_knobs& kn = knobs();
     ordered.clear();
     work.clear();
-    std::vector<costa_tile_op_t> tiny;
-    tiny.reserve(ops.size() + ops.size() / 4);
+    std::vector<const costa_tile_op_t*> wave_ops;  // ops for the wavefront path, in list order
+    wave_ops.reserve(ops.size());
     std::vector<uint64_t> small;
     const uint32_t vec_both = COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST;
     for (const auto& op : ops) {
@@ -415,12 +452,8 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         const int64_t elems = int64_t(op.nf) * op.ns;
         bool large = 2 * elems >= int64_t(bfl) * bsl;
         if (kn.policy == 2 && (op.flags & vec_both) != vec_both) large = false;
-        if (is_tiny(op, E)) {
-            tiny.push_back(op);
-            continue;
-        }
-        if (!large && kn.policy >= 1) {
-            split_for_waves(op, E, tiny);
+        if (is_tiny(op, E) || (!large && kn.policy >= 1)) {
+            wave_ops.push_back(&op);
             continue;
         }
         const uint64_t i = ordered.size();
@@ -433,78 +466,84 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         for (uint64_t k = 0; k < n; ++k) dst.push_back((i << 32) | k);
     }
     // ops are independent (disjoint destinations), so any order is valid; neighbours in
-    // memory run at the same time and share the partially used cache lines at their edges
+    // memory run at the same time and share the partially used cache lines at their edges.
+    // The wavefront ops are ordered first, then cut into their pieces straight into the ordered
+    // list (pieces of one op stay together, in f-major order).
+    const size_t nw = wave_ops.size();
     uint32_t top = 0;  // largest hint (0: none of the ops carries one)
     bool tr = false;
-    for (const auto& o : tiny) {
-        top = std::max(top, o.order);
-        tr = tr || (o.flags & COSTA_TILE_TRANSPOSE);
+    for (const auto* o : wave_ops) {
+        top = std::max(top, o->order);
+        tr = tr || (o->flags & COSTA_TILE_TRANSPOSE);
     }
     const int mode = kn.sort == 4 ? (tr || top == 0 ? 2 : 3) : kn.sort == 3 && top == 0 ? 2 : kn.sort;
-    work_split w;
-    w.n_large = int64_t(work.size());
-    w.n_small = int64_t(small.size());
-    w.tiny_first = int64_t(ordered.size());
-    w.n_tiny = int64_t(tiny.size());
-    work.insert(work.end(), small.begin(), small.end());
-    if (mode == 3 && size_t(top) <= 4 * tiny.size() + 1024) {
-        // the planner's hints are ranks within the list: a stable counting sort, straight into
-        // the ordered list
+    std::vector<uint32_t> perm(nw);
+    if (mode == 3 && size_t(top) <= 4 * nw + 1024) {
+        // the planner's hints are ranks within the list: a stable counting sort
         std::vector<uint32_t> at(size_t(top) + 2, 0);
-        for (const auto& o : tiny) ++at[size_t(o.order) + 1];
+        for (const auto* o : wave_ops) ++at[size_t(o->order) + 1];
         for (size_t k = 1; k < at.size(); ++k) at[k] += at[k - 1];
-        const size_t base = ordered.size();
-        ordered.resize(base + tiny.size());
-        for (const auto& o : tiny) ordered[base + at[o.order]++] = o;
-        return w;
-    }
-    if (mode == 2 && !tiny.empty()) {
+        for (size_t i = 0; i < nw; ++i) perm[at[wave_ops[i]->order]++] = uint32_t(i);
+    } else if (mode == 2 && nw > 0) {
         // by destination address: a stable LSD radix sort of the element offsets from the lowest
-        // destination (14-bit digits, only as many passes as the span needs), straight into the
-        // ordered list
+        // destination (14-bit digits, only as many passes as the span needs)
         uint64_t lo = ~uint64_t(0), hi = 0;
-        for (const auto& o : tiny) {
-            lo = std::min(lo, o.dst);
-            hi = std::max(hi, o.dst);
+        for (const auto* o : wave_ops) {
+            lo = std::min(lo, o->dst);
+            hi = std::max(hi, o->dst);
         }
-        const size_t n = tiny.size();
-        std::vector<uint64_t> key(n), key2(n);
-        std::vector<uint32_t> idx(n), idx2(n);
-        for (size_t i = 0; i < n; ++i) {
-            key[i] = (tiny[i].dst - lo) / uint64_t(E);
-            idx[i] = uint32_t(i);
+        std::vector<uint64_t> key(nw), key2(nw);
+        std::vector<uint32_t> idx2(nw);
+        for (size_t i = 0; i < nw; ++i) {
+            key[i] = (wave_ops[i]->dst - lo) / uint64_t(E);
+            perm[i] = uint32_t(i);
         }
         const uint64_t span = (hi - lo) / uint64_t(E);
         constexpr int B = 14;
         std::vector<uint32_t> at((1 << B) + 1);
         for (int shift = 0; shift == 0 || (shift < 64 && (span >> shift) != 0); shift += B) {
             std::fill(at.begin(), at.end(), 0u);
-            for (size_t i = 0; i < n; ++i) ++at[((key[i] >> shift) & ((1 << B) - 1)) + 1];
+            for (size_t i = 0; i < nw; ++i) ++at[((key[i] >> shift) & ((1 << B) - 1)) + 1];
             for (int d = 1; d <= (1 << B); ++d) at[d] += at[d - 1];
-            for (size_t i = 0; i < n; ++i) {
+            for (size_t i = 0; i < nw; ++i) {
                 const uint32_t p = at[(key[i] >> shift) & ((1 << B) - 1)]++;
                 key2[p] = key[i];
-                idx2[p] = idx[i];
+                idx2[p] = perm[i];
             }
             key.swap(key2);
-            idx.swap(idx2);
+            perm.swap(idx2);
         }
-        const size_t base = ordered.size();
-        ordered.resize(base + n);
-        for (size_t i = 0; i < n; ++i) ordered[base + i] = tiny[idx[i]];
-        return w;
-    }
-    if (mode >= 1 && mode <= 3) {  // sort (key, index) pairs: stable, and cheap to move
-        std::vector<std::pair<uint64_t, uint32_t>> key(tiny.size());
-        for (size_t i = 0; i < tiny.size(); ++i)
-            key[i] = {mode == 1 ? tiny[i].src : mode == 2 ? tiny[i].dst : tiny[i].order,
-                      uint32_t(i)};
+    } else if (mode >= 1 && mode <= 3) {  // sort (key, index) pairs: stable
+        std::vector<std::pair<uint64_t, uint32_t>> key(nw);
+        for (size_t i = 0; i < nw; ++i) {
+            const costa_tile_op_t& o = *wave_ops[i];
+            key[i] = {mode == 1 ? o.src : mode == 2 ? o.dst : o.order, uint32_t(i)};
+        }
         std::sort(key.begin(), key.end());
-        std::vector<costa_tile_op_t> sorted(tiny.size());
-        for (size_t i = 0; i < key.size(); ++i) sorted[i] = tiny[key[i].second];
-        tiny.swap(sorted);
+        for (size_t i = 0; i < nw; ++i) perm[i] = key[i].second;
+    } else {
+        for (size_t i = 0; i < nw; ++i) perm[i] = uint32_t(i);
     }
-    ordered.insert(ordered.end(), tiny.begin(), tiny.end());
+    // pieces: count per op, scan, fill (host threads for long lists)
+    std::vector<wave_grid> grid(nw);
+    std::vector<size_t> at_piece(nw + 1, 0);
+    host_parallel(nw, [&](size_t b, size_t e) {
+        for (size_t i = b; i < e; ++i) grid[i] = wave_pieces(*wave_ops[perm[i]], E);
+    });
+    for (size_t i = 0; i < nw; ++i)
+        at_piece[i + 1] = at_piece[i] + size_t(grid[i].nfc * grid[i].nsc);
+    work_split w;
+    w.n_large = int64_t(work.size());
+    w.n_small = int64_t(small.size());
+    w.tiny_first = int64_t(ordered.size());
+    w.n_tiny = int64_t(at_piece[nw]);
+    work.insert(work.end(), small.begin(), small.end());
+    const size_t base = ordered.size();
+    ordered.resize(base + at_piece[nw]);
+    host_parallel(nw, [&](size_t b, size_t e) {
+        for (size_t i = b; i < e; ++i)
+            emit_pieces(*wave_ops[perm[i]], E, grid[i], &ordered[base + at_piece[i]]);
+    });
     return w;
 }
 
