@@ -416,9 +416,11 @@ void host_parallel(size_t n, F fn) {
 
 namespace {
 struct wave_knobs {  // defaults, overridable for tuning runs
-    int policy = 1;  // COSTA_WAVE_POLICY 0: only ops within the budget take the wave path (the
+    int policy = 2;  // COSTA_WAVE_POLICY 0: only ops within the budget take the wave path (the
                      // rest: 256-thread small shape); 1: every op below the large threshold;
-                     // 2: also large ops that are not 16-byte aligned on both sides
+                     // 2: also large ops that are not 16-byte aligned on both sides (r11: cfg 5
+                     // geometry with doubled edges 3.41 -> 4.14 TB/s 'N', 3.47 -> 3.88 'T',
+                     // the rest unchanged; profiles/r11/c5_align_policy*.log)
     int sort = 4;    // COSTA_TINY_SORT 0: list order, 1: by source, 2: by destination address,
                      // 3: by the planner's locality hint (costa_tile_op_t::order), 4: 3 for
                      // copy-only lists, 2 for lists that transpose (cfg 5 'T' 3.88 against

@@ -39,6 +39,10 @@ def layout(rs, cs, buf):
     return costa.custom_layout(len(rs) - 1, len(cs) - 1, rs, cs, own, blocks, "C", costa.FLOAT), off
 
 
+OP = os.environ.get("PROBE_OP", "N")  # 'T': alpha=-0.5, beta=2 (cfg 5's 'T' variant)
+AL, BE = (1.0, 0.0) if OP == "N" else (-0.5, 2.0)
+
+
 def run(q, scale=1.0, qc=None):
     qc = q if qc is None else qc  # C's edges may be rounded differently from A's
     ars, acs = splits(0xC5A1, 8, 96, q, scale), splits(0xC5A2, 8, 96, q, scale)
@@ -49,19 +53,19 @@ def run(q, scale=1.0, qc=None):
     LC, _ = layout(crs, ccs, C)
     comm = costa.Comm.self(0)
     for _ in range(3):
-        costa.transform_async(LA, LC, comm, "N", 1.0, 0.0)
+        costa.transform_async(LA, LC, comm, OP, AL, BE)
     costa.synchronize(comm)
     costa.set_profiling(True)
     costa.get_stats(reset=True)
     steps = 10
     for _ in range(steps):
-        costa.transform_async(LA, LC, comm, "N", 1.0, 0.0)
+        costa.transform_async(LA, LC, comm, OP, AL, BE)
     costa.synchronize(comm)
     st = costa.get_stats(reset=True)
     costa.set_profiling(False)
     p = costa.plan_export([LA], [LC], 0, 1)
     ms = st["local_ms"] / steps
-    print(json.dumps({"edge_multiple_A": q, "edge_multiple_C": qc, "edge_scale": scale,
+    print(json.dumps({"op": OP, "edge_multiple_A": q, "edge_multiple_C": qc, "edge_scale": scale,
                       "tiles": int(p.local_ops.size),
                       "kernel_ms": round(ms, 4),
                       "GBps": round(st["local_bytes"] / steps / (ms * 1e-3) / 1e9, 1)}), flush=True)
