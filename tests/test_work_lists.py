@@ -1,0 +1,26 @@
+"""Wavefront work lists (engine.cpp build_work) on BASELINE cfg 5's geometry, on the CPU: every
+piece within the wavefront budget, the pieces of each op inside it and adding up to it, copy lists
+in locality-hint order, transposing lists in destination order, and two builds identical (the
+cut runs on several host threads).  The checks live in tools/work_check.cpp, built here with g++
+against the in-tree libcosta_amd.so; block addresses are never dereferenced."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "costa_amd", "lib")
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no g++")
+def test_work_lists_cfg5(tmp_path):
+    if not os.path.exists(os.path.join(LIB, "libcosta_amd.so")):
+        pytest.skip("libcosta_amd.so not built (run __graft_entry__.build())")
+    exe = tmp_path / "work_check"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I" + os.path.join(ROOT, "include"),
+                    "-I" + os.path.join(ROOT, "costa_amd", "csrc"),
+                    os.path.join(ROOT, "tools", "work_check.cpp"), "-L" + LIB, "-lcosta_amd",
+                    "-Wl,-rpath," + LIB, "-o", str(exe)], check=True, timeout=300)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
