@@ -33,13 +33,16 @@ def layout(rs, cs, buf):
     for i in range(len(rs) - 1):
         for j in range(len(cs) - 1):
             rows, cols = rs[i + 1] - rs[i], cs[j + 1] - cs[j]
-            blocks.append((buf.data_ptr() + 4 * off, rows, i, j))
+            blocks.append((buf.data_ptr() + ES * off, rows, i, j))
             off += (rows * cols + 63) // 64 * 64
     own = np.zeros((len(rs) - 1, len(cs) - 1), np.int64)
-    return costa.custom_layout(len(rs) - 1, len(cs) - 1, rs, cs, own, blocks, "C", costa.FLOAT), off
+    return costa.custom_layout(len(rs) - 1, len(cs) - 1, rs, cs, own, blocks, "C", CDT), off
 
 
 OP = os.environ.get("PROBE_OP", "N")  # 'T': alpha=-0.5, beta=2 (cfg 5's 'T' variant)
+# PROBE_DTYPE=double: the same geometry in fp64; PROBE_FIRST=1: only the first (cfg 5) case
+TDT, CDT, ES = ((torch.float64, costa.DOUBLE, 8) if os.environ.get("PROBE_DTYPE") == "double"
+                else (torch.float32, costa.FLOAT, 4))
 AL, BE = (1.0, 0.0) if OP == "N" else (-0.5, 2.0)
 
 
@@ -47,8 +50,8 @@ def run(q, scale=1.0, qc=None):
     qc = q if qc is None else qc  # C's edges may be rounded differently from A's
     ars, acs = splits(0xC5A1, 8, 96, q, scale), splits(0xC5A2, 8, 96, q, scale)
     crs, ccs = splits(0xC5A3, 16, 160, qc, scale), splits(0xC5A4, 16, 160, qc, scale)
-    A = torch.rand(N * N + (len(ars) * len(acs)) * 64, dtype=torch.float32, device="cuda")
-    C = torch.zeros(N * N + (len(crs) * len(ccs)) * 64, dtype=torch.float32, device="cuda")
+    A = torch.rand(N * N + (len(ars) * len(acs)) * 64, dtype=TDT, device="cuda")
+    C = torch.zeros(N * N + (len(crs) * len(ccs)) * 64, dtype=TDT, device="cuda")
     LA, _ = layout(ars, acs, A)
     LC, _ = layout(crs, ccs, C)
     comm = costa.Comm.self(0)
@@ -71,6 +74,7 @@ def run(q, scale=1.0, qc=None):
                       "GBps": round(st["local_bytes"] / steps / (ms * 1e-3) / 1e9, 1)}), flush=True)
 
 
-for q, scale, qc in ((1, 1.0, 1), (4, 1.0, 4), (32, 1.0, 32), (1, 1.35, 1), (1, 2.0, 1),
-                     (32, 0.75, 32), (32, 1.0, 1), (1, 1.0, 32)):
+CASES = ((1, 1.0, 1), (4, 1.0, 4), (32, 1.0, 32), (1, 1.35, 1), (1, 2.0, 1),
+                     (32, 0.75, 32), (32, 1.0, 1), (1, 1.0, 32))
+for q, scale, qc in CASES[:1] if os.environ.get("PROBE_FIRST") else CASES:
     run(q, scale, qc)
