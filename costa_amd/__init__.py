@@ -131,6 +131,7 @@ def lib():
         "costa_hip_custom_layout": (i, [i, i, i, C.POINTER(i), C.POINTER(i), C.POINTER(i), i,
                                         C.POINTER(_Block), c, C.POINTER(vp)]),
         "costa_hip_layout_destroy": (None, [vp]),
+        "costa_hip_layout_reorder_ranks": (i, [vp, C.POINTER(i), i]),
         "costa_hip_layout_num_blocks": (i, [vp]),
         "costa_hip_layout_block": (i, [vp, i, C.POINTER(i), C.POINTER(i), C.POINTER(i),
                                        C.POINTER(i), C.POINTER(vp), C.POINTER(i)]),
@@ -233,6 +234,13 @@ class Layout:
         _check(lib().costa_hip_layout_block(self._h, i, *[C.byref(x) for x in v], C.byref(d),
                                             C.byref(ld)))
         return BlockInfo(v[0].value, v[1].value, v[2].value, v[3].value, d.value or 0, ld.value)
+
+    def reorder_ranks(self, reordering: Sequence[int]):
+        """Rank relabelling: owner(i, j) -> reordering[owner(i, j)] (reference
+        grid_layout::reorder_ranks, grid_layout.hpp:32-34)."""
+        p = np.ascontiguousarray(reordering, dtype=np.int32)
+        _check(lib().costa_hip_layout_reorder_ranks(self._h, p.ctypes.data_as(C.POINTER(C.c_int)),
+                                                    int(p.size)))
 
     def close(self):
         if self._h and self._h.value:

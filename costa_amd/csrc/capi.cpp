@@ -4,6 +4,7 @@
 
 #include <costa/transform.hpp>
 
+#include <algorithm>
 #include <cctype>
 #include <complex>
 #include <cstring>
@@ -11,6 +12,7 @@
 
 struct costa_layout_s {
     costa::engine::elayout e;
+    std::vector<int> base_owners;  // owners before a rank relabelling (empty: none applied)
 };
 struct costa_comm_s {
     costa::engine::comm* c = nullptr;
@@ -184,6 +186,30 @@ int costa_hip_custom_layout(costa_dtype_t dtype, int rowblocks, int colblocks, c
 }
 
 void costa_hip_layout_destroy(costa_layout_t layout) { delete layout; }
+
+int costa_hip_layout_reorder_ranks(costa_layout_t layout, const int* reordering, int n) {
+    return guarded([&] {
+        if (!layout || n < 0 || (n > 0 && !reordering))
+            throw costa::engine::error(COSTA_ERR_ARG, "null argument");
+        auto& e = layout->e;
+        if (layout->base_owners.empty()) layout->base_owners = e.owners;
+        const std::vector<int>& base = layout->base_owners;
+        int n_base = 0;
+        for (int o : base) n_base = std::max(n_base, o + 1);
+        // the reference replaces the relabelling (assigned_grid2D::reorder_ranks, grid2D.hpp:219-221)
+        // and maps every owner through it (owner(), grid2D.hpp:183-187)
+        if (n > 0 && n < n_base)
+            throw costa::engine::error(COSTA_ERR_ARG, "costa: reordering shorter than the ranks");
+        for (int k = 0; k < n; ++k)
+            if (reordering[k] < 0 || reordering[k] >= n)
+                throw costa::engine::error(COSTA_ERR_ARG, "costa: reordering out of range");
+        std::vector<int> owners(base.size());
+        for (size_t k = 0; k < base.size(); ++k) owners[k] = n > 0 ? reordering[base[k]] : base[k];
+        e.owners = std::move(owners);
+        e.n_ranks = std::max(e.n_ranks, n);
+        e.hash = costa::engine::layout_hash(e);  // a relabelled handle is a different layout
+    });
+}
 
 int costa_hip_layout_num_blocks(costa_layout_t layout) {
     return layout ? int(layout->e.blocks.size()) : -1;

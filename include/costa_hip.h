@@ -17,6 +17,7 @@
  *   costa_hip_transform_batch       costa::transform<T>(vector<layout_ref>..., trans*, alpha*, beta*, comm)
  *                                   and costa::transformer<T>::transform()
  *                                                                  transform.hpp:38-43, transformer.hpp:8-62
+ *   costa_hip_layout_reorder_ranks  grid_layout<T>::reorder_ranks   grid2grid/grid_layout.hpp:32-34
  *   costa_hip_copy_and_transform    costa::memory::copy_and_transform<T>
  *                                                                  src/costa/grid2grid/memory_utils.hpp:339-412
  *   costa_hip_execute_tiles         the pack / local / unpack loops
@@ -120,6 +121,13 @@ int costa_hip_custom_layout(costa_dtype_t dtype, int rowblocks, int colblocks, c
                             const int* colsplit, const int* owners, int nlocalblocks,
                             const costa_block_t* localblocks, char ordering, costa_layout_t* out);
 void costa_hip_layout_destroy(costa_layout_t layout);
+/* rank relabelling: owner(i, j) becomes reordering[owner(i, j)] (replaces any earlier one;
+ * n = 0 restores the identity).  Replaces grid_layout<T>::reorder_ranks
+ * (src/costa/grid2grid/grid_layout.hpp:32-34, grid2D.hpp:183-187, 219-221); the permutation
+ * usually comes from costa::optimal_reordering (<costa/grid2grid/ranks_reordering.hpp>).  As in
+ * the reference's README (README.md:343-362), rank r's relabelled target layout holds the local
+ * blocks of rank reordering[r]. */
+int costa_hip_layout_reorder_ranks(costa_layout_t layout, const int* reordering, int n);
 /* number of local blocks / the i-th block (global intervals, data pointer, ld) */
 int costa_hip_layout_num_blocks(costa_layout_t layout);
 int costa_hip_layout_block(costa_layout_t layout, int i, int* row_start, int* row_end,

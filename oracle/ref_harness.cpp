@@ -152,11 +152,22 @@ int run_case(std::istream& in, const std::string& out, int rank, int P) {
     std::vector<T> alpha(np), beta(np);
     std::vector<int> noscale(np);
     std::vector<uint64_t> seedA(np), seedC(np);
+    std::vector<std::vector<int>> relabel(np);  // target-layout rank relabelling (may be empty)
     std::vector<lspec> A, C;
     for (int p = 0; p < npairs; ++p) {
         double ar, ai, br, bi;
         in >> tok >> trans[size_t(p)] >> tok >> ar >> ai >> tok >> br >> bi >> tok >>
             noscale[size_t(p)] >> tok >> seedA[size_t(p)] >> tok >> seedC[size_t(p)];
+        // optional "relabelC k p0 .. p(k-1)": the target layout of rank r holds the local
+        // blocks of rank p[r] and its grid is relabelled by reorder_ranks(p) (README.md:343-362,
+        // grid_layout.hpp:32-34)
+        in >> std::ws;
+        if (in.peek() == 'r') {
+            int k;
+            in >> tok >> k;
+            relabel[size_t(p)].resize(size_t(k));
+            for (auto& x : relabel[size_t(p)]) in >> x;
+        }
         if constexpr (std::is_same<T, std::complex<double>>::value ||
                       std::is_same<T, std::complex<float>>::value) {
             alpha[size_t(p)] = T(ar, ai);
@@ -175,12 +186,15 @@ int run_case(std::istream& in, const std::string& out, int rank, int P) {
     for (int p = 0; p < npairs; ++p) {
         auto& a = abuf[size_t(p)];
         auto& c = cbuf[size_t(p)];
+        auto& rl = relabel[size_t(p)];
+        const int crank = rl.empty() ? rank : rl[size_t(rank)];
         a.resize(size_t(buf_size(A[size_t(p)], rank)));
-        c.resize(size_t(buf_size(C[size_t(p)], rank)));
+        c.resize(size_t(buf_size(C[size_t(p)], crank)));
         for (size_t k = 0; k < a.size(); ++k) a[k] = gen<T>(seedA[size_t(p)], rank, k);
         for (size_t k = 0; k < c.size(); ++k) c[k] = gen<T>(seedC[size_t(p)], rank, k);
         la.push_back(build<T>(A[size_t(p)], a, rank));
-        lc.push_back(build<T>(C[size_t(p)], c, rank));
+        lc.push_back(build<T>(C[size_t(p)], c, crank));
+        if (!rl.empty()) lc.back().reorder_ranks(rl);
     }
     if (npairs == 1) {
         if (noscale[0])

@@ -187,6 +187,12 @@ class Pair:
     noscale: bool = False  # use the no-scale overload transform(A, C, comm)
     seedA: int = 0xC057A0
     seedC: int = 0xC057C0
+    # rank relabelling of the target layout (README.md:343-362): rank r's C layout holds the
+    # local blocks of rank relabel[r] and is relabelled by reorder_ranks(relabel)
+    relabel: list | None = None
+
+    def c_rank(self, rank):
+        return rank if self.relabel is None else int(self.relabel[rank])
 
 
 @dataclass
@@ -205,8 +211,11 @@ class Case:
         out = [f"dtype {self.dtype}", f"npairs {len(self.pairs)}"]
         for p in self.pairs:
             a, b = complex(p.alpha), complex(p.beta)
-            out.append(f"trans {p.trans} alpha {a.real!r} {a.imag!r} beta {b.real!r} {b.imag!r} "
-                       f"noscale {int(p.noscale)} seedA {p.seedA} seedC {p.seedC}")
+            line = (f"trans {p.trans} alpha {a.real!r} {a.imag!r} beta {b.real!r} {b.imag!r} "
+                    f"noscale {int(p.noscale)} seedA {p.seedA} seedC {p.seedC}")
+            if p.relabel is not None:
+                line += f" relabelC {len(p.relabel)} " + " ".join(map(str, p.relabel))
+            out.append(line)
             out.append(p.A.spec(self.P).rstrip("\n"))
             out.append(p.C.spec(self.P).rstrip("\n"))
         return "\n".join(out) + "\n"
@@ -215,8 +224,30 @@ class Case:
     def inputs(self, pair_idx, rank):
         p = self.pairs[pair_idx]
         a = oracle.gen(self.dtype, p.seedA, rank, p.A.buf_elems(rank, self.P))
-        c = oracle.gen(self.dtype, p.seedC, rank, p.C.buf_elems(rank, self.P))
+        c = oracle.gen(self.dtype, p.seedC, rank, p.C.buf_elems(p.c_rank(rank), self.P))
         return a, c
+
+    # ---- the product's layouts of one rank (the C layout relabelled where the pair says so)
+    def layout_A(self, k, rank, ptr):
+        return self.pairs[k].A.make_layout(rank, ptr, self.P, self.dtype)
+
+    def layout_C(self, k, rank, ptr):
+        p = self.pairs[k]
+        L = p.C.make_layout(p.c_rank(rank), ptr, self.P, self.dtype)
+        if p.relabel is not None:
+            L.reorder_ranks(p.relabel)
+        return L
+
+    def geom_C(self, k):
+        """oracle geometry of the target; a relabelled cell of owner o lives on rank relabel[o]"""
+        p = self.pairs[k]
+        rs, cs, tab, cm = p.C.geom(self.P)
+        if p.relabel is not None:
+            t = np.array(tab, np.int64).reshape(-1, 3)
+            own = t[:, 0] >= 0
+            t[own, 0] = np.asarray(p.relabel, np.int64)[t[own, 0]]
+            tab = t.reshape(-1)
+        return rs, cs, tab, cm
 
     # ---- oracle
     def expected(self):
@@ -228,7 +259,7 @@ class Case:
             al = 1 if p.noscale else p.alpha
             be = 0 if p.noscale else p.beta
             tr = "N" if p.noscale else p.trans
-            oracle.transform(self.dtype, tr, al, be, p.A.geom(self.P), A, p.C.geom(self.P), Cb)
+            oracle.transform(self.dtype, tr, al, be, p.A.geom(self.P), A, self.geom_C(k), Cb)
             res.append(Cb)
         return res
 

@@ -9,6 +9,15 @@ Sources of the named cases (eth-cscs/COSTA):
   sweep_*       seeded random sweep over grids x blocks x op x alpha/beta x orderings x dtypes,
                 submatrices (ia, ja != 1), rank sources, ld padding, custom irregular grids
   batch_*       transformer<T> with several layout pairs in one exchange (transformer.hpp:8-62)
+  cfg3_*        BASELINE configs[2] geometry scaled down: pxgemr2d fp64 2x2 'R' -> 4x1 'R',
+                128^2 blocks, no-scale overload, 4 ranks (also with ia, ja != 1 and rank sources)
+  cfg4_*        BASELINE configs[3] geometry: pztranu / pztranc complex<double> on a 2x4 'R' grid,
+                128^2 blocks, alpha = 0.75-0.5i, beta = 1.25+0.25i, 8 ranks
+  cfg5_*        BASELINE configs[4] geometry: custom layouts, A edges 8-96, C edges 16-160,
+                owners uniform over 8 ranks, fp32 'N' (alpha 1, beta 0) and 'T' (-0.5, 2)
+  relabel_*     transforms onto rank-relabelled targets: grid_layout::reorder_ranks
+                (grid_layout.hpp:32-34) with the permutation optimal_reordering gives, applied as
+                README.md:343-362 prescribes
 """
 from __future__ import annotations
 
@@ -109,8 +118,84 @@ def _sweep(n_cases=32, seed=20251015):
     return cases
 
 
+def _edges(seed, n, lo, hi):
+    r = np.random.default_rng(seed)
+    s = [0]
+    while s[-1] < n:
+        s.append(min(n, s[-1] + int(r.integers(lo, hi + 1))))
+    return s
+
+
+def _baseline_geometries():
+    """BASELINE.json configs[2..4] at fixture size, on their own rank counts (4 and 8)."""
+    cases = []
+    # cfg 3: pxgemr2d = the no-scale overload, 2x2 -> 4x1 row-major grids, ragged last blocks
+    cases.append(Case("cfg3_remap", D, [Pair(BC(1000, 1100, 128, 128, pm=2, pn=2, order="R"),
+                                             BC(1000, 1100, 128, 128, pm=4, pn=1, order="R"),
+                                             noscale=True, seedA=0x3A, seedC=0x3C)]))
+    cases.append(Case("cfg3_remap_sub", D, [Pair(
+        BC(1100, 1200, 128, 128, 37, 51, 1000, 1100, 2, 2, "R", 1, 0, "C", 3),
+        BC(1060, 1130, 128, 128, 11, 5, 1000, 1100, 4, 1, "R", 2, 0, "C", 0),
+        noscale=True, seedA=0x3B, seedC=0x3D)]))
+    # cfg 4: pztranu ('T') and pztranc ('C'); sub(A) is n x m, sub(C) m x n
+    m, n = 1200, 1100
+    for op in ("T", "C"):
+        cases.append(Case(f"cfg4_{op}", Z, [Pair(BC(n, m, 128, 128, pm=2, pn=4, order="R"),
+                                                BC(m, n, 128, 128, pm=2, pn=4, order="R"),
+                                                op, 0.75 - 0.5j, 1.25 + 0.25j,
+                                                seedA=0x4A, seedC=0x4C)]))
+    # cfg 5: irregular custom grids, every block its own owner draw over 8 ranks
+    m, n = 2048, 1920
+    for op, al, be in (("N", 1.0, 0.0), ("T", -0.5, 2.0)):
+        am, an = (n, m) if op == "T" else (m, n)
+        ars, acs = _edges(0xC5A1, am, 8, 96), _edges(0xC5A2, an, 8, 96)
+        crs, ccs = _edges(0xC5A3, m, 16, 160), _edges(0xC5A4, n, 16, 160)
+        ao = np.random.default_rng(0xC5A5).integers(0, 8, (len(ars) - 1, len(acs) - 1))
+        co = np.random.default_rng(0xC5A6).integers(0, 8, (len(crs) - 1, len(ccs) - 1))
+        cases.append(Case(f"cfg5_{op}", S, [Pair(Custom(ars, acs, ao, ord="C"),
+                                                Custom(crs, ccs, co, ord="C"), op, al, be,
+                                                seedA=0x5A, seedC=0x5C)], P=8))
+    return cases
+
+
+def _split(n, b):
+    return list(range(0, n, b)) + [n]
+
+
+def _relabelled():
+    """Targets relabelled by involutions of the kind optimal_reordering proposes (pairs of ranks
+    swapped; relabel_readme uses the reference's own proposal for that geometry,
+    tests/golden/relabel.json)."""
+    cases = []
+    # README.md:461-470 geometry (2x4 'R' -> 4x2 'C' ranks), scaled to 1000^2 / 100^2 blocks
+    cases.append(Case("relabel_readme", D, [Pair(
+        BC(1000, 1000, 100, 100, pm=2, pn=4, order="R"), BC(1000, 1000, 100, 100, pm=4, pn=2, order="C"),
+        noscale=True, seedA=0x7A, seedC=0x7C, relabel=[0, 1, 2, 6, 4, 5, 3, 7])]))
+    # the same grid with ranks permuted: relabelled, every tile stays local
+    rs = _split(1000, 50)
+    own = (np.arange(len(rs) - 1)[:, None] % 2) * 2 + (np.arange(len(rs) - 1)[None, :] % 2)
+    sigma = np.array([2, 0, 3, 1])
+    cases.append(Case("relabel_permuted", D, [Pair(
+        BC(1000, 1000, 50, 50, pm=2, pn=2, order="R"), Custom(rs, rs, sigma[own], ord="C"),
+        "N", 0.75, 0.0, seedA=0x7B, seedC=0x7D, relabel=[2, 3, 0, 1])], P=4))
+    # 2x3 -> 6x1 remap, complex<double> with alpha, beta
+    cases.append(Case("relabel_remap", Z, [Pair(
+        BC(1200, 900, 32, 40, pm=2, pn=3, order="R"), BC(1200, 900, 25, 35, pm=6, pn=1, order="R"),
+        "N", 0.75 - 0.5j, 1.25 + 0.25j, seedA=0x7E, seedC=0x7F, relabel=[0, 5, 2, 3, 4, 1])]))
+    # irregular custom grids over 5 ranks, complex<float> 'T'
+    m, n = 700, 500
+    a_rs, a_cs = _edges(0x71, n, 10, 90), _edges(0x72, m, 10, 90)
+    c_rs, c_cs = _edges(0x73, m, 20, 120), _edges(0x74, n, 20, 120)
+    ao = np.random.default_rng(0x75).integers(0, 5, (len(a_rs) - 1, len(a_cs) - 1))
+    co = np.random.default_rng(0x76).integers(0, 5, (len(c_rs) - 1, len(c_cs) - 1))
+    cases.append(Case("relabel_custom_T", CF, [Pair(
+        Custom(a_rs, a_cs, ao, ord="R"), Custom(c_rs, c_cs, co, ord="C"), "T",
+        0.75 - 0.5j, 1.25 + 0.25j, seedA=0x77, seedC=0x78, relabel=[0, 3, 4, 1, 2])], P=5))
+    return cases
+
+
 def all_cases():
-    return _named() + _sweep()
+    return _named() + _sweep() + _baseline_geometries() + _relabelled()
 
 
 def by_name():

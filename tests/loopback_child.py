@@ -36,8 +36,8 @@ def main():
             continue
         n += 1
         bufs = [tuple(dev(x) for x in case.inputs(k, 0)) for k in range(len(case.pairs))]
-        As = [p.A.make_layout(0, bufs[k][0].data_ptr(), 1, case.dtype) for k, p in enumerate(case.pairs)]
-        Cs = [p.C.make_layout(0, bufs[k][1].data_ptr(), 1, case.dtype) for k, p in enumerate(case.pairs)]
+        As = [case.layout_A(k, 0, bufs[k][0].data_ptr()) for k in range(len(case.pairs))]
+        Cs = [case.layout_C(k, 0, bufs[k][1].data_ptr()) for k in range(len(case.pairs))]
         eff = [case.effective(k) for k in range(len(case.pairs))]
         costa.transform_batch(As, Cs, comm, [e[0] for e in eff], [e[1] for e in eff],
                               [e[2] for e in eff])
@@ -75,10 +75,8 @@ def main():
             if case.P != 1:
                 continue
             bufs = [case.inputs(k, 0) for k in range(len(case.pairs))]
-            As = [p.A.make_layout(0, bufs[k][0].ctypes.data, 1, case.dtype)
-                  for k, p in enumerate(case.pairs)]
-            Cs = [p.C.make_layout(0, bufs[k][1].ctypes.data, 1, case.dtype)
-                  for k, p in enumerate(case.pairs)]
+            As = [case.layout_A(k, 0, bufs[k][0].ctypes.data) for k in range(len(case.pairs))]
+            Cs = [case.layout_C(k, 0, bufs[k][1].ctypes.data) for k in range(len(case.pairs))]
             eff = [case.effective(k) for k in range(len(case.pairs))]
             costa.transform_batch(As, Cs, comm, [e[0] for e in eff], [e[1] for e in eff],
                                   [e[2] for e in eff])

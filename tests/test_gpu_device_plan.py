@@ -52,10 +52,8 @@ def both(costa, As, Cs, rank, P, trans, alpha, beta):
 def test_device_plan_equals_host_golden(gpu, case):
     eff = [case.effective(k) for k in range(len(case.pairs))]
     for r in range(case.P):
-        As = [p.A.make_layout(r, (1 << 40) + (k << 34), case.P, case.dtype)
-              for k, p in enumerate(case.pairs)]
-        Cs = [p.C.make_layout(r, (1 << 41) + (k << 34), case.P, case.dtype)
-              for k, p in enumerate(case.pairs)]
+        As = [case.layout_A(k, r, (1 << 40) + (k << 34)) for k in range(len(case.pairs))]
+        Cs = [case.layout_C(k, r, (1 << 41) + (k << 34)) for k in range(len(case.pairs))]
         both(gpu, As, Cs, r, case.P, [e[0] for e in eff], [e[1] for e in eff],
              [e[2] for e in eff])
 

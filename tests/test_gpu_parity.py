@@ -77,8 +77,8 @@ def _run_single_rank(costa, case, on_device=True):
         a, c = dbufs[k]
         pa = a.data_ptr() if on_device else a.ctypes.data
         pc = c.data_ptr() if on_device else c.ctypes.data
-        As.append(p.A.make_layout(0, pa, 1, case.dtype))
-        Cs.append(p.C.make_layout(0, pc, 1, case.dtype))
+        As.append(case.layout_A(k, 0, pa))
+        Cs.append(case.layout_C(k, 0, pc))
     eff = [case.effective(k) for k in range(len(case.pairs))]
     comm = costa.Comm.self(0)
     costa.transform_batch(As, Cs, comm, [e[0] for e in eff], [e[1] for e in eff],
@@ -97,10 +97,8 @@ def _run_emulated_ranks(costa, case):
     eff = [case.effective(k) for k in range(len(case.pairs))]
     plans, keep = [], []
     for r in range(P):
-        As = [p.A.make_layout(r, bufs[r][k][0].data_ptr(), P, case.dtype)
-              for k, p in enumerate(case.pairs)]
-        Cs = [p.C.make_layout(r, bufs[r][k][1].data_ptr(), P, case.dtype)
-              for k, p in enumerate(case.pairs)]
+        As = [case.layout_A(k, r, bufs[r][k][0].data_ptr()) for k in range(len(case.pairs))]
+        Cs = [case.layout_C(k, r, bufs[r][k][1].data_ptr()) for k in range(len(case.pairs))]
         keep.append((As, Cs))
         plans.append(costa.plan_export(As, Cs, r, P, [e[0] for e in eff], [e[1] for e in eff],
                                        [e[2] for e in eff]))

@@ -1,4 +1,4 @@
-"""The N > 1 path on the CPU: one process per rank (torch.distributed, gloo, world size 2-4).
+"""The N > 1 path on the CPU: one process per rank (torch.distributed, gloo, world size 2-8).
 
 Each rank plans its own transform with the product planner (costa_hip_plan_export), packs with
 the oracle executor, exchanges the packed segments with all_to_all_single using exactly the
@@ -17,7 +17,8 @@ import torch.multiprocessing as mp  # noqa: E402
 
 from cases import all_cases  # noqa: E402
 
-CASES = {p: [c.name for c in all_cases() if c.P == p] for p in (2, 3, 4)}
+WORLDS = (2, 3, 4, 5, 6, 8)
+CASES = {p: [c.name for c in all_cases() if c.P == p] for p in WORLDS}
 
 
 def _free_port():
@@ -47,10 +48,8 @@ def _worker(rank, world, port, names, result_dir):
         dt = oracle.NP[case.dtype]
         E = np.dtype(dt).itemsize
         bufs = [case.inputs(k, rank) for k in range(len(case.pairs))]
-        As = [p.A.make_layout(rank, bufs[k][0].ctypes.data, world, case.dtype)
-              for k, p in enumerate(case.pairs)]
-        Cs = [p.C.make_layout(rank, bufs[k][1].ctypes.data, world, case.dtype)
-              for k, p in enumerate(case.pairs)]
+        As = [case.layout_A(k, rank, bufs[k][0].ctypes.data) for k in range(len(case.pairs))]
+        Cs = [case.layout_C(k, rank, bufs[k][1].ctypes.data) for k in range(len(case.pairs))]
         eff = [case.effective(k) for k in range(len(case.pairs))]
         plan = costa.plan_export(As, Cs, rank, world, [e[0] for e in eff], [e[1] for e in eff],
                                  [e[2] for e in eff])
@@ -77,9 +76,10 @@ def _worker(rank, world, port, names, result_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("world", WORLDS)
 def test_ranks_gloo(tmp_path, world):
-    """every golden case of `world` ranks (grids 1x2 .. 2x2, remaps, custom grids, batches)"""
+    """every golden case of `world` ranks (grids 1x2 .. 2x4, remaps, custom grids, batches,
+    BASELINE cfg 3 / 4 / 5 geometries, relabelled targets)"""
     names = CASES[world]
     assert names, f"no {world}-rank golden cases"
     mp.spawn(_worker, args=(world, _free_port(), names, str(tmp_path)), nprocs=world, join=True)

@@ -20,8 +20,8 @@ def _layouts(costa, case, rank, bufs):
     As, Cs = [], []
     for k, p in enumerate(case.pairs):
         a, c = bufs[k]
-        As.append(p.A.make_layout(rank, a.ctypes.data, case.P, case.dtype))
-        Cs.append(p.C.make_layout(rank, c.ctypes.data, case.P, case.dtype))
+        As.append(case.layout_A(k, rank, a.ctypes.data))
+        Cs.append(case.layout_C(k, rank, c.ctypes.data))
     return As, Cs
 
 
