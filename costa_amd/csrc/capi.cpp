@@ -2,6 +2,8 @@
 // (include/costa/transform.hpp).  No exception crosses the C boundary.
 #include "engine.hpp"
 
+#include <hip/hip_runtime.h>
+
 #include <costa/transform.hpp>
 
 #include <algorithm>
@@ -39,6 +41,25 @@ int guarded(F&& f) {
         g_last_error = "unknown error";
         return COSTA_ERR_INTERNAL;
     }
+}
+
+// Entry points that may switch the calling thread's HIP device (hipSetDevice to the
+// communicator's or the call's device) put the caller's current device back on the way out:
+// a process driving several GPUs keeps its own device selection across costa calls.
+struct device_restore {
+    int dev = -1;
+    device_restore() {
+        if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+    }
+    ~device_restore() {
+        if (dev >= 0) (void)hipSetDevice(dev);
+    }
+};
+
+template <typename F>
+int gpu_guarded(F&& f) {
+    device_restore keep;
+    return guarded(std::forward<F>(f));
 }
 
 using costa::engine::dtype_size;
@@ -158,7 +179,7 @@ int costa_hip_block_cyclic_layout(costa_dtype_t dtype, int m, int n, int block_m
                                                    p_n, rank_grid_ordering, rsrc, csrc,
                                                    static_cast<T*>(ptr), lld, data_ordering, rank);
             h->e = costa::engine::erase(L);
-            h->e.hash = costa::engine::layout_hash(h->e);  // handles are immutable
+            costa::engine::set_layout_hash(h->e);  // handles are immutable
         });
         *out = h.release();
     });
@@ -179,7 +200,7 @@ int costa_hip_custom_layout(costa_dtype_t dtype, int rowblocks, int colblocks, c
                                              reinterpret_cast<const costa::block_t*>(localblocks),
                                              ordering);
             h->e = costa::engine::erase(L);
-            h->e.hash = costa::engine::layout_hash(h->e);  // handles are immutable
+            costa::engine::set_layout_hash(h->e);  // handles are immutable
         });
         *out = h.release();
     });
@@ -207,7 +228,7 @@ int costa_hip_layout_reorder_ranks(costa_layout_t layout, const int* reordering,
         for (size_t k = 0; k < base.size(); ++k) owners[k] = n > 0 ? reordering[base[k]] : base[k];
         e.owners = std::move(owners);
         e.n_ranks = std::max(e.n_ranks, n);
-        e.hash = costa::engine::layout_hash(e);  // a relabelled handle is a different layout
+        costa::engine::set_layout_hash(e);  // a relabelled handle is a different layout
     });
 }
 
@@ -231,7 +252,7 @@ int costa_hip_layout_block(costa_layout_t layout, int i, int* row_start, int* ro
 }
 
 int costa_hip_comm_self(int device, costa_comm_t* out) {
-    return guarded([&] {
+    return gpu_guarded([&] {
         if (!out) throw costa::engine::error(COSTA_ERR_ARG, "null output handle");
         auto h = std::make_unique<costa_comm_s>();
         h->c = costa::engine::comm_self(device);
@@ -245,7 +266,7 @@ int costa_hip_comm_unique_id(unsigned char id[128]) {
 
 int costa_hip_comm_create(const unsigned char id[128], int nranks, int rank, int device,
                           costa_comm_t* out) {
-    return guarded([&] {
+    return gpu_guarded([&] {
         if (!out || !id) throw costa::engine::error(COSTA_ERR_ARG, "null argument");
         auto h = std::make_unique<costa_comm_s>();
         h->c = costa::engine::comm_create(id, nranks, rank, device);
@@ -269,7 +290,7 @@ int costa_hip_transform(costa_layout_t A, costa_layout_t C, char trans, const vo
 int costa_hip_transform_batch(int n, const costa_layout_t* A, const costa_layout_t* C,
                               const char* trans, const void* alpha, const void* beta,
                               costa_comm_t comm) {
-    return guarded([&] {
+    return gpu_guarded([&] {
         if (!comm || !alpha || !beta) throw costa::engine::error(COSTA_ERR_ARG, "null argument");
         auto jobs = make_jobs(n, A, C, trans, alpha, beta);
         costa::engine::transform(jobs, comm->c);
@@ -284,7 +305,7 @@ int costa_hip_transform_async(costa_layout_t A, costa_layout_t C, char trans, co
 int costa_hip_transform_batch_async(int n, const costa_layout_t* A, const costa_layout_t* C,
                                     const char* trans, const void* alpha, const void* beta,
                                     costa_comm_t comm, void* stream) {
-    return guarded([&] {
+    return gpu_guarded([&] {
         if (!comm || !alpha || !beta) throw costa::engine::error(COSTA_ERR_ARG, "null argument");
         auto jobs = make_jobs(n, A, C, trans, alpha, beta);
         costa::engine::transform(jobs, comm->c, stream, true);
@@ -292,7 +313,7 @@ int costa_hip_transform_batch_async(int n, const costa_layout_t* A, const costa_
 }
 
 int costa_hip_synchronize(costa_comm_t comm) {
-    return guarded([&] {
+    return gpu_guarded([&] {
         if (!comm) throw costa::engine::error(COSTA_ERR_ARG, "null communicator");
         costa::engine::synchronize(comm->c);
     });
@@ -302,7 +323,7 @@ int costa_hip_copy_and_transform(costa_dtype_t dtype, int n_rows, int n_cols, co
                                  int src_stride, int src_col_major, void* dst, int dst_stride,
                                  int dst_col_major, int transpose, int conjugate,
                                  const void* alpha, const void* beta) {
-    return guarded([&] {
+    return gpu_guarded([&] {
         if (!alpha || !beta) throw costa::engine::error(COSTA_ERR_ARG, "null scalar");
         costa::engine::copy_and_transform(dtype, n_rows, n_cols, src, src_stride, src_col_major != 0,
                                           dst, dst_stride, dst_col_major != 0, transpose != 0,
@@ -313,7 +334,7 @@ int costa_hip_copy_and_transform(costa_dtype_t dtype, int n_rows, int n_cols, co
 int costa_hip_execute_tiles(costa_dtype_t dtype, const costa_tile_op_t* ops, int64_t n,
                             const void* src_base, void* dst_base, const void* scalars,
                             int n_slots, int device) {
-    return guarded([&] {
+    return gpu_guarded([&] {
         if (n < 0 || (n > 0 && (!ops || !scalars)))
             throw costa::engine::error(COSTA_ERR_ARG, "null argument");
         costa::engine::execute_tiles(dtype, ops, n, src_base, dst_base, scalars, n_slots, device);
@@ -338,6 +359,7 @@ int costa_hip_plan_export_device(int device, int n, const costa_layout_t* A, con
                                  costa_tile_op_t* pack_ops, costa_tile_op_t* unpack_ops,
                                  int64_t* send_counts, int64_t* send_displs, int64_t* recv_counts,
                                  int64_t* recv_displs, void* scalars) {
+    device_restore keep;
     return export_plan(
         [&](const std::vector<job>& jobs) {
             auto p = costa::engine::make_plan_device(jobs, rank, nranks, 0, device, nullptr);
@@ -381,7 +403,7 @@ int costa_hip_set_host_staging(int mode) {
 }
 
 int costa_hip_release_caches(void) {
-    return guarded([&] { costa::engine::release_caches(); });
+    return gpu_guarded([&] { costa::engine::release_caches(); });
 }
 
 }  // extern "C"
@@ -402,7 +424,7 @@ engine::scal scal_of(T a, T b) {
 template <typename T>
 void run(std::vector<layout_ref<T>>& from, std::vector<layout_ref<T>>& to, const char* trans,
          const T* alpha, const T* beta, costa_comm_t comm) {
-    raise(guarded([&] {
+    raise(gpu_guarded([&] {
         if (from.size() != to.size())
             throw engine::error(COSTA_ERR_ARG, "costa::transform: from/to sizes differ");
         if (!comm) throw engine::error(COSTA_ERR_ARG, "costa::transform: null communicator");

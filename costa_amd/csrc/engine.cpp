@@ -421,6 +421,13 @@ struct wave_knobs {  // defaults, overridable for tuning runs
                      // 2: also large ops that are not 16-byte aligned on both sides (r11: cfg 5
                      // geometry with doubled edges 3.41 -> 4.14 TB/s 'N', 3.47 -> 3.88 'T',
                      // the rest unchanged; profiles/r11/c5_align_policy*.log)
+    int large_sort = 1;  // COSTA_LARGE_SORT 1: large ops in the order of the planner's locality
+                         // hint (column-major target order: consecutive ops continue down the
+                         // same target columns, so the write stream is sequential in aggregate);
+                         // 0: list order (the reference's message order: target row-major, every
+                         // op a new target column at the same in-column offset, which camps on
+                         // HBM channels; tools/copy_ceiling.hip "pat ... ord-1" 6.27 against 5.64
+                         // TB/s, "segcamp" 4.4-4.9 against 6.4)
     int sort = 4;    // COSTA_TINY_SORT 0: list order, 1: by source, 2: by destination address,
                      // 3: by the planner's locality hint (costa_tile_op_t::order), 4: 3 for
                      // copy-only lists, 2 for lists that transpose (cfg 5 'T' 3.88 against
@@ -431,6 +438,7 @@ const wave_knobs& knobs() {
         wave_knobs x;
         if (const char* s = std::getenv("COSTA_WAVE_POLICY")) x.policy = std::atoi(s);
         if (const char* s = std::getenv("COSTA_TINY_SORT")) x.sort = std::atoi(s);
+        if (const char* s = std::getenv("COSTA_LARGE_SORT")) x.large_sort = std::atoi(s);
         return x;
     }();
     return k;
@@ -449,7 +457,11 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     wave_ops.reserve(ops.size());
     std::vector<uint64_t> small;
     const uint32_t vec_both = COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST;
-    for (const auto& op : ops) {
+    // classify: wavefront path, or a shaped (large / small) op
+    std::vector<uint32_t> shaped;
+    std::vector<uint8_t> is_large;
+    for (size_t li = 0; li < ops.size(); ++li) {
+        const costa_tile_op_t& op = ops[li];
         if (op.nf <= 0 || op.ns <= 0) continue;
         const int64_t elems = int64_t(op.nf) * op.ns;
         bool large = 2 * elems >= int64_t(bfl) * bsl;
@@ -458,6 +470,23 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
             wave_ops.push_back(&op);
             continue;
         }
+        shaped.push_back(uint32_t(li));
+        is_large.push_back(large);
+    }
+    // shaped ops in hint order when every one carries a hint
+    std::vector<uint32_t> sperm(shaped.size());
+    for (size_t i = 0; i < shaped.size(); ++i) sperm[i] = uint32_t(i);
+    if (kn.large_sort == 1 && !shaped.empty()) {
+        bool hints = true;
+        for (uint32_t li : shaped) hints = hints && ops[li].order != 0;
+        if (hints)
+            std::stable_sort(sperm.begin(), sperm.end(), [&](uint32_t a, uint32_t b) {
+                return ops[shaped[a]].order < ops[shaped[b]].order;
+            });
+    }
+    for (const uint32_t k : sperm) {
+        const costa_tile_op_t& op = ops[shaped[k]];
+        const bool large = is_large[k];
         const uint64_t i = ordered.size();
         if (i > 0xFFFFFFFFull) throw error(COSTA_ERR_ARG, "costa: too many tiles in one list");
         ordered.push_back(op);
@@ -465,7 +494,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         const uint64_t n = uint64_t((op.nf + bf - 1) / bf) * uint64_t((op.ns + bs - 1) / bs);
         if (n > 0xFFFFFFFFull) throw error(COSTA_ERR_ARG, "costa: tile too large");
         auto& dst = large ? work : small;
-        for (uint64_t k = 0; k < n; ++k) dst.push_back((i << 32) | k);
+        for (uint64_t q = 0; q < n; ++q) dst.push_back((i << 32) | q);
     }
     // ops are independent (disjoint destinations), so any order is valid; neighbours in
     // memory run at the same time and share the partially used cache lines at their edges.
@@ -643,12 +672,15 @@ namespace {
 
 struct hasher {
     uint64_t h = 0x9E3779B97F4A7C15ull;
+    uint64_t h2 = 0x2545F4914F6CDD1Dull;  // second lane: other seed, other multiplier
     void mix(uint64_t v) {
         v ^= v >> 33;
         v *= 0xff51afd7ed558ccdull;
         v ^= v >> 33;
         h = (h ^ v) * 0xc4ceb9fe1a85ec53ull + 0x165667b19e3779f9ull;
         h ^= h >> 29;
+        h2 = (h2 + v) * 0x9fb21c651e98df25ull;
+        h2 ^= h2 >> 31;
     }
     void mix_vec(const std::vector<int>& v) {
         mix(v.size());
@@ -679,6 +711,15 @@ uint64_t layout_hash(const elayout& L) {
     return h.h | 1;  // never 0 (0 = "not computed")
 }
 
+void layout_hashes(const elayout& L, uint64_t& h1, uint64_t& h2) {
+    hasher h;
+    h.mix_layout(L);
+    h1 = h.h | 1;
+    h2 = h.h2;
+}
+
+void set_layout_hash(elayout& L) { layout_hashes(L, L.hash, L.hash2); }
+
 namespace {
 
 struct cached_plan {
@@ -704,7 +745,31 @@ struct cached_plan {
 };
 
 constexpr size_t kMaxPlans = 16;
-std::list<std::pair<uint64_t, std::unique_ptr<cached_plan>>> g_plans;  // MRU first
+// A plan is found by a 64-bit hash and then verified against its full key: the second content
+// hash of every layout plus cheap identity fields (sizes, first / last block pointer and ld).
+// A hit on the hash alone would replay another layout pair's raw device addresses.
+struct keyed_plan {
+    uint64_t h = 0;
+    std::vector<uint64_t> key;
+    std::unique_ptr<cached_plan> plan;
+};
+std::list<keyed_plan> g_plans;  // MRU first
+
+void key_layout(std::vector<uint64_t>& k, const elayout& L) {
+    uint64_t h1 = L.hash, h2 = L.hash2;
+    if (!h1) layout_hashes(L, h1, h2);  // C++-API layouts are hashed per call
+    k.push_back(h1);
+    k.push_back(h2);
+    k.push_back(uint64_t(L.dtype) | uint64_t(uint8_t(L.ordering)) << 8 |
+                uint64_t(uint32_t(L.n_ranks)) << 32);
+    k.push_back(uint64_t(uint32_t(L.nbr())) | uint64_t(uint32_t(L.nbc())) << 32);
+    k.push_back(L.blocks.size());
+    if (!L.blocks.empty())
+        for (const eblock* b : {&L.blocks.front(), &L.blocks.back()}) {
+            k.push_back(reinterpret_cast<uintptr_t>(b->data));
+            k.push_back(uint64_t(uint32_t(b->ld)) | uint64_t(uint32_t(b->rows.start)) << 32);
+        }
+}
 
 // remap every block pointer of `L` that lies in a staged range to its device address
 elayout remap(const elayout& L, const std::vector<hrange>& ranges, char* dev) {
@@ -787,25 +852,27 @@ std::unique_ptr<plan> plan_jobs(const std::vector<job>& jobs, comm* c, hipStream
 }
 
 cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
-    hasher h;
-    h.mix(uint64_t(c->rank));
-    h.mix(uint64_t(c->size));
-    h.mix(uint64_t(c->device));
-    h.mix(uint64_t(host_staging_mode()));
-    h.mix(jobs.size());
+    std::vector<uint64_t> key;
+    key.reserve(4 + jobs.size() * 30);
+    key.push_back(uint64_t(uint32_t(c->rank)) | uint64_t(uint32_t(c->size)) << 32);
+    key.push_back(uint64_t(uint32_t(c->device)) | uint64_t(uint32_t(host_staging_mode())) << 32);
+    key.push_back(jobs.size());
     for (const auto& j : jobs) {
-        h.mix(j.A->hash ? j.A->hash : layout_hash(*j.A));  // handles cache their hash
-        h.mix(j.C->hash ? j.C->hash : layout_hash(*j.C));
-        h.mix(uint64_t(uint8_t(std::toupper(static_cast<unsigned char>(j.trans)))));
+        key_layout(key, *j.A);  // handles cache their hashes
+        key_layout(key, *j.C);
+        uint64_t w = uint64_t(uint8_t(std::toupper(static_cast<unsigned char>(j.trans))));
         // the scale kinds (not the values) are baked into the ops
         for (bool cm : {true, false})
-            h.mix(scale_kind(j.A->dtype, j.s, cm, std::toupper(j.trans) == 'C'));
+            w = w << 8 | scale_kind(j.A->dtype, j.s, cm, std::toupper(j.trans) == 'C');
+        key.push_back(w);
     }
+    hasher h;
+    for (uint64_t w : key) h.mix(w);
     for (auto it = g_plans.begin(); it != g_plans.end(); ++it) {
-        if (it->first == h.h) {
+        if (it->h == h.h && it->key == key) {
             g_plans.splice(g_plans.begin(), g_plans, it);
             g_stats.plan_hits++;
-            return g_plans.front().second.get();
+            return g_plans.front().plan.get();
         }
     }
     g_stats.plan_misses++;
@@ -899,9 +966,9 @@ cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
                 exchange_round_of_ops(*cp->p, R, pr, ur);
                 cp->pipe = make_host_pipeline(cp->p->dtype, cp->p->pack_ops, cp->p->local_ops,
                                               cp->p->unpack_ops, pr, ur, R);
-                g_plans.emplace_front(h.h, std::move(cp));
+                g_plans.push_front({h.h, std::move(key), std::move(cp)});
                 while (g_plans.size() > kMaxPlans) g_plans.pop_back();
-                return g_plans.front().second.get();
+                return g_plans.front().plan.get();
             }
         }
         cp->stage.reserve(std::max<size_t>(off, 256));
@@ -1001,9 +1068,9 @@ cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
                      p.local_ops.size(), p.pack_ops.size(), p.unpack_ops.size(), t_resid, t_plan,
                      t_work, now() - t0 - t_resid - t_plan - t_work, now() - t0);
 
-    g_plans.emplace_front(h.h, std::move(cp));
+    g_plans.push_front({h.h, std::move(key), std::move(cp)});
     while (g_plans.size() > kMaxPlans) g_plans.pop_back();
-    return g_plans.front().second.get();
+    return g_plans.front().plan.get();
 }
 
 void upload_scalars(cached_plan& cp, const std::vector<job>& jobs, hipStream_t s) {

@@ -34,7 +34,8 @@ struct elayout {
     int n_ranks = 1;
     char ordering = 'C';
     std::vector<eblock> blocks;
-    uint64_t hash = 0;  // content hash (plan-cache key); 0 = not computed yet
+    uint64_t hash = 0;   // content hash (plan-cache key); 0 = not computed yet
+    uint64_t hash2 = 0;  // a second, independently seeded content hash (verified on a cache hit)
 
     int nbr() const { return int(rows_split.size()) - 1; }
     int nbc() const { return int(cols_split.size()) - 1; }
@@ -48,6 +49,9 @@ elayout erase(const grid_layout<T>& L);
 
 // content hash of a layout (splits, owners, ordering, every block's intervals/pointer/ld)
 uint64_t layout_hash(const elayout& L);
+// both content hashes (h1 == layout_hash(L)), stored in L.hash / L.hash2 by set_layout_hash
+void layout_hashes(const elayout& L, uint64_t& h1, uint64_t& h2);
+void set_layout_hash(elayout& L);
 
 // scalars (alpha, beta) of one layout pair, stored as raw bytes of the dtype
 struct scal {

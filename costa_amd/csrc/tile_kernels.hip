@@ -94,11 +94,45 @@ struct __attribute__((aligned(16))) raw16 {
     uint32_t w[4];
 };
 
+// 16-byte vector accesses of the tile kernels are non-temporal (`nt`): every byte of a
+// transform is read once and written once, and on MI355X the nt policy moves such streams
+// faster (tools/copy_ceiling.hip, profiles/r2/: a strided 2 GiB copy in 1 KiB column segments
+// 6.37-6.49 TB/s with nt loads and stores against 6.02-6.23 without; cfg 2's transposed access
+// pattern 6.27 against 5.73).  COSTA_NT_LOADS / COSTA_NT_STORES = 0 build the default-policy
+// variant (tuning builds only).
+#ifndef COSTA_NT_LOADS
+#define COSTA_NT_LOADS 1
+#endif
+#ifndef COSTA_NT_STORES
+#define COSTA_NT_STORES 1
+#endif
+typedef uint32_t u32x4a __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ raw16 ld16(const void* p) {
+    raw16 r;
+#if COSTA_NT_LOADS
+    const u32x4a v = __builtin_nontemporal_load(reinterpret_cast<const u32x4a*>(p));
+    __builtin_memcpy(&r, &v, 16);
+#else
+    r = *reinterpret_cast<const raw16*>(p);
+#endif
+    return r;
+}
+__device__ __forceinline__ void st16(void* p, const raw16& r) {
+#if COSTA_NT_STORES
+    u32x4a v;
+    __builtin_memcpy(&v, &r, 16);
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x4a*>(p));
+#else
+    *reinterpret_cast<raw16*>(p) = r;
+#endif
+}
+
 template <typename T>
 __device__ __forceinline__ void vload(vec<T>& out, const T* p, int n, bool vec_ok) {
     constexpr int V = vec<T>::V;
     if (vec_ok && n >= V) {
-        raw16 r = *reinterpret_cast<const raw16*>(p);
+        raw16 r = ld16(p);
         __builtin_memcpy(&out, &r, 16);
     } else {
 #pragma unroll
@@ -113,7 +147,7 @@ __device__ __forceinline__ void vstore(T* p, const vec<T>& in, int n, bool vec_o
     if (vec_ok && n >= V) {
         raw16 r;
         __builtin_memcpy(&r, &in, 16);
-        *reinterpret_cast<raw16*>(p) = r;
+        st16(p, r);
     } else {
 #pragma unroll
         for (int k = 0; k < V; ++k)

@@ -197,7 +197,7 @@ __global__ __launch_bounds__(256) void v_persist(const op_t* ops, const uint64_t
 // ----------------------------------------------------------------------------------
 // V3: generic BF x BS tile, NT threads, pair-exchange 16-B stores, optional nt loads.
 // Load: LPC = BF/2 lanes per column; store: 32 lane-pairs cover 64 s per row pair.
-template <int BF, int BS, int NT, int NTL>
+template <int BF, int BS, int NT, int NTL, int NTS = 0>
 __global__ __launch_bounds__(NT) void v_gen(const op_t* ops, const uint64_t* work) {
     constexpr int P = BF + 2;
     __shared__ __attribute__((aligned(16))) double tile[BS * P];
@@ -237,7 +237,8 @@ __global__ __launch_bounds__(NT) void v_gen(const op_t* ops, const uint64_t* wor
         double got = __shfl_xor(odd ? v.x : v.y, 1);
         d2 o;
         if (!odd) { o.x = v.x; o.y = got; } else { o.x = got; o.y = v.y; }
-        *reinterpret_cast<d2*>(dst + int64_t(2 * rp + (odd ? 1 : 0)) * op.ldd + (lane & ~1) + 64 * j) = o;
+        d2* q = reinterpret_cast<d2*>(dst + int64_t(2 * rp + (odd ? 1 : 0)) * op.ldd + (lane & ~1) + 64 * j);
+        if (NTS) __builtin_nontemporal_store(o, q); else *q = o;
     }
 }
 
@@ -293,7 +294,7 @@ __global__ __launch_bounds__(1024) void v_rowstore(const op_t* ops, const uint64
 // ----------------------------------------------------------------------------------
 // V4: v_gen as a persistent loop: the next sub-tile's loads are issued before the current
 // sub-tile's LDS read-out and stores (register double buffering).
-template <int BF, int BS, int NT>
+template <int BF, int BS, int NT, int NTL = 0, int NTS = 0>
 __global__ __launch_bounds__(NT) void v_gen_persist(const op_t* ops, const uint64_t* work,
                                                     int64_t n) {
     constexpr int P = BF + 2;
@@ -321,9 +322,12 @@ __global__ __launch_bounds__(NT) void v_gen_persist(const op_t* ops, const uint6
     };
     geo(i);
     d2 x[PL];
+    auto ld = [&](int k) {
+        const d2* p = reinterpret_cast<const d2*>(src + int64_t(c0 + CPP * k) * lds + lf);
+        return NTL ? __builtin_nontemporal_load(p) : *p;
+    };
 #pragma unroll
-    for (int k = 0; k < PL; ++k)
-        x[k] = *reinterpret_cast<const d2*>(src + int64_t(c0 + CPP * k) * lds + lf);
+    for (int k = 0; k < PL; ++k) x[k] = ld(k);
     while (true) {
 #pragma unroll
         for (int k = 0; k < PL; ++k) *reinterpret_cast<d2*>(&tile[(c0 + CPP * k) * P + lf]) = x[k];
@@ -334,8 +338,7 @@ __global__ __launch_bounds__(NT) void v_gen_persist(const op_t* ops, const uint6
         if (nxt < n) {
             geo(nxt);
 #pragma unroll
-            for (int k = 0; k < PL; ++k)
-                x[k] = *reinterpret_cast<const d2*>(src + int64_t(c0 + CPP * k) * lds + lf);
+            for (int k = 0; k < PL; ++k) x[k] = ld(k);
         }
         d2 y[PS];
 #pragma unroll
@@ -351,7 +354,8 @@ __global__ __launch_bounds__(NT) void v_gen_persist(const op_t* ops, const uint6
             double got = __shfl_xor(odd ? v.x : v.y, 1);
             d2 o;
             if (!odd) { o.x = v.x; o.y = got; } else { o.x = got; o.y = v.y; }
-            *reinterpret_cast<d2*>(cdst + int64_t(2 * rp + (odd ? 1 : 0)) * cldd + (lane & ~1) + 64 * j) = o;
+            d2* q = reinterpret_cast<d2*>(cdst + int64_t(2 * rp + (odd ? 1 : 0)) * cldd + (lane & ~1) + 64 * j);
+            if (NTS) __builtin_nontemporal_store(o, q); else *q = o;
         }
         if (nxt >= n) break;
         i = nxt;
@@ -489,7 +493,7 @@ __global__ __launch_bounds__(512) void v_glds(const op_t* ops, const uint64_t* w
 // of sub-tile i: the stores of earlier sub-tiles and the loads of later ones stay in flight
 // (vmcnt counts in issue order).  Store: lane pairs swap halves so every lane writes 16 B
 // along s (BS s-values per row pair, 64 / BS row pairs per instruction).
-template <int BS, int NT, int NB, int NTL>
+template <int BS, int NT, int NB, int NTL, int NTS = 0>
 __global__ __launch_bounds__(NT) void v_ring(const op_t* ops, const uint64_t* work, int64_t n) {
     constexpr int BF = 128, P = BF + 2;
     constexpr int NW = NT / 64;
@@ -569,9 +573,61 @@ __global__ __launch_bounds__(NT) void v_ring(const op_t* ops, const uint64_t* wo
             double got = __shfl_xor(odd ? v.x : v.y, 1);
             d2 o;
             if (!odd) { o.x = v.x; o.y = got; } else { o.x = got; o.y = v.y; }
-            *reinterpret_cast<d2*>(cdst + int64_t(2 * rp + (odd ? 1 : 0)) * cld + (sl & ~1)) = o;
+            d2* q = reinterpret_cast<d2*>(cdst + int64_t(2 * rp + (odd ? 1 : 0)) * cld + (sl & ~1));
+            if (NTS) __builtin_nontemporal_store(o, q); else *q = o;
         }
         b = (b + 1) % NB;
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// V9: generic BF (f) x BS (s) sub-tile per NT-thread WG, BS <= 64: one store instruction covers
+// 64 / BS row pairs of BS s-values (pair exchange), optional nt loads / stores.  Small tiles
+// (16-32 KiB) keep up to 8 WGs per CU resident, so load and store phases of different WGs overlap
+// on every CU (the flat copy's best shape: 16 KiB per 256-thread WG, nt both ways).
+template <int BF, int BS, int NT, int NTL, int NTS>
+__global__ __launch_bounds__(NT) void v_tr(const op_t* ops, const uint64_t* work) {
+    constexpr int P = BF + 2;
+    __shared__ __attribute__((aligned(16))) double tile[BS * P];
+    const uint64_t w = work[blockIdx.x];
+    const op_t op = ops[w >> 32];
+    const uint32_t sub = uint32_t(w);
+    const int nbf = op.nf / BF;
+    const int f0 = int(sub % nbf) * BF, s0 = int(sub / nbf) * BS;
+    const double* src = reinterpret_cast<const double*>(op.src) + int64_t(s0) * op.lds + f0;
+    double* dst = reinterpret_cast<double*>(op.dst) + int64_t(f0) * op.ldd + s0;
+    constexpr int LPC = BF / 2, CPP = NT / LPC, PL = BS / CPP;
+    static_assert(NT % LPC == 0 && BS % CPP == 0 && BS <= 64, "mapping");
+    const int lf = (threadIdx.x % LPC) * 2, c0 = threadIdx.x / LPC;
+    d2 x[PL];
+#pragma unroll
+    for (int k = 0; k < PL; ++k) {
+        const d2* p = reinterpret_cast<const d2*>(src + int64_t(c0 + CPP * k) * op.lds + lf);
+        x[k] = NTL ? __builtin_nontemporal_load(p) : *p;
+    }
+#pragma unroll
+    for (int k = 0; k < PL; ++k) *reinterpret_cast<d2*>(&tile[(c0 + CPP * k) * P + lf]) = x[k];
+    __syncthreads();
+    constexpr int NW = NT / 64, RPI = 64 / BS, SI = (BF / 2) / RPI, PS = SI / NW;
+    static_assert(SI % NW == 0 && PS >= 1, "store mapping");
+    const int lane = threadIdx.x % 64, wave = threadIdx.x / 64;
+    const bool odd = lane & 1;
+    const int sl = lane % BS, rq = lane / BS;
+    d2 y[PS];
+#pragma unroll
+    for (int k = 0; k < PS; ++k) {
+        const int rp = (wave + NW * k) * RPI + rq;
+        y[k] = *reinterpret_cast<const d2*>(&tile[sl * P + 2 * rp]);
+    }
+#pragma unroll
+    for (int k = 0; k < PS; ++k) {
+        const int rp = (wave + NW * k) * RPI + rq;
+        d2 v = y[k];
+        double got = __shfl_xor(odd ? v.x : v.y, 1);
+        d2 o;
+        if (!odd) { o.x = v.x; o.y = got; } else { o.x = got; o.y = v.y; }
+        d2* q = reinterpret_cast<d2*>(dst + int64_t(2 * rp + (odd ? 1 : 0)) * op.ldd + (sl & ~1));
+        if (NTS) __builtin_nontemporal_store(o, q); else *q = o;
     }
 }
 
@@ -653,10 +709,15 @@ int main(int argc, char** argv) {
     op_t* d_ops;
     CK(hipMalloc(&d_ops, ops.size() * sizeof(op_t)));
     CK(hipMemcpy(d_ops, ops.data(), ops.size() * sizeof(op_t), hipMemcpyHostToDevice));
-    auto mkwork = [&](int BS, int BF = 64, bool xcd = false) {
+    // tord: ops in the order of the product's locality hint (target column-major: consecutive
+    // ops continue down the same C columns); otherwise source column-major (ops[] order)
+    auto mkwork = [&](int BS, int BF = 64, bool xcd = false, bool tord = false) {
         std::vector<uint64_t> w;
-        for (size_t o = 0; o < ops.size(); ++o)
+        const int nb = n / b;
+        for (size_t q = 0; q < ops.size(); ++q) {
+            const size_t o = tord ? (q % nb) * nb + q / nb : q;
             for (uint64_t k = 0; k < uint64_t(b / BF) * (b / BS); ++k) w.push_back((uint64_t(o) << 32) | k);
+        }
         if (xcd) {  // blockIdx p -> XCD p%8: give each XCD a contiguous run of the list
             std::vector<uint64_t> v(w.size());
             const size_t per = w.size() / 8;
@@ -672,6 +733,11 @@ int main(int argc, char** argv) {
     auto w64x = mkwork(64, 64, true);
     auto g128x64 = mkwork(64, 128), g128x128 = mkwork(128, 128), g64x128 = mkwork(128, 64);
     auto g128x32 = mkwork(32, 128);
+    auto g64x32 = mkwork(32, 64), g32x64 = mkwork(64, 32), g128x16 = mkwork(16, 128);
+    auto g256x16 = mkwork(16, 256), g256x32 = mkwork(32, 256);
+    auto t128x128 = mkwork(128, 128, false, true), t128x64 = mkwork(64, 128, false, true);
+    auto t64x128 = mkwork(128, 64, false, true), t64x64 = mkwork(64, 64, false, true);
+    auto t128x32 = mkwork(32, 128, false, true);
     unsigned long long* bad;
     CK(hipMalloc(&bad, 8));
     hipEvent_t e0, e1;
@@ -687,6 +753,54 @@ int main(int argc, char** argv) {
         std::vector<float> ms;
     };
     std::vector<var> V;
+    // ---- r2: hint (target column-major) order, nt loads and stores
+    V.push_back({"H gen 128x128 t1024", [&] { hipLaunchKernelGGL((v_gen<128, 128, 1024, 1, 1>), dim3(t128x128.second), dim3(1024), 0, 0, d_ops, t128x128.first); }, true, {}});
+    V.push_back({"H gen 128x128 t1024 plain", [&] { hipLaunchKernelGGL((v_gen<128, 128, 1024, 0, 0>), dim3(t128x128.second), dim3(1024), 0, 0, d_ops, t128x128.first); }, true, {}});
+    V.push_back({"H gen 128x64 t512", [&] { hipLaunchKernelGGL((v_gen<128, 64, 512, 1, 1>), dim3(t128x64.second), dim3(512), 0, 0, d_ops, t128x64.first); }, true, {}});
+    V.push_back({"H gen 64x128 t512", [&] { hipLaunchKernelGGL((v_gen<64, 128, 512, 1, 1>), dim3(t64x128.second), dim3(512), 0, 0, d_ops, t64x128.first); }, true, {}});
+    V.push_back({"H gen 64x64 t256", [&] { hipLaunchKernelGGL((v_gen<64, 64, 256, 1, 1>), dim3(t64x64.second), dim3(256), 0, 0, d_ops, t64x64.first); }, true, {}});
+    V.push_back({"H gen 128x128 t512", [&] { hipLaunchKernelGGL((v_gen<128, 128, 512, 1, 1>), dim3(t128x128.second), dim3(512), 0, 0, d_ops, t128x128.first); }, true, {}});
+    V.push_back({"H tr 128x32 t256", [&] { hipLaunchKernelGGL((v_tr<128, 32, 256, 1, 1>), dim3(t128x32.second), dim3(256), 0, 0, d_ops, t128x32.first); }, true, {}});
+    V.push_back({"H tr 64x64 t256", [&] { hipLaunchKernelGGL((v_tr<64, 64, 256, 1, 1>), dim3(t64x64.second), dim3(256), 0, 0, d_ops, t64x64.first); }, true, {}});
+    V.push_back({"H tr 128x64 t512", [&] { hipLaunchKernelGGL((v_tr<128, 64, 512, 1, 1>), dim3(t128x64.second), dim3(512), 0, 0, d_ops, t128x64.first); }, true, {}});
+    V.push_back({"H tr 128x64 t256", [&] { hipLaunchKernelGGL((v_tr<128, 64, 256, 1, 1>), dim3(t128x64.second), dim3(256), 0, 0, d_ops, t128x64.first); }, true, {}});
+    for (int k : {1, 2}) {
+        V.push_back({"H gpersist 128x128 t1024 x" + std::to_string(k), [&, k] { hipLaunchKernelGGL((v_gen_persist<128, 128, 1024, 1, 1>), dim3(cus * k), dim3(1024), 0, 0, d_ops, t128x128.first, t128x128.second); }, true, {}});
+    }
+    for (int k : {2, 3}) {
+        V.push_back({"H gpersist 128x64 t512 x" + std::to_string(k), [&, k] { hipLaunchKernelGGL((v_gen_persist<128, 64, 512, 1, 1>), dim3(cus * k), dim3(512), 0, 0, d_ops, t128x64.first, t128x64.second); }, true, {}});
+    }
+    {
+        auto hring = [&](auto kern, const char* name, int bs, int nt, int nb) {
+            const int bytes = nb * bs * 130 * 8;
+            CK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+            auto w = bs == 64 ? t128x64 : t128x32;
+            V.push_back({name, [=] { hipLaunchKernelGGL(kern, dim3(cus), dim3(nt), bytes, 0, d_ops,
+                                                        w.first, w.second); }, true, {}});
+        };
+        hring(&v_ring<64, 512, 2, 1, 1>, "H ring 128x64 t512 nb2", 64, 512, 2);
+        hring(&v_ring<64, 1024, 2, 1, 1>, "H ring 128x64 t1024 nb2", 64, 1024, 2);
+        hring(&v_ring<32, 512, 4, 1, 1>, "H ring 128x32 t512 nb4", 32, 512, 4);
+        hring(&v_ring<32, 512, 3, 1, 1>, "H ring 128x32 t512 nb3", 32, 512, 3);
+    }
+#define VTR(BF, BS, NT, NTL, NTS, W)                                                              \
+    V.push_back({"tr " #BF "x" #BS " t" #NT " ntl" #NTL " nts" #NTS, [&] {                       \
+        hipLaunchKernelGGL((v_tr<BF, BS, NT, NTL, NTS>), dim3(W.second), dim3(NT), 0, 0, d_ops,    \
+                           W.first); }, true, {}})
+    VTR(64, 32, 256, 1, 1, g64x32);
+    VTR(64, 32, 256, 0, 0, g64x32);
+    VTR(64, 32, 256, 1, 0, g64x32);
+    VTR(32, 64, 256, 1, 1, g32x64);
+    VTR(32, 64, 256, 0, 0, g32x64);
+    VTR(128, 16, 256, 1, 1, g128x16);
+    VTR(128, 32, 256, 1, 1, g128x32);
+    VTR(128, 32, 256, 0, 0, g128x32);
+    VTR(64, 64, 256, 1, 1, w64);
+    VTR(256, 16, 256, 1, 1, g256x16);
+    VTR(256, 32, 512, 1, 1, g256x32);
+    VTR(128, 64, 512, 1, 1, g128x64);
+    VTR(64, 32, 128, 1, 1, g64x32);
     V.push_back({"basic 64x64", [&] { hipLaunchKernelGGL((v_basic<64, 0>), dim3(w64.second), dim3(256), 0, 0, d_ops, w64.first); }, true, {}});
     V.push_back({"basic 64x64 nt-store", [&] { hipLaunchKernelGGL((v_basic<64, 1>), dim3(w64.second), dim3(256), 0, 0, d_ops, w64.first); }, true, {}});
     V.push_back({"basic 64x128", [&] { hipLaunchKernelGGL((v_basic<128, 0>), dim3(w128.second), dim3(256), 0, 0, d_ops, w128.first); }, true, {}});
@@ -719,6 +833,13 @@ int main(int argc, char** argv) {
         V.push_back({"gpersist 128x64 t512 x" + std::to_string(k), [&, k] { hipLaunchKernelGGL((v_gen_persist<128, 64, 512>), dim3(cus * k), dim3(512), 0, 0, d_ops, g128x64.first, g128x64.second); }, true, {}});
     }
     V.push_back({"gpersist 64x64 t256 x4", [&] { hipLaunchKernelGGL((v_gen_persist<64, 64, 256>), dim3(cus * 4), dim3(256), 0, 0, d_ops, w64.first, w64.second); }, true, {}});
+    V.push_back({"gen 128x128 t1024 nt-both", [&] { hipLaunchKernelGGL((v_gen<128, 128, 1024, 1, 1>), dim3(g128x128.second), dim3(1024), 0, 0, d_ops, g128x128.first); }, true, {}});
+    V.push_back({"gen 128x128 t1024 nt-store", [&] { hipLaunchKernelGGL((v_gen<128, 128, 1024, 0, 1>), dim3(g128x128.second), dim3(1024), 0, 0, d_ops, g128x128.first); }, true, {}});
+    V.push_back({"gen 128x64 t512 nt-both", [&] { hipLaunchKernelGGL((v_gen<128, 64, 512, 1, 1>), dim3(g128x64.second), dim3(512), 0, 0, d_ops, g128x64.first); }, true, {}});
+    V.push_back({"gen 64x128 t512 nt-both", [&] { hipLaunchKernelGGL((v_gen<64, 128, 512, 1, 1>), dim3(g64x128.second), dim3(512), 0, 0, d_ops, g64x128.first); }, true, {}});
+    V.push_back({"gen 64x64 t256 nt-both", [&] { hipLaunchKernelGGL((v_gen<64, 64, 256, 1, 1>), dim3(w64.second), dim3(256), 0, 0, d_ops, w64.first); }, true, {}});
+    V.push_back({"gen 128x64 t256 nt-both", [&] { hipLaunchKernelGGL((v_gen<128, 64, 256, 1, 1>), dim3(g128x64.second), dim3(256), 0, 0, d_ops, g128x64.first); }, true, {}});
+    V.push_back({"gen 128x128 t512 nt-both", [&] { hipLaunchKernelGGL((v_gen<128, 128, 512, 1, 1>), dim3(g128x128.second), dim3(512), 0, 0, d_ops, g128x128.first); }, true, {}});
     V.push_back({"gen 128x128 t512", [&] { hipLaunchKernelGGL((v_gen<128, 128, 512, 0>), dim3(g128x128.second), dim3(512), 0, 0, d_ops, g128x128.first); }, true, {}});
     V.push_back({"copyshape 128x32 t256", [&] { hipLaunchKernelGGL((v_copyshape<0>), dim3(g128x32.second), dim3(256), 0, 0, d_ops, g128x32.first); }, true, {}});
     V.push_back({"copyshape 128x32 t256 nt-load", [&] { hipLaunchKernelGGL((v_copyshape<1>), dim3(g128x32.second), dim3(256), 0, 0, d_ops, g128x32.first); }, true, {}});
@@ -754,6 +875,7 @@ int main(int argc, char** argv) {
     V.push_back({"copy U4 grid 8/CU", [&] { hipLaunchKernelGGL((v_copy_ilp<4, 0, 0>), dim3(cus * 8), dim3(256), 0, 0, (const d2*)A, (d2*)Cm, n2); }, false, {}});
     V.push_back({"copy U16 grid 4/CU", [&] { hipLaunchKernelGGL((v_copy_ilp<16, 0, 0>), dim3(cus * 4), dim3(256), 0, 0, (const d2*)A, (d2*)Cm, n2); }, false, {}});
     V.push_back({"copy U8 nt-load", [&] { hipLaunchKernelGGL((v_copy_ilp<8, 1, 0>), dim3(cus * 8), dim3(256), 0, 0, (const d2*)A, (d2*)Cm, n2); }, false, {}});
+    V.push_back({"copy U8 nt-both", [&] { hipLaunchKernelGGL((v_copy_ilp<8, 1, 1>), dim3(cus * 8), dim3(256), 0, 0, (const d2*)A, (d2*)Cm, n2); }, false, {}});
     V.push_back({"copy U8 nt-store", [&] { hipLaunchKernelGGL((v_copy_ilp<8, 0, 1>), dim3(cus * 8), dim3(256), 0, 0, (const d2*)A, (d2*)Cm, n2); }, false, {}});
     V.push_back({"copy U8 one-shot grid", [&] { hipLaunchKernelGGL((v_copy_ilp<8, 0, 0>), dim3(n2 / 2048), dim3(256), 0, 0, (const d2*)A, (d2*)Cm, n2); }, false, {}});
     V.push_back({"read-only 2GiB x2 (as 4GiB)", [&] { hipLaunchKernelGGL((v_read<8>), dim3(cus * 8), dim3(256), 0, 0, (const d2*)A, n2, (d2*)Cm); hipLaunchKernelGGL((v_read<8>), dim3(cus * 8), dim3(256), 0, 0, (const d2*)Cm, n2, (d2*)A); }, false, {}});
