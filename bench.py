@@ -10,6 +10,11 @@ Workload (one "step" = one costa::transform over all local tiles, data already i
   N > 1   the same per rank (weak scaling): global (16384*pm) x (16384*pn) fp64 on a pm x pn
           rank grid, C = A^T on the transposed grid; remote tiles go pack -> RCCL -> unpack,
           local tiles are transposed in place (overlapping the exchange).
+  extra   BASELINE's multi-GPU configurations on the GPU counts they are quoted on, measured
+          after the headline in the same processes and reported under "baseline_configs":
+          N = 4: configs[2] pxgemr2d fp64 65536^2, 2x2 -> 4x1, 128^2 blocks ('N', RCCL);
+          N = 8: configs[3] pztranu c128 32768^2 on 2x4, alpha, beta != 0, and configs[4]
+          custom_layout fp32 16384^2 with owners uniform over the 8 ranks.
 Timing: W untimed steps; then barrier + device sync, K steps, device sync + barrier; max over
 ranks.  value = algorithmic bytes of all ranks / that time (read + write of every
 element moved, + read of C when beta != 0).  Rank 0 prints ONE JSON line.
@@ -18,8 +23,10 @@ roofline: the dominant kernel's algorithmic bytes per launch / its average durat
 HIP events recorded on the stream it runs on (costa_hip_get_stats), against 8 TB/s.  Those
 events are recorded in a second pass of the same K steps: in the `value` pass they are off, as
 they are in the shipped library (each event pair adds ~11 us to a 0.83 ms cfg 2 step).
-cpu_baseline: the oracle's restatement of the reference's OpenMP tile loop (256x256-blocked
-transpose, OpenMP over tiles) on a bounded sample of the same tiles, rank 0 at N = 1.
+cpu_baseline: the REFERENCE's own costa::transform (oracle/_ref/ref_harness, compiled from
+/root/reference by oracle/Makefile) on the full cfg 2 matrix with every CPU this process may
+use, rank 0 at N = 1; our restatement of its tile loop (oracle/) is reported beside it and
+stands in, loudly, when the reference binary is absent.
 """
 from __future__ import annotations
 
@@ -61,19 +68,50 @@ def measured_traffic(alg_bytes: int):
     return best if best else (None, None)
 
 
-def cpu_baseline(n=16384, b=256, slab_cols=2048, target_s=10.0):
-    """Oracle restatement of the reference tile loop on a 16384 x 2048 column slab of A
-    (512 tiles of 256^2 fp64, 256 MiB in / 256 MiB out), repeated for ~target_s seconds."""
+def host_cpus():
+    """(threads to use, description): the host CPUs this job may use.  On the GPU pool the
+    affinity mask shows the whole 256-CPU machine, but one GPU's job gets a CPU share (its cgroup
+    quota; OMP_NUM_THREADS is set to it): 256 OpenMP threads under a 16-CPU quota ran the
+    reference at 11 GB/s against ~60 with 16 (profiles/r2/).  Order: the cgroup CPU quota, then
+    OMP_NUM_THREADS, then the affinity mask."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = os.cpu_count() or 1
+    n, src = aff, "affinity mask"
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n, src = max(1, min(aff, int(int(q) // int(p)))), "cgroup cpu.max quota"
+    except Exception:
+        omp = os.environ.get("OMP_NUM_THREADS", "")
+        if omp.isdigit() and int(omp) > 0:
+            n, src = min(aff, int(omp)), "OMP_NUM_THREADS"
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    return n, {"cpus_usable": n, "cpus_usable_from": src, "cpus_machine": os.cpu_count(),
+               "cpu_model": model}
+
+
+def cpu_baseline(n=16384, b=256, target_s=10.0):
+    """Oracle restatement of the reference tile loop (256x256-blocked transpose, OpenMP over
+    tiles) on the full cfg 2 matrix (4096 tiles of 256^2 fp64), repeated for ~target_s s."""
     import numpy as np
     import oracle
-    threads = min(16, os.cpu_count() or 1)
-    a = np.random.default_rng(1).standard_normal(n * slab_cols)  # col-major, ld n
-    c = np.zeros(slab_cols * n)                                  # col-major, ld slab_cols
+    threads, info = host_cpus()
+    a = np.random.default_rng(1).standard_normal(n * n)  # col-major, ld n
+    c = np.zeros(n * n)
     tiles = []
-    for j in range(slab_cols // b):
+    for j in range(n // b):
         for i in range(n // b):
             # A tile (i, j) -> C tile (j, i): (src_off, lds, dst_off, ldd, F, S)
-            tiles.append((i * b + j * b * n, n, j * b + i * b * slab_cols, slab_cols, b, b))
+            tiles.append((i * b + j * b * n, n, j * b + i * b * n, n, b, b))
     tiles = np.array(tiles, np.int64)
     oracle.transform_tiles(1, 1, 0, 1.0, 0.0, a, c, tiles, threads)  # warm-up, first touch
     reps, t0 = 0, time.perf_counter()
@@ -83,40 +121,53 @@ def cpu_baseline(n=16384, b=256, slab_cols=2048, target_s=10.0):
         el = time.perf_counter() - t0
         if el >= target_s or reps >= 1000:
             break
-    ok = np.array_equal(c.reshape(n, slab_cols).T, a.reshape(slab_cols, n))
+    ok = np.array_equal(c.reshape(n, n).T, a.reshape(n, n))
     bytes_per = 2 * a.nbytes
-    return {"value": round(bytes_per * reps / el / 1e9, 3), "unit": "GB/s", "cores": threads,
-            "kind": "port",
-            "sample": f"{len(tiles)} tiles of 256x256 fp64 ('T', alpha=1, beta=0; a 16384x2048 "
-                      f"slab of cfg 2), {reps} passes in {el:.1f} s, oracle/costa_oracle.c "
-                      f"oracle_transform_tiles, OpenMP {threads} threads, verified={ok}"}
+    out = {"value": round(bytes_per * reps / el / 1e9, 3), "unit": "GB/s", "cores": threads,
+           "kind": "port",
+           "sample": f"the full cfg 2 matrix: {len(tiles)} tiles of 256x256 fp64 ('T', alpha=1, "
+                     f"beta=0), {reps} passes in {el:.1f} s, oracle/costa_oracle.c "
+                     f"oracle_transform_tiles, OpenMP {threads} threads, verified={ok}"}
+    out.update(info)
+    return out
 
 
-def cpu_baseline_reference(n=16384, b=256, slab_cols=2048, target_s=10.0):
+def cpu_baseline_reference(n=16384, b=256, target_s=10.0):
     """The REFERENCE itself on the host cores: oracle/_ref/ref_harness (eth-cscs/COSTA compiled
     from its own sources by oracle/Makefile; the binary travels with the repo snapshot) runs
-    costa::transform 'T' (alpha 1, beta 0) on a 16384 x 2048 fp64 slab in 256^2 blocks (the
-    same 512 tiles as cpu_baseline) for ~target_s seconds.  Started as a child process before
-    this process touches the GPU.  None when the binary is absent."""
+    costa::transform 'T' (alpha 1, beta 0) on the full cfg 2 matrix (16384^2 fp64, 256^2 blocks,
+    one rank) for ~target_s seconds, timed like the reference's miniapps (pxgemr2d_utils.hpp:
+    284-292: wall time around each call).  Started as a child process before this process
+    touches the GPU.  None (and a warning on stderr) when the binary is absent."""
     import subprocess
     exe = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
     if not os.path.exists(exe):
+        print("bench.py: WARNING oracle/_ref/ref_harness is absent (build it with "
+              "`make -C oracle ref` where /root/reference exists): cpu_baseline falls back to "
+              "kind 'port', our restatement of the reference's tile loop", file=sys.stderr)
         return None
-    threads = min(16, os.cpu_count() or 1)
+    threads, info = host_cpus()
     env = dict(os.environ, OMP_NUM_THREADS=str(threads))
     try:
-        r = subprocess.run([exe, "bench", str(n), str(slab_cols), str(b), str(target_s)],
-                           capture_output=True, text=True, timeout=6 * target_s + 120, env=env)
+        r = subprocess.run([exe, "bench", str(n), str(n), str(b), str(target_s)],
+                           capture_output=True, text=True, timeout=6 * target_s + 180, env=env)
         d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
-    except Exception:
+    except Exception as e:
+        print(f"bench.py: WARNING reference CPU baseline failed ({e}); using kind 'port'",
+              file=sys.stderr)
         return None
     if r.returncode != 0 or not d.get("verified"):
+        print("bench.py: WARNING reference CPU baseline not verified; using kind 'port'",
+              file=sys.stderr)
         return None
-    return {"value": round(d["GBps"], 3), "unit": "GB/s", "cores": d["threads"], "kind": "reference",
-            "sample": f"{n}x{slab_cols} fp64 slab, {b}x{b} blocks on one rank: the reference's "
-                      f"costa::transform 'T' (alpha=1, beta=0; planning included, as every "
-                      f"reference call re-plans), {d['reps']} calls in {d['seconds']:.1f} s, "
-                      f"OpenMP {d['threads']} threads, verified C == A^T"}
+    out = {"value": round(d["GBps"], 3), "unit": "GB/s", "cores": d["threads"], "kind": "reference",
+           "sample": f"the full cfg 2 matrix, {n}x{n} fp64 in {b}x{b} blocks on one rank: the "
+                     f"reference's costa::transform 'T' (alpha=1, beta=0; planning included, as "
+                     f"every reference call re-plans), {d['reps']} calls in {d['seconds']:.1f} s, "
+                     f"OpenMP {d['threads']} threads = every CPU this job may use ({info['cpus_usable_from']}; "
+                     f"the host has {info['cpus_machine']}), verified C == A^T"}
+    out.update(info)
+    return out
 
 
 def cfg5_workload(costa, torch, rank, world, op):
@@ -166,7 +217,15 @@ def cfg5_workload(costa, torch, rank, world, op):
     wl = (f"costa::custom_layout fp32 16384x16384, irregular tiles (A edges 8-96: "
           f"{len(ars) - 1}x{len(acs) - 1} blocks, C edges 16-160: {len(crs) - 1}x{len(ccs) - 1}), "
           f"owners uniform over {world} rank(s), op {op} (BASELINE configs[4])")
-    return LA, LC, A, C, op, al, be, wl
+
+    def mask(blocks, cs, size):  # the elements the blocks cover (not the arena padding)
+        m = np.zeros(size + 1, np.int32)
+        for o, r, i, j in blocks:
+            m[o] += 1
+            m[o + r * (cs[j + 1] - cs[j])] -= 1
+        return torch.from_numpy(np.cumsum(m[:size]) > 0).cuda()
+    masks = (mask(ab, acs, an), mask(cb, ccs, cn))
+    return LA, LC, A, C, op, al, be, wl, masks
 
 
 def main():
@@ -185,6 +244,11 @@ def main():
     ap.add_argument("--cfg5-op", choices=["N", "T"], default="N")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip BASELINE's multi-GPU configs (cfg 3 at 4 GPUs, cfg 4 / 5 at 8)")
+    ap.add_argument("--extra", default=None,
+                    help="run these extra configs instead of the GPU count's own, e.g. "
+                         "'cfg3,cfg4:32768,cfg5:N' (rehearsal of the multi-GPU entries)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -224,60 +288,93 @@ def main():
     else:
         comm = costa.Comm.self(device)
 
-    # ---- workload
-    n, b = args.edge, args.block
-    pm, pn = grid_for(world)
-    M, N = n * pm, n * pn  # A: M x N on pm x pn; C = A^T: N x M on the same rank grid
-    if args.workload == "cfg5":
-        LA, LC, A, Cm, op, al, be, wl = cfg5_workload(costa, torch, rank, world, args.cfg5_op)
-        check = None
-    elif args.workload == "cfg3":
-        # BASELINE configs[2]: pxgemr2d fp64 'N' (bit copy), 128^2 blocks, A on
-        # the pm x pn grid -> C on a world x 1 grid ('R' rank order both); 32768^2 per rank
-        b, e3 = 128, 32768
-        M, N = e3 * pm, e3 * pn
-        lr_a, lc_a = M // pm, N // pn
-        lr_c, lc_c = M // world, N
-        g = torch.Generator(device="cuda")
-        g.manual_seed(3333 + rank)
-        A = torch.rand(lr_a * lc_a, dtype=torch.float64, device="cuda", generator=g)
-        Cm = torch.zeros(lr_c * lc_c, dtype=torch.float64, device="cuda")
-        LA = costa.block_cyclic_layout(M, N, b, b, 1, 1, M, N, pm, pn, "R", 0, 0, A.data_ptr(),
-                                       lr_a, "C", rank)
-        LC = costa.block_cyclic_layout(M, N, b, b, 1, 1, M, N, world, 1, "R", 0, 0, Cm.data_ptr(),
-                                       lr_c, "C", rank)
-        op, al, be = "N", 1.0, 0.0
-        wl = (f"pxgemr2d fp64 {M}x{N}, 128x128 blocks, {pm}x{pn} -> {world}x1 grid remap, op N "
-              f"(BASELINE configs[2]{', single-GPU slice' if world == 1 else ''})")
+    # ---- workloads
+    def checksum(t, mask=None):
+        """order-independent checksum of a tensor's bit patterns (equal for any permutation of
+        the same elements), summed over the ranks"""
+        x = t.view(torch.int32 if t.element_size() == 4 else torch.int64).reshape(-1)
+        if mask is not None:
+            x = x[mask]
+        x = x.to(torch.int64)
+        v = torch.stack([x.sum(), (x * x).sum(), (x ^ (x >> 7)).sum()]).cpu()
+        if world > 1:
+            dist.all_reduce(v)
+        return v.tolist()
 
-        def check():
-            assert torch.equal(Cm, A), "pxgemr2d copy wrong"
-    elif args.workload == "cfg4":
-        # BASELINE configs[3]: pztranu, c128, 128^2 blocks, alpha=(0.75,-0.5),
-        # beta=(1.25,0.25) (C is read); per rank 16384^2, weak-scaled on the pm x pn grid
-        b = 128
-        lr_a, lc_a = M // pm, N // pn
-        lr_c, lc_c = N // pm, M // pn
-        g = torch.Generator(device="cuda")
-        g.manual_seed(4321 + rank)
-        A = torch.rand(lr_a * lc_a, dtype=torch.complex128, device="cuda", generator=g)
-        Cm = torch.rand(lr_c * lc_c, dtype=torch.complex128, device="cuda", generator=g)
-        LA = costa.block_cyclic_layout(M, N, b, b, 1, 1, M, N, pm, pn, "R", 0, 0, A.data_ptr(),
-                                       lr_a, "C", rank, dtype=costa.CDOUBLE)
-        LC = costa.block_cyclic_layout(N, M, b, b, 1, 1, N, M, pm, pn, "R", 0, 0, Cm.data_ptr(),
-                                       lr_c, "C", rank, dtype=costa.CDOUBLE)
-        op, al, be = "T", complex(0.75, -0.5), complex(1.25, 0.25)
-        wl = (f"pztranu c128 {M}x{N} on a {pm}x{pn} rank grid (16384^2 per rank), 128x128 "
-              f"blocks, op T, alpha=(0.75,-0.5) beta=(1.25,0.25) (BASELINE configs[3], "
-              f"{'single-GPU slice' if world == 1 else 'weak-scaled'})")
-        C0 = Cm.clone() if world == 1 else None
+    def build(kind, edge=None):
+        """-> dict: layouts, tensors, op / alpha / beta, description, correctness check"""
+        n, b = args.edge, args.block
+        pm, pn = grid_for(world)
+        w = {"kind": kind, "check": None, "repeatable": True}
+        if kind == "cfg5":
+            LA, LC, A, Cm, op, al, be, wl, masks = cfg5_workload(costa, torch, rank, world,
+                                                               args.cfg5_op if edge is None else edge)
+            w.update(LA=LA, LC=LC, A=A, C=Cm, op=op, al=al, be=be, wl=wl)
+            if op == "N":  # a bit permutation of A's block elements into C's blocks
+                ref = checksum(A, masks[0])
+                w["check"] = lambda: checksum(Cm, masks[1]) == ref
+            return w
+        if kind == "cfg3":
+            # BASELINE configs[2] (SURVEY §8d): pxgemr2d fp64 'N' (bit copy), 128^2 blocks, A on
+            # the pm x pn grid -> C on a world x 1 grid ('R' rank order both); 32768^2 per rank
+            # (65536^2 2x2 -> 4x1 at 4 ranks)
+            b, e3 = 128, 32768
+            M, N = e3 * pm, e3 * pn
+            lr_a, lc_a = M // pm, N // pn
+            lr_c, lc_c = M // world, N
+            g = torch.Generator(device="cuda")
+            g.manual_seed(3333 + rank)
+            A = torch.rand(lr_a * lc_a, dtype=torch.float64, device="cuda", generator=g)
+            Cm = torch.zeros(lr_c * lc_c, dtype=torch.float64, device="cuda")
+            LA = costa.block_cyclic_layout(M, N, b, b, 1, 1, M, N, pm, pn, "R", 0, 0,
+                                           A.data_ptr(), lr_a, "C", rank)
+            LC = costa.block_cyclic_layout(M, N, b, b, 1, 1, M, N, world, 1, "R", 0, 0,
+                                           Cm.data_ptr(), lr_c, "C", rank)
+            wl = (f"pxgemr2d fp64 {M}x{N}, 128x128 blocks, {pm}x{pn} -> {world}x1 grid remap, "
+                  f"op N (BASELINE configs[2])" if world > 1 else
+                  f"copy slice of BASELINE configs[2]: pxgemr2d fp64 {M}x{N}, 128x128 blocks on "
+                  f"one rank (1x1 -> 1x1: every tile is a local bit copy, no remap)")
+            ref = checksum(A)
+            w.update(LA=LA, LC=LC, A=A, C=Cm, op="N", al=1.0, be=0.0, wl=wl, grid=f"{pm}x{pn}",
+                     m=M, n=N, block=b)
+            w["check"] = (lambda: torch.equal(Cm, A)) if world == 1 else (lambda: checksum(Cm) == ref)
+            return w
+        if kind == "cfg4":
+            # BASELINE configs[3] (SURVEY §8d): pztranu, c128, 128^2 blocks, alpha=(0.75,-0.5),
+            # beta=(1.25,0.25) (C is read); `edge` = the global square edge (32768 at 8 ranks),
+            # else 16384^2 per rank weak-scaled on the pm x pn grid
+            b = 128
+            M, N = (edge, edge) if edge else (n * pm, n * pn)
+            lr_a, lc_a = M // pm, N // pn
+            lr_c, lc_c = N // pm, M // pn
+            g = torch.Generator(device="cuda")
+            g.manual_seed(4321 + rank)
+            A = torch.rand(lr_a * lc_a, dtype=torch.complex128, device="cuda", generator=g)
+            Cm = torch.rand(lr_c * lc_c, dtype=torch.complex128, device="cuda", generator=g)
+            LA = costa.block_cyclic_layout(M, N, b, b, 1, 1, M, N, pm, pn, "R", 0, 0,
+                                           A.data_ptr(), lr_a, "C", rank, dtype=costa.CDOUBLE)
+            LC = costa.block_cyclic_layout(N, M, b, b, 1, 1, N, M, pm, pn, "R", 0, 0,
+                                           Cm.data_ptr(), lr_c, "C", rank, dtype=costa.CDOUBLE)
+            al, be = complex(0.75, -0.5), complex(1.25, 0.25)
+            wl = (f"pztranu c128 {M}x{N} on a {pm}x{pn} rank grid, 128x128 blocks, op T, "
+                  f"alpha=(0.75,-0.5) beta=(1.25,0.25) (BASELINE configs[3]"
+                  f"{', single-GPU slice' if world == 1 else ''}"
+                  f"{', weak-scaled 16384^2 per rank' if world > 1 and not edge else ''})")
+            w.update(LA=LA, LC=LC, A=A, C=Cm, op="T", al=al, be=be, wl=wl, grid=f"{pm}x{pn}",
+                     m=M, n=N, block=b, repeatable=False)
+            if world == 1:
+                C0 = Cm.clone()
+                nn = M
 
-        def check():  # after the first call only (beta != 0: every step changes C)
-            k = torch.randint(0, n * n, (100000,), device="cuda")
-            i, j = k % n, k // n  # C(i, j) at i + j*n; A(j, i) at j + i*n
-            exp = be * C0[k] + al * A[j + i * n]
-            assert torch.allclose(Cm[k], exp, rtol=1e-13, atol=1e-13), "cfg4 result wrong"
-    else:
+                def check():  # after the first call only (beta != 0: every step changes C)
+                    k = torch.randint(0, nn * nn, (100000,), device="cuda")
+                    i, j = k % nn, k // nn  # C(i, j) at i + j*n; A(j, i) at j + i*n
+                    exp = be * C0[k] + al * A[j + i * nn]
+                    return bool(torch.allclose(Cm[k], exp, rtol=1e-13, atol=1e-13))
+                w["check"] = check
+            return w
+        # pxtran: BASELINE configs[1] at one rank, weak-scaled 16384^2 per rank beyond
+        M, N = n * pm, n * pn  # A: M x N on pm x pn; C = A^T: N x M on the same rank grid
         lr_a, lc_a = M // pm, N // pn
         lr_c, lc_c = N // pm, M // pn
         g = torch.Generator(device="cuda")
@@ -288,88 +385,132 @@ def main():
                                        lr_a, "C", rank)
         LC = costa.block_cyclic_layout(N, M, b, b, 1, 1, N, M, pm, pn, "R", 0, 0, Cm.data_ptr(),
                                        lr_c, "C", rank)
-        op, al, be = "T", 1.0, 0.0
         wl = (("pxtran fp64 16384x16384, 256x256 blocks, op T, alpha=1 beta=0, "
                "1x1 grid (BASELINE configs[1])") if world == 1 else
               (f"pxtran fp64 weak-scaled: {M}x{N} on a {pm}x{pn} rank grid "
                f"(16384^2 per rank), 256x256 blocks, op T, alpha=1 beta=0"))
+        ref = checksum(A)
+        w.update(LA=LA, LC=LC, A=A, C=Cm, op="T", al=1.0, be=0.0, wl=wl, grid=f"{pm}x{pn}",
+                 m=M, n=N, block=b)
+        w["check"] = ((lambda: torch.equal(Cm.view(n, n), A.view(n, n).t())) if world == 1
+                      else (lambda: checksum(Cm) == ref))
+        return w
 
-        def check():
-            assert torch.equal(Cm.view(n, n), A.view(n, n).t()), "transpose result wrong"
-    torch.cuda.synchronize()
+    def measure(w, steps, warmup, planning_modes=False):
+        LA, LC, op, al, be = w["LA"], w["LC"], w["op"], w["al"], w["be"]
 
-    def step_blocking():
-        costa.transform(LA, LC, comm, op, al, be)
+        def step_blocking():
+            costa.transform(LA, LC, comm, op, al, be)
 
-    def step_async():  # stream-ordered: the host queues step k+1 while step k runs
-        costa.transform_async(LA, LC, comm, op, al, be)
+        def step_async():  # stream-ordered: the host queues step k+1 while step k runs
+            costa.transform_async(LA, LC, comm, op, al, be)
 
-    def timed(step, profile=True):
-        costa.set_profiling(profile)
+        def timed(step, profile=True):
+            costa.set_profiling(profile)
+            costa.get_stats(reset=True)
+            barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                step()
+            costa.synchronize(comm)
+            torch.cuda.synchronize()
+            barrier()
+            el = max_over_ranks(time.perf_counter() - t0)
+            st = costa.get_stats(reset=True)
+            costa.set_profiling(False)
+            return el, st
+
+        r = {}
+        # first call on these layouts: planning + descriptor upload + kernels (plan-cache miss)
+        torch.cuda.synchronize()
         costa.get_stats(reset=True)
         barrier()
-        torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        costa.synchronize(comm)
-        torch.cuda.synchronize()
-        barrier()
-        el = max_over_ranks(time.perf_counter() - t0)
-        st = costa.get_stats(reset=True)
-        costa.set_profiling(False)
-        return el, st
-
-    # first call on these layouts: planning + descriptor upload + kernels (plan-cache miss)
-    costa.get_stats(reset=True)
-    barrier()
-    t0 = time.perf_counter()
-    step_blocking()
-    first_call_ms = max_over_ranks(time.perf_counter() - t0) * 1e3
-    st0 = costa.get_stats(reset=True)
-    repeatable = args.workload != "cfg4"  # beta != 0: only the first call's result is known
-    if world == 1 and check and not repeatable:
-        check()  # before any further call changes C
-    planning = {"planner": "device" if st0["device_plans"] else "host",
-                "plan_ms": round(st0["plan_ms"], 2)}
-    if world == 1:  # warm plan-cache misses with each planner (the first call pays one-time costs)
-        for mode, key in ((1, "default"), (0, "host"), (2, "device")):
-            costa.set_planner(mode)
-            costa.release_caches()
-            t0 = time.perf_counter()
-            step_blocking()
-            sm = costa.get_stats(reset=True)
-            planning[key] = {"call_ms": round((time.perf_counter() - t0) * 1e3, 2),
-                             "plan_ms": round(sm["plan_ms"], 2),
-                             "planner": "device" if sm["device_plans"] else "host"}
-        costa.set_planner(1)
-    for _ in range(args.warmup):
         step_blocking()
-    if world == 1 and check and repeatable:  # correctness of what we time
-        check()
-    el_block, _ = timed(step_blocking, profile=False)
-    for _ in range(args.warmup):
-        step_async()
-    # value: the product as shipped (phase-timing events off: recording them costs ~11 us per
-    # step on cfg 2, tools/step_gap_probe.py); then the same K steps again with the events on,
-    # for the kernel durations (roofline.avg_launch_ms, phase_ms_per_step)
-    el, st_val = timed(step_async, profile=False)
-    el_ev, st = timed(step_async)
-    assert all(st_val[k] == st[k] for k in ("local_bytes", "pack_bytes", "unpack_bytes"))
-    if world == 1 and check and repeatable:
-        check()
+        r["first_call_ms"] = max_over_ranks(time.perf_counter() - t0) * 1e3
+        st0 = costa.get_stats(reset=True)
+        verified = []
+        if w["check"] and not w["repeatable"]:
+            verified.append(w["check"]())  # before any further call changes C
+        planning = {"planner": "device" if st0["device_plans"] else "host",
+                    "plan_ms": round(max_over_ranks(st0["plan_ms"]), 2)}
+        if planning_modes:  # warm plan-cache misses with each planner
+            for mode, key in ((1, "default"), (0, "host"), (2, "device")):
+                costa.set_planner(mode)
+                costa.release_caches()
+                t0 = time.perf_counter()
+                step_blocking()
+                sm = costa.get_stats(reset=True)
+                planning[key] = {"call_ms": round((time.perf_counter() - t0) * 1e3, 2),
+                                 "plan_ms": round(sm["plan_ms"], 2),
+                                 "planner": "device" if sm["device_plans"] else "host"}
+            costa.set_planner(1)
+        r["planning"] = planning
+        for _ in range(warmup):
+            step_blocking()
+        if w["check"] and w["repeatable"]:  # correctness of what we time
+            verified.append(w["check"]())
+        r["el_block"], _ = timed(step_blocking, profile=False)
+        for _ in range(warmup):
+            step_async()
+        # value: the product as shipped (phase-timing events off: recording them costs ~11 us per
+        # step on cfg 2, tools/step_gap_probe.py); then the same steps again with the events on,
+        # for the kernel durations (roofline.avg_launch_ms, phase_ms_per_step)
+        r["el"], st_val = timed(step_async, profile=False)
+        r["el_ev"], st = timed(step_async)
+        assert all(st_val[k] == st[k] for k in ("local_bytes", "pack_bytes", "unpack_bytes"))
+        if w["check"] and w["repeatable"]:
+            verified.append(w["check"]())
+        r["verified"] = all(verified) if verified else None
+        if r["verified"] is False:
+            raise RuntimeError(f"bench.py: wrong result for workload {w['kind']}")
+        r["st"] = st
+        alg_bytes = st["local_bytes"] + st["pack_bytes"] + st["unpack_bytes"]  # this rank
+        total = float(alg_bytes)
+        if world > 1:
+            t = torch.tensor([total], dtype=torch.float64)
+            dist.all_reduce(t)
+            total = t.item()
+        r["total_bytes"] = total
+        r["value"] = total / r["el"] / 1e9
+        # SURVEY §8(d) node figure: kernel time only (pack + local + unpack), summed bytes / max t
+        kern_ms = (st["local_ms"] + st["pack_ms"] + st["unpack_ms"]) / steps
+        r["kern_ms_max"] = max_over_ranks(kern_ms)
+        r["kernel_node"] = (total / steps / (r["kern_ms_max"] * 1e-3) / 1e9
+                            if r["kern_ms_max"] > 0 else None)
+        # this rank's kernels against the roofline; min / max over the ranks
+        own = alg_bytes / steps / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
+        r["rank_frac"] = [round(-max_over_ranks(-own) / HBM_PEAK_GBPS, 4),
+                          round(max_over_ranks(own) / HBM_PEAK_GBPS, 4)]
+        r["exchange_ms"] = max_over_ranks(st["exchange_ms"] / steps)
+        return r
 
-    alg_bytes = st["local_bytes"] + st["pack_bytes"] + st["unpack_bytes"]  # this rank, K steps
-    total_bytes = alg_bytes
-    if world > 1:
-        t = torch.tensor([float(alg_bytes)], dtype=torch.float64)
-        dist.all_reduce(t)
-        total_bytes = t.item()
-    value = total_bytes / el / 1e9
-    # SURVEY §8(d) node figure: kernel time only (pack + local + unpack), summed bytes / max t
-    kern_ms = (st["local_ms"] + st["pack_ms"] + st["unpack_ms"]) / args.steps
-    kern_ms = max_over_ranks(kern_ms)
-    kernel_node = total_bytes / args.steps / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else None
+    def summary(w, r, steps):  # one extra-config entry of the JSON line
+        out = {"workload": w["wl"], "n_gpus": world, "rccl_ranks": world if world > 1 else 0,
+               "steps": steps, "bytes_per_step": int(r["total_bytes"] / steps),
+               "ms_per_step": round(r["el"] / steps * 1e3, 4), "GBps": round(r["value"], 2),
+               "kernel_node_GBps": round(r["kernel_node"], 2) if r["kernel_node"] else None,
+               "rank_kernel_frac_min_max": r["rank_frac"],
+               "exchange_ms_per_step": round(r["exchange_ms"], 4),
+               "phase_ms_per_step": {k: round(r["st"][k + "_ms"] / steps, 4)
+                                     for k in ("pack", "local", "unpack")},
+               "first_call_ms": round(r["first_call_ms"], 2), "verified": r["verified"]}
+        for k in ("grid", "m", "n", "block"):
+            if k in w:
+                out[k] = w[k]
+        return out
+
+    wmain = build(args.workload)
+    torch.cuda.synchronize()
+    res = measure(wmain, args.steps, args.warmup, planning_modes=world == 1)
+    el, el_block, el_ev, st = res["el"], res["el_block"], res["el_ev"], res["st"]
+    total_bytes, value, kernel_node = res["total_bytes"], res["value"], res["kernel_node"]
+    op, al, be, wl = wmain["op"], wmain["al"], wmain["be"], wmain["wl"]
+    A, Cm = wmain["A"], wmain["C"]
+    n, b = args.edge, args.block
+    pm, pn = grid_for(world)
+    M, N = wmain.get("m", 0), wmain.get("n", 0)
 
     # dominant kernel: the launch list moving the most bytes on this rank
     kern = max([("local", st["local_bytes"], st["local_ms"], st["local_launches"]),
@@ -398,7 +539,7 @@ def main():
         hc = np.zeros_like(ha)
         HA = costa.block_cyclic_layout(M, N, b, b, 1, 1, M, N, pm, pn, "R", 0, 0, ha, M, "C", rank)
         HC = costa.block_cyclic_layout(N, M, b, b, 1, 1, N, M, pm, pn, "R", 0, 0, hc, N, "C", rank)
-        res = {}
+        res_e = {}
         for mode in (1, 0):  # pipelined host staging (default), then the mirror scheme
             costa.set_host_staging(mode)
             hc[:] = 0
@@ -412,16 +553,16 @@ def main():
             te = (time.perf_counter() - t1) / reps
             sx = costa.get_stats(reset=True)
             costa.set_profiling(False)
-            res[mode] = {"GBps_algorithmic": round(2 * ha.nbytes / te / 1e9, 2),
-                         "ms_per_call": round(te * 1e3, 2),
-                         "h2d_ms": round(sx["h2d_ms"] / reps, 2),
-                         "d2h_ms": round(sx["d2h_ms"] / reps, 2),
-                         "kernel_ms": round(sx["local_ms"] / reps, 3)}
+            res_e[mode] = {"GBps_algorithmic": round(2 * ha.nbytes / te / 1e9, 2),
+                           "ms_per_call": round(te * 1e3, 2),
+                           "h2d_ms": round(sx["h2d_ms"] / reps, 2),
+                           "d2h_ms": round(sx["d2h_ms"] / reps, 2),
+                           "kernel_ms": round(sx["local_ms"] / reps, 3)}
             if mode == 1:
-                res[mode].update({"groups": sx["host_groups"] // reps, "verified": ok})
+                res_e[mode].update({"groups": sx["host_groups"] // reps, "verified": ok})
         costa.set_host_staging(1)
-        e2e = dict(res[1])
-        e2e["mirror"] = res[0]
+        e2e = dict(res_e[1])
+        e2e["mirror"] = res_e[0]
         e2e["note"] = ("pageable host A and C (numpy), 2 x 2 GiB over PCIe. Pipelined (default): "
                        "64 MiB tile groups, host gather -> H2D -> tile kernels -> D2H -> host "
                        "scatter, both copy directions at once (h2d_ms/d2h_ms = span of each "
@@ -444,12 +585,39 @@ def main():
             costa.transform(SA, SC, comm, "T", 1.0, 0.0)
         overhead_us = round((time.perf_counter() - t1) / 200 * 1e6, 1)
 
+    # BASELINE's multi-GPU configurations at the GPU counts they are quoted on (the driver runs
+    # only `bench.py --gpus N`): cfg 3 at 4 GPUs, cfg 4 and cfg 5 at 8 GPUs
+    extra = {}
+    extra_plan = {4: [("cfg3", None)], 8: [("cfg4", 32768), ("cfg5", "N")]}
+    plan_x = extra_plan.get(world, [])
+    if args.extra:
+        plan_x = []
+        for item in args.extra.split(","):
+            k, _, e = item.partition(":")
+            plan_x.append((k, (int(e) if e.isdigit() else e) if e else None))
+    if args.workload == "pxtran" and not args.no_extra and plan_x:
+        for key in ("LA", "LC", "check"):
+            wmain.pop(key, None)
+        for kind, edge in plan_x:
+            costa.release_caches()
+            torch.cuda.empty_cache()
+            wx = build(kind, edge)
+            ksteps = max(1, min(args.steps, 5 if kind != "cfg5" else 10))
+            rx = measure(wx, ksteps, 1)
+            key = kind if kind not in extra else f"{kind}_{edge}"
+            extra[key] = summary(wx, rx, ksteps)
+            del wx, rx
+            costa.release_caches()
+            torch.cuda.empty_cache()
+
     cpu = None
     if want_cpu:
         port = cpu_baseline(n=n, b=b)  # our restatement of the tile loop (oracle/), same tiles
         cpu = cpu_ref or port
         if cpu_ref:
             cpu["port"] = {k: port[k] for k in ("value", "cores", "kind", "sample")}
+        else:
+            cpu["note"] = "REFERENCE BINARY ABSENT: this is our restatement (kind 'port')"
 
     if rank == 0:
         def js(x):  # complex scalars as [re, im]
@@ -458,7 +626,7 @@ def main():
                "parallelism": f"{world} rank(s), one per GPU, RCCL send/recv exchange",
                "bytes_per_step": int(total_bytes / args.steps)}
         if args.workload in ("pxtran", "cfg3", "cfg4"):
-            cfg.update({"m": M, "n": N, "block": b, "grid": f"{pm}x{pn}"})
+            cfg.update({"m": M, "n": N, "block": wmain.get("block", b), "grid": f"{pm}x{pn}"})
         line = {
             "metric": "GB/s device-resident tile pack+transpose+unpack (fp64), % HBM peak",
             "value": round(value, 2),
@@ -477,9 +645,10 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "e2e_host": e2e,
+            "verified": res["verified"],
             "call_overhead_us": overhead_us,
-            "first_call_ms": round(first_call_ms, 2),  # plan-cache miss: planning + upload + kernels
-            "planning": planning,
+            "first_call_ms": round(res["first_call_ms"], 2),  # plan-cache miss
+            "planning": res["planning"],
             "blocking": {"ms_per_step": round(el_block / args.steps * 1e3, 4),
                          "GBps": round(total_bytes / el_block / 1e9, 2),
                          "note": "costa_hip_transform (reference semantics: host waits for C)"},
@@ -491,9 +660,12 @@ def main():
                                           "pair around every phase: the source of the kernel "
                                           "durations (roofline.avg_launch_ms)"},
             "kernel_node_GBps": round(kernel_node, 2) if kernel_node else None,
+            "rank_kernel_frac_min_max": res["rank_frac"],
             "phase_ms_per_step": {k: round(st[k + "_ms"] / args.steps, 4)
                                   for k in ("pack", "local", "unpack", "exchange")},
         }
+        if extra:
+            line["baseline_configs"] = extra
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -77,10 +77,10 @@ __device__ __forceinline__ T scale(T x, T y, uint32_t kind, bool conj, T alpha, 
 }
 
 // ---- cross-lane moves ----
-__device__ __forceinline__ float shfl(float v, int l) { return __shfl(v, l); }
-__device__ __forceinline__ int shfl(int v, int l) { return __shfl(v, l); }
-__device__ __forceinline__ double shfl(double v, int l) { return __shfl(v, l); }
-__device__ __forceinline__ cpx<float> shfl(cpx<float> v, int l) {
+[[maybe_unused]] __device__ __forceinline__ float shfl(float v, int l) { return __shfl(v, l); }
+[[maybe_unused]] __device__ __forceinline__ int shfl(int v, int l) { return __shfl(v, l); }
+[[maybe_unused]] __device__ __forceinline__ double shfl(double v, int l) { return __shfl(v, l); }
+[[maybe_unused]] __device__ __forceinline__ cpx<float> shfl(cpx<float> v, int l) {
     return {__shfl(v.re, l), __shfl(v.im, l)};
 }
 
@@ -188,26 +188,68 @@ __device__ __forceinline__ void ustore(T* p, const vec<T>& in, int n) {
 
 // Lanes k = 0..V-1 of an aligned group hold in[.] = row k of a V x V block; afterwards
 // lane k holds column k.  Round r: every lane offers element (k - r) mod V and reads the
-// offer of lane (k + r) mod V.  All indices are compile-time after unrolling.
+// offer of lane (k + r) mod V.  All indices are compile-time after unrolling.  The cross-lane
+// read is a DPP quad permutation (a VALU move; V <= 4 lanes sit in one quad), not an LDS
+// permute: the large shape spends its non-overlapped LDS time on the tile itself
+// (COSTA_DPP_XCHG=0 builds the ds_bpermute form, tuning builds only).
+#ifndef COSTA_DPP_XCHG
+#define COSTA_DPP_XCHG 1
+#endif
+template <int V, int R>
+constexpr int quad_ctrl() {  // quad_perm: lane q of each quad reads lane sel(q)
+    int c = 0;
+    for (int q = 0; q < 4; ++q) {
+        const int base = q & ~(V - 1), k = q & (V - 1);
+        c |= (base + ((k + R) & (V - 1))) << (2 * q);
+    }
+    return c;
+}
+template <int CTRL, typename T>
+__device__ __forceinline__ T dpp_move(T v) {
+    static_assert(sizeof(T) % 4 == 0, "32-bit words");
+    uint32_t w[sizeof(T) / 4];
+    __builtin_memcpy(w, &v, sizeof(T));
+#pragma unroll
+    for (unsigned i = 0; i < sizeof(T) / 4; ++i)
+        w[i] = uint32_t(__builtin_amdgcn_mov_dpp(int(w[i]), CTRL, 0xF, 0xF, true));
+    T out;
+    __builtin_memcpy(&out, w, sizeof(T));
+    return out;
+}
+template <typename T, int R>
+__device__ __forceinline__ void xround(const vec<T>& in, vec<T>& out, int lane) {
+    constexpr int V = vec<T>::V;
+    const int k = lane & (V - 1);
+    const int give = (k - R) & (V - 1), from = (k + R) & (V - 1);
+    T offer = in.e[0];
+#pragma unroll
+    for (int e = 1; e < V; ++e)
+        if (e == give) offer = in.e[e];
+    T got = offer;
+    if constexpr (R != 0) {
+#if COSTA_DPP_XCHG
+        got = dpp_move<quad_ctrl<V, R>()>(offer);
+#else
+        got = shfl(offer, lane - k + from);
+#endif
+    }
+#pragma unroll
+    for (int e = 0; e < V; ++e)
+        if (e == from) out.e[e] = got;
+}
 template <typename T>
 __device__ __forceinline__ vec<T> lane_transpose(const vec<T>& in, int lane) {
     constexpr int V = vec<T>::V;
+    static_assert(V == 1 || V == 2 || V == 4, "one quad");
     vec<T> out;
     if constexpr (V == 1) {
         out = in;
     } else {
-        const int k = lane & (V - 1), base = lane - k;
-#pragma unroll
-        for (int r = 0; r < V; ++r) {
-            const int give = (k - r) & (V - 1), from = (k + r) & (V - 1);
-            T offer = in.e[0];
-#pragma unroll
-            for (int e = 1; e < V; ++e)
-                if (e == give) offer = in.e[e];
-            const T got = r == 0 ? offer : shfl(offer, base + from);
-#pragma unroll
-            for (int e = 0; e < V; ++e)
-                if (e == from) out.e[e] = got;
+        xround<T, 0>(in, out, lane);
+        xround<T, 1>(in, out, lane);
+        if constexpr (V == 4) {
+            xround<T, 2>(in, out, lane);
+            xround<T, 3>(in, out, lane);
         }
     }
     return out;

@@ -175,6 +175,15 @@ __global__ __launch_bounds__(NT) void k_pat(const double* a, double* c) {
         bi = b % 64, bj = (b % 64 + b / 64) % 64;
     } else if (ORD == -3) {  // anti-diagonal stripes with stride 8 in bj
         bi = b % 64, bj = (b / 64 + 8 * (b % 64)) % 64;
+    } else if (ORD <= -10 && ORD > -20) {  // S = -10 - ORD interleaved write streams, each
+        // walking down its own C column band (= along its own A block-row)
+        constexpr long S = ORD <= -10 && ORD > -20 ? -10 - ORD : 1;
+        const long g = b % S, t = b / S;
+        bi = g * (64 / S) + t / 64, bj = t % 64;
+    } else if (ORD <= -20) {  // the same, stream g starting at block column g * 64 / S
+        constexpr long S = ORD <= -20 ? -20 - ORD : 1;
+        const long g = b % S, t = b / S;
+        bi = g * (64 / S) + t / 64, bj = (t + g * (64 / S)) % 64;
     } else {
         constexpr long SB = ORD > 0 ? ORD : 1, NSB = 64 / SB;
         const long sb = b / (SB * SB), in = b % (SB * SB);
@@ -380,6 +389,12 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL((k_pat<BF, BS, NT, NTL, NTS, O>), dim3(unsigned(n * 2 / (BF * BS))), dim3(NT), 0, 0, \
                            (const double*)A, (double*)Cm);                                         \
     }, T, false)
+    PATO(128, 128, 1024, 1, 1, -12);
+    PATO(128, 128, 1024, 1, 1, -14);
+    PATO(128, 128, 1024, 1, 1, -18);
+    PATO(128, 128, 1024, 1, 1, -22);
+    PATO(128, 128, 1024, 1, 1, -24);
+    PATO(128, 128, 1024, 1, 1, -28);
     PATO(128, 128, 1024, 0, 0, -1);
     PATO(128, 128, 1024, 1, 1, -1);
     PATO(128, 128, 1024, 0, 0, -2);

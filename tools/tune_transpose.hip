@@ -632,6 +632,53 @@ __global__ __launch_bounds__(NT) void v_tr(const op_t* ops, const uint64_t* work
 }
 
 // ----------------------------------------------------------------------------------
+// V10: v_gen 128x128 / 1024 threads with the loads done by LDS-DMA (global_load_lds_dwordx4):
+// every source column (1 KiB) lands in one padded LDS row without passing through VGPRs and
+// without ds_write (the most expensive LDS instruction of the VGPR-staged form).
+template <int AUX, int NTS>
+__global__ __launch_bounds__(1024) void v_glds1(const op_t* ops, const uint64_t* work) {
+    constexpr int BF = 128, BS = 128, NT = 1024, P = BF + 2;
+    extern __shared__ __attribute__((aligned(16))) double tile[];
+    const uint64_t w = work[blockIdx.x];
+    const op_t op = ops[w >> 32];
+    const uint32_t sub = uint32_t(w);
+    const int nbf = op.nf / BF;
+    const int f0 = int(sub % nbf) * BF, s0 = int(sub / nbf) * BS;
+    const double* src = reinterpret_cast<const double*>(op.src) + int64_t(s0) * op.lds + f0;
+    double* dst = reinterpret_cast<double*>(op.dst) + int64_t(f0) * op.ldd + s0;
+    const int lane = threadIdx.x % 64;
+    const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / 64);
+    constexpr int NW = NT / 64;
+#pragma unroll
+    for (int k = 0; k < BS / NW; ++k) {
+        const int c = wave + NW * k;
+        __builtin_amdgcn_global_load_lds(
+            (__attribute__((address_space(1))) void*)(src + int64_t(c) * op.lds + 2 * lane),
+            (__attribute__((address_space(3))) void*)(&tile[c * P]), 16, 0, AUX);
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    constexpr int SC = BS / 64, RP = BF / 2, PS = SC * RP / NW;
+    const bool odd = lane & 1;
+    d2 y[PS];
+#pragma unroll
+    for (int k = 0; k < PS; ++k) {
+        const int t = wave + NW * k, j = t / RP, rp = t % RP;
+        y[k] = *reinterpret_cast<const d2*>(&tile[(lane + 64 * j) * P + 2 * rp]);
+    }
+#pragma unroll
+    for (int k = 0; k < PS; ++k) {
+        const int t = wave + NW * k, j = t / RP, rp = t % RP;
+        d2 v = y[k];
+        double got = __shfl_xor(odd ? v.x : v.y, 1);
+        d2 o;
+        if (!odd) { o.x = v.x; o.y = got; } else { o.x = got; o.y = v.y; }
+        d2* q = reinterpret_cast<d2*>(dst + int64_t(2 * rp + (odd ? 1 : 0)) * op.ldd + (lane & ~1) + 64 * j);
+        if (NTS) __builtin_nontemporal_store(o, q); else *q = o;
+    }
+}
+
+// ----------------------------------------------------------------------------------
 // ceiling: flat 16-B copy of the same bytes (grid-stride)
 __global__ __launch_bounds__(256) void v_copy(const d2* a, d2* c, int64_t n) {
     for (int64_t i = blockIdx.x * int64_t(256) + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256)
@@ -764,6 +811,13 @@ int main(int argc, char** argv) {
     V.push_back({"H tr 64x64 t256", [&] { hipLaunchKernelGGL((v_tr<64, 64, 256, 1, 1>), dim3(t64x64.second), dim3(256), 0, 0, d_ops, t64x64.first); }, true, {}});
     V.push_back({"H tr 128x64 t512", [&] { hipLaunchKernelGGL((v_tr<128, 64, 512, 1, 1>), dim3(t128x64.second), dim3(512), 0, 0, d_ops, t128x64.first); }, true, {}});
     V.push_back({"H tr 128x64 t256", [&] { hipLaunchKernelGGL((v_tr<128, 64, 256, 1, 1>), dim3(t128x64.second), dim3(256), 0, 0, d_ops, t128x64.first); }, true, {}});
+    {
+        const int gb = 128 * 130 * 8;
+        CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&v_glds1<2, 1>), hipFuncAttributeMaxDynamicSharedMemorySize, gb));
+        CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&v_glds1<0, 1>), hipFuncAttributeMaxDynamicSharedMemorySize, gb));
+        V.push_back({"H glds1 128x128 t1024 nt", [&, gb] { hipLaunchKernelGGL((v_glds1<2, 1>), dim3(t128x128.second), dim3(1024), gb, 0, d_ops, t128x128.first); }, true, {}});
+        V.push_back({"H glds1 128x128 t1024 ldplain", [&, gb] { hipLaunchKernelGGL((v_glds1<0, 1>), dim3(t128x128.second), dim3(1024), gb, 0, d_ops, t128x128.first); }, true, {}});
+    }
     for (int k : {1, 2}) {
         V.push_back({"H gpersist 128x128 t1024 x" + std::to_string(k), [&, k] { hipLaunchKernelGGL((v_gen_persist<128, 128, 1024, 1, 1>), dim3(cus * k), dim3(1024), 0, 0, d_ops, t128x128.first, t128x128.second); }, true, {}});
     }
