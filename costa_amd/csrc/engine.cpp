@@ -309,30 +309,15 @@ bool any_axpby(const std::vector<costa_tile_op_t>& ops) {
 // rectangular sub-ops within it (a sub-rectangle of a tile op is a tile op).  Budgets: copy
 // mode one wavefront pass of data (tiny_copy_budget), transpose mode tiny_lds_budget() of staged
 // tile (row pitch nf | 1).
-// Copy mode: three quarters of one wavefront pass (64 lanes x tiny_copy_lane_bytes) by default
-// -- an op the wavefront moves in one round trip, cut a little finer for more wavefronts in
-// flight; cfg 5 'N' 4.26 TB/s at 3 KiB against 4.15 at 4 KiB and 4.25 at 2 KiB with 64-byte
-// lanes and the XCD remap (profiles/r11/c5_budget_uc64.log; r09, 128-byte lanes without the
-// remap: 8 KiB best, profiles/r09/c5b.log).  COSTA_TINY_COPY_BUDGET (bytes, <= kTinyCopyBytes)
-// overrides.
-static int64_t tiny_copy_budget(int64_t E) {
-    static const int64_t env = [] {
-        const char* s = std::getenv("COSTA_TINY_COPY_BUDGET");
-        return s ? std::max<int64_t>(256, std::min<int64_t>(kTinyCopyBytes, std::atoll(s))) : 0;
-    }();
-    return env ? env : 48 * int64_t(tiny_copy_lane_bytes(size_t(E)));
-}
+// Copy mode: three quarters of one wavefront pass (64 lanes x tiny_copy_lane_bytes), an op the
+// wavefront moves in one round trip, cut a little finer for more wavefronts in flight; cfg 5 'N'
+// 4.26 TB/s at 3 KiB against 4.15 at 4 KiB and 4.25 at 2 KiB with 64-byte lanes and the XCD
+// remap (profiles/r11/c5_budget_uc64.log; r09, 128-byte lanes without the remap: 8 KiB best,
+// profiles/r09/c5b.log).
+int64_t tiny_copy_budget(int64_t E) { return 48 * int64_t(tiny_copy_lane_bytes(size_t(E))); }
 
-// Transpose mode: the staged tile, kTinyLdsDefault bytes of LDS per wavefront;
-// COSTA_TINY_LDS_BUDGET (bytes, <= kTinyLdsBytes) overrides (tuning).
-int64_t tiny_lds_budget() {
-    static const int64_t b = [] {
-        const char* s = std::getenv("COSTA_TINY_LDS_BUDGET");
-        return s ? std::max<int64_t>(256, std::min<int64_t>(kTinyLdsBytes, std::atoll(s)))
-                 : int64_t(kTinyLdsDefault);
-    }();
-    return b;
-}
+// Transpose mode: the staged tile, kTinyLdsDefault bytes of LDS per wavefront
+int64_t tiny_lds_budget() { return int64_t(kTinyLdsDefault); }
 
 static bool is_tiny(const costa_tile_op_t& op, int64_t E) {
     if (op.flags & COSTA_TILE_TRANSPOSE) return int64_t(op.nf | 1) * op.ns * E <= tiny_lds_budget();
@@ -416,11 +401,13 @@ void host_parallel(size_t n, F fn) {
 
 namespace {
 struct wave_knobs {  // defaults, overridable for tuning runs
-    int policy = 2;  // COSTA_WAVE_POLICY 0: only ops within the budget take the wave path (the
-                     // rest: 256-thread small shape); 1: every op below the large threshold;
-                     // 2: also large ops that are not 16-byte aligned on both sides (r11: cfg 5
-                     // geometry with doubled edges 3.41 -> 4.14 TB/s 'N', 3.47 -> 3.88 'T',
-                     // the rest unchanged; profiles/r11/c5_align_policy*.log)
+    int policy = 2;  // COSTA_WAVE_POLICY 1: every op below the large threshold takes the wave
+                     // path; 2: also large ops that are not 16-byte aligned on both sides, up to
+                     // kUnalignedWaveCap large sub-tiles of data (r11: cfg 5 geometry with
+                     // doubled edges 3.41 -> 4.14 TB/s 'N', 3.47 -> 3.88 'T', the rest
+                     // unchanged; profiles/r11/c5_align_policy*.log).  Bigger unaligned ops stay
+                     // on the large shape (its guarded path): cut into wavefront pieces, a
+                     // 16384^2 fp32 op would become ~350 k pieces of host and device list.
     int large_sort = 1;  // COSTA_LARGE_SORT 1: large ops in the order of the planner's locality
                          // hint (column-major target order: consecutive ops continue down the
                          // same target columns, so the write stream is sequential in aggregate);
@@ -436,7 +423,7 @@ struct wave_knobs {  // defaults, overridable for tuning runs
 const wave_knobs& knobs() {
     static wave_knobs k = [] {
         wave_knobs x;
-        if (const char* s = std::getenv("COSTA_WAVE_POLICY")) x.policy = std::atoi(s);
+        if (const char* s = std::getenv("COSTA_WAVE_POLICY")) x.policy = std::atoi(s) == 1 ? 1 : 2;
         if (const char* s = std::getenv("COSTA_TINY_SORT")) x.sort = std::atoi(s);
         if (const char* s = std::getenv("COSTA_LARGE_SORT")) x.large_sort = std::atoi(s);
         return x;
@@ -447,31 +434,30 @@ const wave_knobs& knobs() {
 
 work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops,
                       std::vector<costa_tile_op_t>& ordered, std::vector<uint64_t>& work) {
-    int bfl = 0, bsl = 0, bfs = 0, bss = 0;
-    tile_shapes(dtype, &bfl, &bsl, &bfs, &bss);
+    int bfl = 0, bsl = 0;
+    tile_shapes(dtype, &bfl, &bsl);
     const int64_t E = int64_t(dtype_size(dtype));
     const wave_knobs& kn = knobs();
     ordered.clear();
     work.clear();
     std::vector<const costa_tile_op_t*> wave_ops;  // ops for the wavefront path, in list order
     wave_ops.reserve(ops.size());
-    std::vector<uint64_t> small;
     const uint32_t vec_both = COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST;
-    // classify: wavefront path, or a shaped (large / small) op
+    const int64_t sub_elems = int64_t(bfl) * bsl;  // one large sub-tile
+    // classify: wavefront path, or the large shape
     std::vector<uint32_t> shaped;
-    std::vector<uint8_t> is_large;
     for (size_t li = 0; li < ops.size(); ++li) {
         const costa_tile_op_t& op = ops[li];
         if (op.nf <= 0 || op.ns <= 0) continue;
         const int64_t elems = int64_t(op.nf) * op.ns;
-        bool large = 2 * elems >= int64_t(bfl) * bsl;
-        if (kn.policy == 2 && (op.flags & vec_both) != vec_both) large = false;
-        if (is_tiny(op, E) || (!large && kn.policy >= 1)) {
+        bool large = 2 * elems >= sub_elems;
+        if (kn.policy == 2 && (op.flags & vec_both) != vec_both && elems <= kUnalignedWaveCap * sub_elems)
+            large = false;
+        if (is_tiny(op, E) || !large) {
             wave_ops.push_back(&op);
             continue;
         }
         shaped.push_back(uint32_t(li));
-        is_large.push_back(large);
     }
     // shaped ops in hint order when every one carries a hint
     std::vector<uint32_t> sperm(shaped.size());
@@ -486,15 +472,12 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     }
     for (const uint32_t k : sperm) {
         const costa_tile_op_t& op = ops[shaped[k]];
-        const bool large = is_large[k];
         const uint64_t i = ordered.size();
         if (i > 0xFFFFFFFFull) throw error(COSTA_ERR_ARG, "costa: too many tiles in one list");
         ordered.push_back(op);
-        const int bf = large ? bfl : bfs, bs = large ? bsl : bss;
-        const uint64_t n = uint64_t((op.nf + bf - 1) / bf) * uint64_t((op.ns + bs - 1) / bs);
+        const uint64_t n = uint64_t((op.nf + bfl - 1) / bfl) * uint64_t((op.ns + bsl - 1) / bsl);
         if (n > 0xFFFFFFFFull) throw error(COSTA_ERR_ARG, "costa: tile too large");
-        auto& dst = large ? work : small;
-        for (uint64_t q = 0; q < n; ++q) dst.push_back((i << 32) | q);
+        for (uint64_t q = 0; q < n; ++q) work.push_back((i << 32) | q);
     }
     // ops are independent (disjoint destinations), so any order is valid; neighbours in
     // memory run at the same time and share the partially used cache lines at their edges.
@@ -565,10 +548,8 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         at_piece[i + 1] = at_piece[i] + size_t(grid[i].nfc * grid[i].nsc);
     work_split w;
     w.n_large = int64_t(work.size());
-    w.n_small = int64_t(small.size());
     w.tiny_first = int64_t(ordered.size());
     w.n_tiny = int64_t(at_piece[nw]);
-    work.insert(work.end(), small.begin(), small.end());
     const size_t base = ordered.size();
     ordered.resize(base + at_piece[nw]);
     host_parallel(nw, [&](size_t b, size_t e) {
@@ -585,7 +566,6 @@ launch_args make_launch(const work_split& w, const void* d_ordered, const void* 
     a.ops = static_cast<const costa_tile_op_t*>(d_ordered);
     a.work = static_cast<const uint64_t*>(d_work);
     a.n_large = w.n_large;
-    a.n_small = w.n_small;
     a.tiny_first = w.tiny_first;
     a.n_tiny = w.n_tiny;
     a.src_base = src_base;

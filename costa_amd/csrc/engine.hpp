@@ -160,20 +160,25 @@ constexpr int kTinyLdsBytes = 8192;
 // r11, cfg 5 'T' with the XCD remap and 32 bytes per lane per pass: 3.80 TB/s at 4 KiB
 // against 3.0 at 8 KiB (profiles/r11/tiny_variants*.log)
 constexpr int kTinyLdsDefault = 4096;
-// staged bytes of one transposing wavefront op (kTinyLdsDefault unless COSTA_TINY_LDS_BUDGET);
+// staged bytes of one transposing wavefront op (kTinyLdsDefault);
 // the launch gives each wavefront that much LDS
 int64_t tiny_lds_budget();
 // bytes a lane of the wavefront copy path moves per pass (tile_kernels.hip tiny_copy_bytes)
 // (64 for every type since r11: 4-byte types at 128 gave cfg 5 'N' 3.77 against 4.15 TB/s once
 // the XCD remap was on, profiles/r11/c5_budget.log; fewer VGPRs, more resident wavefronts)
 constexpr int tiny_copy_lane_bytes(size_t) { return 64; }
+// bytes of one copy-mode wavefront op / of one transposing wavefront op's staged tile (the
+// budgets the host split cuts to)
+int64_t tiny_copy_budget(int64_t elem_size);
+// a large op that is not 16-byte aligned on both sides takes the wavefront path up to this many
+// large sub-tiles of data (engine.cpp wave_knobs::policy)
+constexpr int64_t kUnalignedWaveCap = 4;
 constexpr int tiny_lds_bytes = kTinyLdsBytes;
 
 struct launch_args {
     const costa_tile_op_t* ops;  // device, in build_work order: [sub-tiled ops | tiny ops]
     const uint64_t* work;   // per sub-tile: (op index << 32) | sub-tile index
     int64_t n_large;        // work items using the large sub-tile shape
-    int64_t n_small;        // work items using the small shape (after the large ones)
     int64_t tiny_first;     // ops[tiny_first, tiny_first + n_tiny) run one per wavefront
     int64_t n_tiny;
     const char* src_base;
@@ -186,14 +191,14 @@ bool any_transpose(const std::vector<costa_tile_op_t>& ops);
 bool any_axpby(const std::vector<costa_tile_op_t>& ops);
 void launch_tiles(costa_dtype_t dtype, const launch_args& a, void* stream /* hipStream_t */);
 // sub-tile shapes (elements along the source's fast dim, along its slow dim)
-void tile_shapes(costa_dtype_t dtype, int* bf_large, int* bs_large, int* bf_small, int* bs_small);
+void tile_shapes(costa_dtype_t dtype, int* bf_large, int* bs_large);
 // Execution order of an op list: `ordered` = [sub-tiled ops | tiny ops] (tiny ops sorted by the
 // planner's locality hint, so wavefronts running at the same time share partially used cache
 // lines),
 // `work` = [large-shape sub-tiles | small-shape sub-tiles], indices into `ordered`.
 struct work_split {
-    int64_t n_large = 0, n_small = 0, tiny_first = 0, n_tiny = 0;
-    int64_t n_items() const { return n_large + n_small + n_tiny; }
+    int64_t n_large = 0, tiny_first = 0, n_tiny = 0;
+    int64_t n_items() const { return n_large + n_tiny; }
 };
 work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops,
                       std::vector<costa_tile_op_t>& ordered, std::vector<uint64_t>& work);

@@ -18,8 +18,9 @@
 //   store  a lane reads one 16-byte LDS slot (V elements along f for one s); V lanes then
 //          transpose their V x V block through cross-lane shuffles, so every lane stores one
 //          16-byte vector along the destination's contiguous dimension
-// Two shapes: "large" (1024 threads, ~130 KiB LDS, 1 KiB load segments) for ops with at
-// least half a large sub-tile of data, "small" (256 threads, ~33 KiB) for the rest.
+// Two paths: the "large" shape (1024 threads, ~130 KiB LDS, 1 KiB load segments) for ops with at
+// least half a large sub-tile of data, aligned on both sides; the wavefront path (one op per
+// wavefront, ops cut to wavefront size on the host) for the rest.
 // Measured on MI355X (tools/tune_transpose.hip): the large shape moves cfg-2 transposes at
 // 91 % of the best flat 16-byte copy of the same bytes.
 #include <hip/hip_runtime.h>
@@ -155,37 +156,6 @@ __device__ __forceinline__ void vstore(T* p, const vec<T>& in, int n, bool vec_o
     }
 }
 
-// 16 bytes at 4-byte alignment: one dwordx4 access (the memory pipeline splits one that crosses
-// a cache line); element runs shorter than a vector move element by element
-typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(4)));
-
-template <typename T>
-__device__ __forceinline__ void uload(vec<T>& out, const T* p, int n) {
-    constexpr int V = vec<T>::V;
-    if (n >= V) {
-        const u32x4u r = *reinterpret_cast<const u32x4u*>(p);
-        __builtin_memcpy(&out, &r, 16);
-    } else {
-#pragma unroll
-        for (int k = 0; k < V; ++k)
-            if (k < n) out.e[k] = p[k];
-    }
-}
-
-template <typename T>
-__device__ __forceinline__ void ustore(T* p, const vec<T>& in, int n) {
-    constexpr int V = vec<T>::V;
-    if (n >= V) {
-        u32x4u r;
-        __builtin_memcpy(&r, &in, 16);
-        *reinterpret_cast<u32x4u*>(p) = r;
-    } else {
-#pragma unroll
-        for (int k = 0; k < V; ++k)
-            if (k < n) p[k] = in.e[k];
-    }
-}
-
 // Lanes k = 0..V-1 of an aligned group hold in[.] = row k of a V x V block; afterwards
 // lane k holds column k.  Round r: every lane offers element (k - r) mod V and reads the
 // offer of lane (k + r) mod V.  All indices are compile-time after unrolling.  The cross-lane
@@ -274,28 +244,13 @@ struct shape {
     static constexpr size_t lds_bytes = size_t(BS) * P * sizeof(T);
 };
 
-// large / small shapes per element size (LDS ~130 KiB / ~33 KiB)
+// the large shape per element size (1024 threads, LDS ~130 KiB, 128 KiB of data)
 template <typename T> struct shapes;
-template <> struct shapes<float> {
-    using large = shape<float, 1024, 256, 128>;
-    using small = shape<float, 256, 128, 64>;
-};
-template <> struct shapes<int> {
-    using large = shape<int, 1024, 256, 128>;
-    using small = shape<int, 256, 128, 64>;
-};
-template <> struct shapes<double> {
-    using large = shape<double, 1024, 128, 128>;
-    using small = shape<double, 256, 64, 64>;
-};
-template <> struct shapes<cpx<float>> {
-    using large = shape<cpx<float>, 1024, 128, 128>;
-    using small = shape<cpx<float>, 256, 64, 64>;
-};
-template <> struct shapes<cpx<double>> {
-    using large = shape<cpx<double>, 1024, 64, 128>;
-    using small = shape<cpx<double>, 256, 32, 64>;
-};
+template <> struct shapes<float> { using large = shape<float, 1024, 256, 128>; };
+template <> struct shapes<int> { using large = shape<int, 1024, 256, 128>; };
+template <> struct shapes<double> { using large = shape<double, 1024, 128, 128>; };
+template <> struct shapes<cpx<float>> { using large = shape<cpx<float>, 1024, 128, 128>; };
+template <> struct shapes<cpx<double>> { using large = shape<cpx<double>, 1024, 64, 128>; };
 
 // One sub-tile.  FULL: the sub-tile is a whole BF x BS block with 16-byte aligned rows on
 // both sides, so every guard below folds away and each thread issues its loads and stores
@@ -446,18 +401,21 @@ __global__ __launch_bounds__(S::NT) void tile_kernel(const costa_tile_op_t* __re
 
 // ---------------------------------------------------------------- wavefront path
 // Every op below the large shape, cut on the host into wave-sized rectangles (engine.cpp
-// split_for_waves), runs on one wavefront; by default each wavefront runs one op (K = 1 beat
-// K = 2..16 on cfg 5: more resident wavefronts beat descriptor prefetch).  Lanes walk the tile
-// in linear order: source order (f fastest) for loads, destination order for stores, with
-// (f, s) advanced by a constant per step (no per-element division).  Copy mode needs no LDS;
-// transpose mode stages the tile in the wave's own LDS region with an odd row pitch
-// (conflict-free column reads).
+// wave_pieces), runs on one wavefront.  Lanes walk the tile in linear order: source order (f
+// fastest) for loads, destination order for stores, with (f, s) advanced by a constant per step
+// (no per-element division).  Copy mode needs no LDS; transpose mode stages the tile in the
+// wave's own LDS region with an odd row pitch (conflict-free column reads).
 // Measured on BASELINE cfg 5 (242k tiles of ~33x33 fp32, 'N'): 1.8 TB/s with one 256-thread
-// workgroup per tile (too few bytes in flight per CU), 2.65 TB/s with one wavefront per op,
-// 3.35-3.5 TB/s with the directly indexed, destination-sorted list and the host split.
-// Wavefronts per workgroup: 2 for lists that transpose (8 KiB of LDS per wavefront), 8 for
-// copy-only lists (no LDS).  Measured on cfg 5 (profiles/r06/c5_knobs.log): transposes 3.1-3.3
-// TB/s at 2 against 2.95 at 4; copies 3.40 at 8 against 3.36 at 4.
+// workgroup per tile, 2.65 TB/s with one wavefront per op, 3.35-3.5 TB/s with the directly
+// indexed, destination-sorted list and the host split, 4.3-4.5 with the r11 XCD remap and
+// budgets.  What bounds it now is the access shape itself: a strided copy in whole, aligned
+// 128-byte cache lines reaches 4.8-4.9 TB/s, 256-byte runs 5.4-5.5, 1 KiB runs 6.3
+// (tools/copy_ceiling.hip "seg L*", profiles/r2/); cfg 5's column runs are ~132 bytes with
+// ragged edges.  Variants measured slower and removed: 16-byte copy accesses,
+// several ops per wavefront (strided, chunked, moved together), a persistent pipelined kernel
+// (next op's loads in flight while this op stores: 2.9 against 4.4 TB/s), nt cache policy here.
+// Wavefronts per workgroup: 2 for lists that transpose (4 KiB of LDS per wavefront), 8 for
+// copy-only lists (no LDS) (profiles/r06/c5_knobs.log).
 #ifndef COSTA_TINY_WAVES_TR  // build-time overrides for tuning builds (tools/tiny_variants.sh)
 #define COSTA_TINY_WAVES_TR 2
 #endif
@@ -479,7 +437,6 @@ template <typename T> constexpr int tiny_copy_bytes() { return tiny_copy_lane_by
 template <typename T>
 struct lin {  // (f, s) of linear element index e = f + s*n, stepped by 64
     int f, s, df, ds, n;
-    __device__ __forceinline__ lin() : f(0), s(0), df(0), ds(0), n(1) {}
     __device__ __forceinline__ lin(int lane, int n_) : n(n_) {
         f = lane % n;
         s = lane / n;
@@ -496,62 +453,6 @@ struct lin {  // (f, s) of linear element index e = f + s*n, stepped by 64
     }
 };
 
-// Copy mode with 16-byte accesses: lanes walk the op's columns in runs of V elements (a column's
-// last run may be shorter).  Tile columns start at any element, so the accesses are 4-byte
-// aligned dwordx4; per element the arithmetic is the scalar path's.  A wavefront issues 1/V of
-// the scalar path's memory instructions.  Off by default (COSTA_TINY_VCOPY=1): on cfg 5 'N' it
-// reached 3.15 TB/s against 3.35 for 4-byte accesses (profiles/r09/c5v.log), so instruction
-// issue is not what bounds the wavefront path.
-template <typename T, bool AX, int UC>
-__device__ __forceinline__ void tiny_copy_vec(const T* src, T* dst, int nf, int ns, int64_t lds,
-                                              int64_t ldd, int lane, uint32_t kind, bool conj,
-                                              T alpha, T beta) {
-    constexpr int V = vec<T>::V;
-    constexpr int UQ = UC / 16 > 0 ? UC / 16 : 1;  // runs per lane per pass
-    const int nq = (nf + V - 1) / V, total = nq * ns;
-    lin<T> p(lane, nq);
-    for (int e0 = 0; e0 < total; e0 += 64 * UQ) {
-        vec<T> x[UQ];
-        vec<T> y[AX ? UQ : 1];
-        const lin<T> q0 = p;
-#pragma unroll
-        for (int u = 0; u < UQ; ++u) {
-            if (e0 + u * 64 >= total) break;
-            if (e0 + u * 64 + lane < total) uload(x[u], src + p.s * lds + p.f * V, nf - p.f * V);
-            p.step();
-        }
-        if constexpr (AX) {
-            if (kind == COSTA_SCALE_AXPBY) {
-                lin<T> r = q0;
-#pragma unroll
-                for (int u = 0; u < UQ; ++u) {
-                    if (e0 + u * 64 >= total) break;
-                    if (e0 + u * 64 + lane < total)
-                        uload(y[u], dst + r.s * ldd + r.f * V, nf - r.f * V);
-                    r.step();
-                }
-            }
-        }
-        lin<T> q = q0;
-#pragma unroll
-        for (int u = 0; u < UQ; ++u) {
-            if (e0 + u * 64 >= total) break;
-            if (e0 + u * 64 + lane < total) {
-                vec<T> v = x[u];
-                if (kind != COSTA_SCALE_BITCOPY) {
-#pragma unroll
-                    for (int e = 0; e < V; ++e)
-                        v.e[e] = scale(v.e[e],
-                                       AX && kind == COSTA_SCALE_AXPBY ? y[AX ? u : 0].e[e] : e_zero<T>(),
-                                       kind, conj, alpha, beta);
-                }
-                ustore(dst + q.s * ldd + q.f * V, v, nf - q.f * V);
-            }
-            q.step();
-        }
-    }
-}
-
 // TR = false: the list has no transposing op (the transpose path and its registers are
 // compiled out, so copy-only lists keep a high occupancy).  AX = false: no op of the list reads
 // its destination (beta == 0 everywhere), so the copy path holds no old values.  UC: bytes per
@@ -559,7 +460,7 @@ __device__ __forceinline__ void tiny_copy_vec(const T* src, T* dst, int nf, int 
 template <typename T, int UB, bool TR, bool AX, int UC>
 __device__ __forceinline__ void tiny_op(const costa_tile_op_t& op, int lane, T* t,
                                         const char* src_base, char* dst_base,
-                                        const T* __restrict__ scalars, int vcopy) {
+                                        const T* __restrict__ scalars) {
     const uint32_t flags = op.flags;
     const uint32_t kind = (flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT;
     const bool conj = flags & COSTA_TILE_CONJ;
@@ -576,12 +477,6 @@ __device__ __forceinline__ void tiny_op(const costa_tile_op_t& op, int lane, T* 
     constexpr int U = UB / int(sizeof(T)) > 0 ? UB / int(sizeof(T)) : 1;
 
     if (!TR || !(flags & COSTA_TILE_TRANSPOSE)) {
-        if constexpr (sizeof(T) <= 8) {
-            if (vcopy) {
-                tiny_copy_vec<T, AX, UC>(src, dst, nf, ns, lds, ldd, lane, kind, conj, alpha, beta);
-                return;
-            }
-        }
         // copy mode: dst(f, s) = g(src(f, s)).  Every load of a pass is issued before the first
         // store; passes end where the op ends (wave-uniform tests), and the store walk repeats
         // the load walk instead of keeping every element's address in registers.
@@ -678,215 +573,52 @@ __device__ __forceinline__ void tiny_op(const costa_tile_op_t& op, int lane, T* 
             }
         }
     }
-    // the next op of this wave overwrites the staging area: all lanes' reads are done first
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_wave_barrier();
 }
 
-// Wave w of the grid runs ops w, w + n_waves, ... (strided: the waves resident at one time
-// work on neighbouring ops of the address-sorted list), or, with `chunked`, ops [w*K, w*K + K).
-// `xcd_remap`: blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup
-// dispatch); renumbering them so that each XCD walks one contiguous slice of the list keeps
-// neighbouring ops (which share partially written cache lines) in one L2.
+// One op per wavefront.  Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md,
+// workgroup dispatch); they are renumbered so that each XCD walks one contiguous slice of the
+// locality-ordered list, and neighbouring ops (which share partially written cache lines) meet
+// in one L2 (r11: cfg 5 'N' 3.77 against 3.58 TB/s, 'T' 3.07 against 3.00;
+// profiles/r11/c5_order.log).  Placement only changes speed, never results.
 template <typename T, int W, int UB, bool TR, bool AX, int UC>
-__global__ __launch_bounds__(64 * W) void tiny_kernel(
-    const costa_tile_op_t* __restrict__ ops, int64_t n_ops, int k_per_wave, int chunked,
-    int xcd_remap, const char* src_base, char* dst_base, const T* __restrict__ scalars,
-    int lds_per_wave, int vcopy) {
+__global__ __launch_bounds__(64 * W) void tiny_kernel(const costa_tile_op_t* __restrict__ ops,
+                                                      int64_t n_ops, const char* src_base,
+                                                      char* dst_base, const T* __restrict__ scalars,
+                                                      int lds_per_wave) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = int(threadIdx.x) % 64;
     const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / 64);
-    int64_t b = blockIdx.x;
-    if (xcd_remap) {
-        const int64_t nb = gridDim.x, x = b % 8, i = b / 8, per = nb / 8, rem = nb % 8;
-        b = x < rem ? x * (per + 1) + i : rem * (per + 1) + (x - rem) * per + i;
-    }
+    const int64_t nb = gridDim.x, x = int64_t(blockIdx.x) % 8, per = nb / 8, rem = nb % 8;
+    const int64_t i = int64_t(blockIdx.x) / 8;
+    const int64_t b = x < rem ? x * (per + 1) + i : rem * (per + 1) + (x - rem) * per + i;
     const int64_t w = b * W + wave;
-    const int64_t n_waves = int64_t(gridDim.x) * W;
-    const int64_t first = chunked ? w * k_per_wave : w;
-    const int64_t step = chunked ? 1 : n_waves;
-    const int64_t end = chunked ? min(n_ops, first + k_per_wave) : n_ops;
-    if (first >= end) return;
+    if (w >= n_ops) return;
     T* t = reinterpret_cast<T*>(smem) + int64_t(wave) * lds_per_wave;
-    costa_tile_op_t next = ops[first];
-    for (int64_t i = first; i < end; i += step) {
-        const costa_tile_op_t op = next;
-        if (i + step < end) next = ops[i + step];  // in flight while this op moves its data
-        tiny_op<T, UB, TR, AX, UC>(op, lane, t, src_base, dst_base, scalars, vcopy);
-    }
+    tiny_op<T, UB, TR, AX, UC>(ops[w], lane, t, src_base, dst_base, scalars);
 }
 
-// Copy-only lists, NP ops per wavefront moved together: the loads of all NP ops are issued
-// before the first store, so a wavefront keeps NP ops' bytes in flight for one memory round trip
-// instead of one op's (on cfg 5 a wavefront lives one load-to-store round trip and only ~5.5
-// are resident per CU).  Per element the arithmetic is tiny_op's copy mode.
-// Off by default (COSTA_TINY_MULTI=2|4): on cfg 5 'N' 3.14 / 2.66 against 3.36 TB/s with one op
-// per wavefront (profiles/r09/c5m.log).
-template <typename T, int W, bool AX, int UC, int NP>
-__global__ __launch_bounds__(64 * W) void tiny_multi_kernel(const costa_tile_op_t* __restrict__ ops,
-                                                            int64_t n_ops, const char* src_base,
-                                                            char* dst_base,
-                                                            const T* __restrict__ scalars) {
-    const int lane = int(threadIdx.x) % 64;
-    const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / 64);
-    const int64_t first = (int64_t(blockIdx.x) * W + wave) * NP;
-    if (first >= n_ops) return;
-    constexpr int UCE = UC / int(sizeof(T)) > 0 ? UC / int(sizeof(T)) : 1;
-    const T* src[NP];
-    T* dst[NP];
-    int total[NP];
-    int64_t lds[NP], ldd[NP];
-    uint32_t kind[NP];
-    bool conj[NP];
-    T alpha[NP], beta[NP];
-    lin<T> p[NP];
-    int longest = 0;
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-        total[j] = 0;
-        if (first + j >= n_ops) continue;
-        const costa_tile_op_t op = ops[first + j];
-        src[j] = reinterpret_cast<const T*>(src_base + op.src);
-        dst[j] = reinterpret_cast<T*>(dst_base + op.dst);
-        total[j] = op.nf * op.ns;
-        lds[j] = op.lds;
-        ldd[j] = op.ldd;
-        kind[j] = (op.flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT;
-        conj[j] = op.flags & COSTA_TILE_CONJ;
-        alpha[j] = beta[j] = e_zero<T>();
-        if (kind[j] >= COSTA_SCALE_ALPHA) {
-            const uint32_t slot = op.flags >> COSTA_SLOT_SHIFT;
-            alpha[j] = scalars[2 * slot];
-            beta[j] = scalars[2 * slot + 1];
-        }
-        p[j] = lin<T>(lane, op.nf);
-        longest = max(longest, total[j]);
-    }
-    for (int e0 = 0; e0 < longest; e0 += 64 * UCE) {
-        T x[NP][UCE];
-        T y[AX ? NP : 1][AX ? UCE : 1];
-        lin<T> q0[NP];
-#pragma unroll
-        for (int j = 0; j < NP; ++j) {
-            q0[j] = p[j];
-#pragma unroll
-            for (int u = 0; u < UCE; ++u) {
-                if (e0 + u * 64 >= total[j]) break;
-                if (e0 + u * 64 + lane < total[j]) x[j][u] = src[j][p[j].s * lds[j] + p[j].f];
-                p[j].step();
-            }
-        }
-        if constexpr (AX) {
-#pragma unroll
-            for (int j = 0; j < NP; ++j) {
-                if (kind[j] != COSTA_SCALE_AXPBY) continue;
-                lin<T> r = q0[j];
-#pragma unroll
-                for (int u = 0; u < UCE; ++u) {
-                    if (e0 + u * 64 >= total[j]) break;
-                    if (e0 + u * 64 + lane < total[j]) y[j][u] = dst[j][r.s * ldd[j] + r.f];
-                    r.step();
-                }
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < NP; ++j) {
-            lin<T> q = q0[j];
-#pragma unroll
-            for (int u = 0; u < UCE; ++u) {
-                if (e0 + u * 64 >= total[j]) break;
-                if (e0 + u * 64 + lane < total[j]) {
-                    T v = x[j][u];
-                    if (kind[j] != COSTA_SCALE_BITCOPY)
-                        v = scale(v, AX && kind[j] == COSTA_SCALE_AXPBY ? y[AX ? j : 0][AX ? u : 0]
-                                                                         : e_zero<T>(),
-                                  kind[j], conj[j], alpha[j], beta[j]);
-                    dst[j][q.s * ldd[j] + q.f] = v;
-                }
-                q.step();
-            }
-        }
-    }
-}
-
-struct tiny_cfg {
-    int multi = 0;      // copy-only lists: ops moved together per wavefront (0: tiny_kernel)
-    int k = 1;          // ops per wavefront
-    int chunked = 0;    // 0: strided assignment, 1: contiguous chunks
-    int copy_bytes = 0;  // 0: tiny_copy_bytes<T>()
-    int xcd = 1;  // r11: cfg 5 'N' 3.77 against 3.58 TB/s, 'T' 3.07 against 3.00
-                  // (profiles/r11/c5_order.log, band 0 rows)
-    int vcopy = 0;  // 1: copy mode with 16-byte accesses (4- and 8-byte types); measured slower
-                    // on cfg 5 'N' (3.15 against 3.35 TB/s, profiles/r09/c5v.log)
-};
-const tiny_cfg& tiny_config() {  // COSTA_TINY_{K,CHUNKED,COPY_BYTES,XCD}: tuning overrides
-    static tiny_cfg c = [] {
-        tiny_cfg x;
-        auto env = [](const char* n, int d) {
-            const char* s = std::getenv(n);
-            return s ? std::atoi(s) : d;
-        };
-        x.multi = env("COSTA_TINY_MULTI", x.multi);
-        x.k = std::max(1, env("COSTA_TINY_K", x.k));
-        x.chunked = env("COSTA_TINY_CHUNKED", x.chunked) != 0;
-        x.copy_bytes = env("COSTA_TINY_COPY_BYTES", x.copy_bytes);
-        x.xcd = env("COSTA_TINY_XCD", x.xcd) != 0;
-        x.vcopy = env("COSTA_TINY_VCOPY", x.vcopy) != 0;
-        return x;
-    }();
-    return c;
-}
-
-template <typename T, int W, bool TR, bool AX, int UC>
-void launch_tiny_v(const launch_args& a, const tiny_cfg& cfg, hipStream_t stream) {
+template <typename T, int W, bool TR, bool AX>
+void launch_tiny_v(const launch_args& a, hipStream_t stream) {
+    constexpr int UC = tiny_copy_bytes<T>();
     const int64_t n = a.n_tiny;
-    const int per_wave = a.any_transpose ? int(tiny_lds_budget() / int64_t(sizeof(T))) : 0;
+    const int per_wave = TR ? int(tiny_lds_budget() / int64_t(sizeof(T))) : 0;
     const size_t lds = size_t(per_wave) * sizeof(T) * W;
-    const int64_t waves = (n + cfg.k - 1) / cfg.k;
-    const int64_t blocks = std::min<int64_t>((waves + W - 1) / W, 1LL << 30);
-    const int k = int((n + blocks * W - 1) / (blocks * W));  // chunked: covers all ops
+    const int64_t blocks = (n + W - 1) / W;
+    if (blocks >= (int64_t(1) << 31)) throw error(COSTA_ERR_ARG, "costa: tile list too long");
     hipLaunchKernelGGL((tiny_kernel<T, W, TINY_BYTES, TR, AX, UC>), dim3(unsigned(blocks)),
-                       dim3(64 * W), lds, stream, a.ops + a.tiny_first, n, k, cfg.chunked, cfg.xcd,
-                       a.src_base, a.dst_base, static_cast<const T*>(a.scalars), per_wave,
-                       cfg.vcopy);
-}
-
-template <typename T, bool AX, int UC, int NP>
-void launch_tiny_multi(const launch_args& a, hipStream_t stream) {
-    constexpr int W = TINY_WAVES_COPY;
-    const int64_t waves = (a.n_tiny + NP - 1) / NP;
-    const int64_t blocks = (waves + W - 1) / W;
-    if (blocks >= (1LL << 31)) throw error(COSTA_ERR_ARG, "costa: tile list too long");
-    hipLaunchKernelGGL((tiny_multi_kernel<T, W, AX, UC, NP>), dim3(unsigned(blocks)), dim3(64 * W), 0,
-                       stream, a.ops + a.tiny_first, a.n_tiny, a.src_base, a.dst_base,
-                       static_cast<const T*>(a.scalars));
-}
-
-template <typename T, int UC>
-void launch_tiny_uc(const launch_args& a, const tiny_cfg& cfg, hipStream_t stream) {
-    if (!a.any_transpose && (cfg.multi == 2 || cfg.multi == 4)) {
-        constexpr int UC4 = UC / 2 >= int(sizeof(T)) ? UC / 2 : int(sizeof(T));
-        if (cfg.multi == 2)
-            return a.any_axpby ? launch_tiny_multi<T, true, UC, 2>(a, stream)
-                               : launch_tiny_multi<T, false, UC, 2>(a, stream);
-        return a.any_axpby ? launch_tiny_multi<T, true, UC4, 4>(a, stream)
-                           : launch_tiny_multi<T, false, UC4, 4>(a, stream);
-    }
-    // transposing lists: TINY_WAVES_TR wavefronts per workgroup; copy-only: TINY_WAVES_COPY
-    if (a.any_transpose)
-        return a.any_axpby ? launch_tiny_v<T, TINY_WAVES_TR, true, true, UC>(a, cfg, stream)
-                           : launch_tiny_v<T, TINY_WAVES_TR, true, false, UC>(a, cfg, stream);
-    a.any_axpby ? launch_tiny_v<T, TINY_WAVES_COPY, false, true, UC>(a, cfg, stream)
-                : launch_tiny_v<T, TINY_WAVES_COPY, false, false, UC>(a, cfg, stream);
+                       dim3(64 * W), lds, stream, a.ops + a.tiny_first, n, a.src_base, a.dst_base,
+                       static_cast<const T*>(a.scalars), per_wave);
 }
 
 template <typename T>
 void launch_tiny(const launch_args& a, hipStream_t stream) {
     if (a.n_tiny <= 0) return;
-    const tiny_cfg& cfg = tiny_config();
-    if constexpr (std::is_same<T, float>::value)  // tuning variant (cfg 5 is fp32)
-        if (cfg.copy_bytes == 64) return launch_tiny_uc<T, 64>(a, cfg, stream);
-    launch_tiny_uc<T, tiny_copy_bytes<T>()>(a, cfg, stream);
+    // transposing lists: TINY_WAVES_TR wavefronts per workgroup; copy-only: TINY_WAVES_COPY
+    if (a.any_transpose)
+        return a.any_axpby ? launch_tiny_v<T, TINY_WAVES_TR, true, true>(a, stream)
+                           : launch_tiny_v<T, TINY_WAVES_TR, true, false>(a, stream);
+    a.any_axpby ? launch_tiny_v<T, TINY_WAVES_COPY, false, true>(a, stream)
+                : launch_tiny_v<T, TINY_WAVES_COPY, false, false>(a, stream);
 }
 
 template <typename T, typename S>
@@ -904,18 +636,15 @@ void launch_shape(const launch_args& a, const uint64_t* work, int64_t n, hipStre
 
 template <typename T>
 void launch_t(const launch_args& a, hipStream_t stream) {
-    // work list: [large sub-tiles | small sub-tiles], then the tiny ops
+    // work list: the large shape's sub-tiles, then the wavefront ops
     launch_shape<T, typename shapes<T>::large>(a, a.work, a.n_large, stream);
-    launch_shape<T, typename shapes<T>::small>(a, a.work + a.n_large, a.n_small, stream);
     launch_tiny<T>(a, stream);
 }
 
 template <typename T>
-void shape_of(int* bf_l, int* bs_l, int* bf_s, int* bs_s) {
+void shape_of(int* bf_l, int* bs_l) {
     *bf_l = shapes<T>::large::BF;
     *bs_l = shapes<T>::large::BS;
-    *bf_s = shapes<T>::small::BF;
-    *bs_s = shapes<T>::small::BS;
 }
 
 template <typename T>
@@ -928,19 +657,19 @@ void set_lds_limits() {
 
 }  // namespace
 
-void tile_shapes(costa_dtype_t dtype, int* bf_large, int* bs_large, int* bf_small, int* bs_small) {
+void tile_shapes(costa_dtype_t dtype, int* bf_large, int* bs_large) {
     switch (dtype) {
-    case COSTA_FLOAT: shape_of<float>(bf_large, bs_large, bf_small, bs_small); return;
-    case COSTA_DOUBLE: shape_of<double>(bf_large, bs_large, bf_small, bs_small); return;
-    case COSTA_CFLOAT: shape_of<cpx<float>>(bf_large, bs_large, bf_small, bs_small); return;
-    case COSTA_CDOUBLE: shape_of<cpx<double>>(bf_large, bs_large, bf_small, bs_small); return;
-    case COSTA_INT32: shape_of<int>(bf_large, bs_large, bf_small, bs_small); return;
+    case COSTA_FLOAT: shape_of<float>(bf_large, bs_large); return;
+    case COSTA_DOUBLE: shape_of<double>(bf_large, bs_large); return;
+    case COSTA_CFLOAT: shape_of<cpx<float>>(bf_large, bs_large); return;
+    case COSTA_CDOUBLE: shape_of<cpx<double>>(bf_large, bs_large); return;
+    case COSTA_INT32: shape_of<int>(bf_large, bs_large); return;
     }
     throw error(COSTA_ERR_ARG, "unknown dtype");
 }
 
 void launch_tiles(costa_dtype_t dtype, const launch_args& a, void* stream) {
-    if (a.n_large + a.n_small + a.n_tiny <= 0) return;
+    if (a.n_large + a.n_tiny <= 0) return;
     static bool once = [] {
         set_lds_limits<float>();
         set_lds_limits<double>();

@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <functional>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #define CK(x)                                                                               \
@@ -236,6 +237,26 @@ __global__ __launch_bounds__(256) void k_seg_camp(const u32x4* a, u32x4* c) {
     }
 }
 
+// ---- H: flat copy with narrow lanes: W-byte accesses (4, 8, 16), U per thread, 16 KiB per
+// 256-thread WG for W = 16 (the same bytes per WG for every W: U = 64 / W * 4)
+template <int W, int NTL, int NTS>
+__global__ __launch_bounds__(256) void k_narrow(const unsigned char* a, unsigned char* c) {
+    typedef unsigned int u1 __attribute__((ext_vector_type(1)));
+    typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+    using T = typename std::conditional<W == 4, unsigned int,
+              typename std::conditional<W == 8, u2, u32x4>::type>::type;
+    constexpr int U = 16384 / (256 * W);
+    const T* s = reinterpret_cast<const T*>(a) + long(blockIdx.x) * U * 256;
+    T* d = reinterpret_cast<T*>(c) + long(blockIdx.x) * U * 256;
+    T x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) x[u] = NTL ? __builtin_nontemporal_load(s + u * 256 + threadIdx.x) : s[u * 256 + threadIdx.x];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        if (NTS) __builtin_nontemporal_store(x[u], d + u * 256 + threadIdx.x); else d[u * 256 + threadIdx.x] = x[u];
+    }
+}
+
 // ---- E: read-only and write-only streams
 template <int U, int LA>
 __global__ __launch_bounds__(256) void k_read(const u32x4* a, long n, u32x4* sink) {
@@ -371,6 +392,10 @@ int main(int argc, char** argv) {
     add("seg L" #L " ntl" #NTL " nts" #NTS, [&] {                                                 \
         hipLaunchKernelGGL((k_seg<L, NTL, NTS>), dim3(unsigned(n / 1024)), dim3(256), 0, 0, A, Cm); \
     }, T, true)
+    SEG(64, 0, 0);
+    SEG(128, 0, 0);
+    SEG(128, 1, 1);
+    SEG(256, 0, 0);
     SEG(256, 1, 1);
     SEG(512, 1, 1);
     SEG(1024, 1, 1);
@@ -432,6 +457,17 @@ int main(int argc, char** argv) {
     PAT(64, 64, 256, 0, 0);
     PAT(64, 64, 256, 1, 1);
     PAT(128, 64, 512, 1, 1);
+#define NARROW(W, NTL, NTS)                                                                       \
+    add("narrow W" #W " ntl" #NTL " nts" #NTS, [&] {                                              \
+        hipLaunchKernelGGL((k_narrow<W, NTL, NTS>), dim3(unsigned(bytes1 / 16384)), dim3(256), 0, 0, \
+                           (const unsigned char*)A, (unsigned char*)Cm);                           \
+    }, T, true)
+    NARROW(4, 0, 0);
+    NARROW(4, 1, 1);
+    NARROW(8, 0, 0);
+    NARROW(8, 1, 1);
+    NARROW(16, 0, 0);
+    NARROW(16, 1, 1);
     add("hipMemcpyDtoD", [&] { CK(hipMemcpyAsync(Cm, A, bytes1, hipMemcpyDeviceToDevice, 0)); }, T, true);
     // reads and writes alone (4 GiB of traffic each, like the copy)
     add("read U8 ld0 8/CU x2", [&] {

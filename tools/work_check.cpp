@@ -1,16 +1,22 @@
-// Invariants of the wavefront work lists (engine.cpp build_work) on BASELINE cfg 5's geometry,
-// without a GPU (block addresses are never touched).  Run by tests/test_work_lists.py.
-// For op 'N' (copy list) and 'T' (transposing list):
-//   * no op takes the large or small shapes (every cfg 5 tile is below the large threshold);
-//   * every piece fits the wavefront budget (3 KiB copy, 4 KiB staged with pitch nf | 1);
-//   * the pieces of every op (found by its unique locality hint) lie inside it and add up to it;
-//   * order: copy lists by hint, transposing lists by the op's destination address;
-//   * two builds give byte-identical lists (the threaded cut is deterministic).
+// Invariants of the work lists (engine.cpp build_work), without a GPU (block addresses are never
+// touched).  Run by tests/test_work_lists.py.
+//   cfg 5 'N' (copy list) and 'T' (transposing list) on BASELINE cfg 5's geometry:
+//     * no op takes the large shape (every cfg 5 tile is below the large threshold);
+//     * every piece fits the wavefront budget the library uses (tiny_copy_budget,
+//       tiny_lds_budget; staged pitch nf | 1);
+//     * the pieces of every op (found by its unique locality hint) lie inside it and add up to it;
+//     * order: copy lists by hint, transposing lists by the op's destination address;
+//     * two builds give byte-identical lists (the threaded cut is deterministic).
+//   a sub-list of every 8th cfg 5 op (what one exchange round's pack / unpack list looks like:
+//     hints sparse in the list, so the comparison sort replaces the counting sort): the same.
+//   unaligned large ops (fp32, lld % 4 != 0): ops up to kUnalignedWaveCap large sub-tiles are cut
+//     into wavefront pieces (the same checks), bigger ones stay on the large shape.
 // Prints "ok" and exits 0, or prints the first violation and exits 1.
 #include <cstdio>
 #include <cstring>
 #include <map>
 #include <random>
+#include <string>
 #include <vector>
 
 #include "engine.hpp"
@@ -44,67 +50,104 @@ static grid_layout<float> layout(const std::vector<int>& rs, const std::vector<i
 #define CHECK(c, ...)                                  \
     do {                                               \
         if (!(c)) {                                    \
-            std::printf("FAIL %c: ", op);              \
+            std::printf("FAIL %s: ", name.c_str());    \
             std::printf(__VA_ARGS__);                  \
             std::printf("\n");                         \
-            return 1;                                  \
+            return false;                              \
         }                                              \
     } while (0)
+
+// `ops` must carry unique, non-zero hints; expect_large: ops that must stay on the large shape
+static bool check_list(const std::string& name, costa_dtype_t dt, const std::vector<costa_tile_op_t>& ops,
+                       int64_t expect_large_ops) {
+    const int64_t E = int64_t(dtype_size(dt));
+    std::vector<costa_tile_op_t> ord, ord2;
+    std::vector<uint64_t> work, work2;
+    const work_split w = build_work(dt, ops, ord, work);
+    build_work(dt, ops, ord2, work2);
+    CHECK(w.tiny_first == expect_large_ops, "%lld ops on the large shape, expected %lld",
+          (long long)w.tiny_first, (long long)expect_large_ops);
+    CHECK(ord.size() == ord2.size() && work == work2 &&
+              std::memcmp(ord.data(), ord2.data(), ord.size() * sizeof(costa_tile_op_t)) == 0,
+          "two builds differ");
+    std::map<uint32_t, const costa_tile_op_t*> parent;
+    for (const auto& o : ops) CHECK(o.order > 0 && parent.emplace(o.order, &o).second, "hint %u not unique", o.order);
+    std::map<uint32_t, int64_t> area;
+    for (int64_t i = 0; i < w.tiny_first; ++i) {  // large-shape ops: whole, in hint order
+        const costa_tile_op_t& s = ord[size_t(i)];
+        CHECK(parent.count(s.order) && std::memcmp(&s, parent[s.order], sizeof(s)) == 0, "large op %lld", (long long)i);
+        CHECK(i == 0 || ord[size_t(i) - 1].order < s.order, "large op %lld out of hint order", (long long)i);
+        area[s.order] += int64_t(s.nf) * s.ns;
+    }
+    bool tr_list = false;
+    for (int64_t i = w.tiny_first; i < w.tiny_first + w.n_tiny; ++i)
+        tr_list = tr_list || (ord[size_t(i)].flags & COSTA_TILE_TRANSPOSE);
+    uint64_t last_key = 0;
+    for (int64_t i = w.tiny_first; i < w.tiny_first + w.n_tiny; ++i) {
+        const costa_tile_op_t& s = ord[size_t(i)];
+        const bool tr = s.flags & COSTA_TILE_TRANSPOSE;
+        const int64_t bytes = tr ? int64_t(s.nf | 1) * s.ns * E : int64_t(s.nf) * s.ns * E;
+        CHECK(bytes <= (tr ? tiny_lds_budget() : tiny_copy_budget(E)), "piece %lld over budget (%lld B)",
+              (long long)i, (long long)bytes);
+        auto it = parent.find(s.order);
+        CHECK(it != parent.end(), "piece %lld has no parent", (long long)i);
+        const costa_tile_op_t& q = *it->second;
+        CHECK(s.lds == q.lds && s.ldd == q.ldd && s.src >= q.src, "piece %lld strides", (long long)i);
+        const int64_t off = int64_t(s.src - q.src) / E, s0 = off / q.lds, f0 = off % q.lds;
+        CHECK(f0 + s.nf <= q.nf && s0 + s.ns <= q.ns, "piece %lld outside its op", (long long)i);
+        const uint64_t dst = q.dst + uint64_t((tr ? f0 * q.ldd + s0 : s0 * q.ldd + f0) * E);
+        CHECK(s.dst == dst, "piece %lld destination", (long long)i);
+        area[s.order] += int64_t(s.nf) * s.ns;
+        const uint64_t key = tr_list ? q.dst : uint64_t(q.order);
+        CHECK(key >= last_key, "piece %lld out of order", (long long)i);
+        last_key = key;
+    }
+    for (const auto& o : ops)
+        CHECK(area[o.order] == int64_t(o.nf) * o.ns, "op %u: pieces cover %lld of %lld", o.order,
+              (long long)area[o.order], (long long)(int64_t(o.nf) * o.ns));
+    std::printf("%s: %zu ops -> %lld large, %lld pieces\n", name.c_str(), ops.size(),
+                (long long)w.tiny_first, (long long)w.n_tiny);
+    return true;
+}
+
+static std::unique_ptr<plan> plan_of(const elayout& a, const elayout& c, char op, float alpha, float beta) {
+    job j;
+    j.A = &a;
+    j.C = &c;
+    j.trans = op;
+    std::memcpy(j.s.alpha.data(), &alpha, 4);
+    std::memcpy(j.s.beta.data(), &beta, 4);
+    return make_plan({j}, 0, 1);
+}
 
 int main() {
     const int n = 16384;
     auto LA = layout(splits(0xC5A1, 8, 96, n), splits(0xC5A2, 8, 96, n), uint64_t(1) << 40);
     auto LC = layout(splits(0xC5A3, 16, 160, n), splits(0xC5A4, 16, 160, n), uint64_t(1) << 41);
     elayout a = erase(LA), c = erase(LC);
-    const int64_t E = 4;
     for (char op : {'N', 'T'}) {
-        job j;
-        j.A = &a;
-        j.C = &c;
-        j.trans = op;
-        const float alpha = op == 'N' ? 1.f : -0.5f, beta = op == 'N' ? 0.f : 2.f;
-        std::memcpy(j.s.alpha.data(), &alpha, 4);
-        std::memcpy(j.s.beta.data(), &beta, 4);
-        auto p = make_plan({j}, 0, 1);
-        const auto& ops = p->local_ops;
-        std::vector<costa_tile_op_t> ord, ord2;
-        std::vector<uint64_t> work, work2;
-        const work_split w = build_work(p->dtype, ops, ord, work);
-        build_work(p->dtype, ops, ord2, work2);
-        CHECK(w.n_large == 0 && w.n_small == 0, "large %lld small %lld", (long long)w.n_large,
-              (long long)w.n_small);
-        CHECK(ord.size() == ord2.size() &&
-                  std::memcmp(ord.data(), ord2.data(), ord.size() * sizeof(costa_tile_op_t)) == 0,
-              "two builds differ");
-        std::map<uint32_t, const costa_tile_op_t*> parent;
-        for (const auto& o : ops) {
-            CHECK(o.order > 0 && parent.emplace(o.order, &o).second, "hint %u not unique", o.order);
-        }
-        std::map<uint32_t, int64_t> area;
-        uint64_t last_key = 0;
-        for (int64_t i = w.tiny_first; i < w.tiny_first + w.n_tiny; ++i) {
-            const costa_tile_op_t& s = ord[size_t(i)];
-            const bool tr = s.flags & COSTA_TILE_TRANSPOSE;
-            const int64_t bytes = tr ? int64_t(s.nf | 1) * s.ns * E : int64_t(s.nf) * s.ns * E;
-            CHECK(bytes <= (tr ? 4096 : 3072), "piece %lld over budget (%lld B)", (long long)i,
-                  (long long)bytes);
-            auto it = parent.find(s.order);
-            CHECK(it != parent.end(), "piece %lld has no parent", (long long)i);
-            const costa_tile_op_t& q = *it->second;
-            CHECK(s.lds == q.lds && s.ldd == q.ldd && s.src >= q.src, "piece %lld strides", (long long)i);
-            const int64_t off = int64_t(s.src - q.src) / E, s0 = off / q.lds, f0 = off % q.lds;
-            CHECK(f0 + s.nf <= q.nf && s0 + s.ns <= q.ns, "piece %lld outside its op", (long long)i);
-            const uint64_t dst = q.dst + uint64_t((tr ? f0 * q.ldd + s0 : s0 * q.ldd + f0) * E);
-            CHECK(s.dst == dst, "piece %lld destination", (long long)i);
-            area[s.order] += int64_t(s.nf) * s.ns;
-            const uint64_t key = tr ? q.dst : uint64_t(q.order);
-            CHECK(key >= last_key, "piece %lld out of order", (long long)i);
-            last_key = key;
-        }
-        for (const auto& o : ops)
-            CHECK(area[o.order] == int64_t(o.nf) * o.ns, "op %u: pieces cover %lld of %lld", o.order,
-                  (long long)area[o.order], (long long)(int64_t(o.nf) * o.ns));
-        std::printf("%c: %zu ops -> %lld pieces\n", op, ops.size(), (long long)w.n_tiny);
+        auto p = plan_of(a, c, op, op == 'N' ? 1.f : -0.5f, op == 'N' ? 0.f : 2.f);
+        if (!check_list(std::string("cfg5 ") + op, p->dtype, p->local_ops, 0)) return 1;
+        // one exchange round's share of a list: every 8th op (hints sparse)
+        std::vector<costa_tile_op_t> sub;
+        for (size_t i = 0; i < p->local_ops.size(); i += 8) sub.push_back(p->local_ops[i]);
+        if (!check_list(std::string("cfg5 sub-list ") + op, p->dtype, sub, 0)) return 1;
+    }
+    // unaligned large ops: fp32 4096^2 'T' with lld = 4097 (columns 4-byte aligned only)
+    for (int nb : {256, 1024}) {
+        const int m = 4096, lld = m + 1;
+        auto A = block_cyclic_layout<float>(m, m, nb, nb, 1, 1, m, m, 1, 1, 'R', 0, 0,
+                                            reinterpret_cast<float*>(uint64_t(1) << 40), lld, 'C', 0);
+        auto C = block_cyclic_layout<float>(m, m, nb, nb, 1, 1, m, m, 1, 1, 'R', 0, 0,
+                                            reinterpret_cast<float*>(uint64_t(1) << 41), lld, 'C', 0);
+        elayout ea = erase(A), ec = erase(C);
+        auto p = plan_of(ea, ec, 'T', 1.f, 0.f);
+        int bf = 0, bs = 0;
+        tile_shapes(COSTA_FLOAT, &bf, &bs);
+        const int64_t elems = int64_t(nb) * nb, sub_elems = int64_t(bf) * bs;
+        const int64_t expect = elems > kUnalignedWaveCap * sub_elems ? int64_t(p->local_ops.size()) : 0;
+        if (!check_list("unaligned " + std::to_string(nb) + "^2 blocks", p->dtype, p->local_ops, expect))
+            return 1;
     }
     std::printf("ok\n");
     return 0;
