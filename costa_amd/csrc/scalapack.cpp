@@ -6,25 +6,41 @@
 //   costa::pxgemr2d<T>     pxgemr2d/costa_pxgemr2d.cpp:14-171
 //   costa::pxtran_op<T>    pxtran_op/costa_pxtran_op.cpp:15-175  (sub(A) is n x m: :68-69)
 //   descriptor fields      scalapack.hpp:9-45; leading_dimension scalapack.cpp:37-39
-//   rank grid ordering     scalapack.cpp:3-16 (probe of Cblacs_pcoord(ctxt, 1))
 //   ctxt -> MPI_Comm       scalapack.cpp:42-53 (Cblacs_get(ctxt, 10) + Cblacs2sys_handle)
-// Difference: each matrix's process grid is read from ITS OWN descriptor context; the
-// reference builds both p?gemr2d layouts with the grid of `ictxt` (costa_pxgemr2d.cpp:47,144,
-// 157), which mis-describes A or C whenever the two grids differ.
+//   communicator           comm_union(comm_a, comm_c) (scalapack.cpp:172-185, costa_pxgemr2d.cpp:60)
+// Differences:
+//   * The transform runs on the processes of the call's context (ictxt for p?gemr2d, the common
+//     context for p?tran*), a communicator made once per context with MPI_Comm_create_group (only
+//     those processes take part) and cached; the reference takes the union of A's and C's system
+//     communicators -- the whole MPI_COMM_WORLD for ordinary grids -- and makes a new one on every
+//     call (never freed).  ScaLAPACK defines ictxt as a context holding every process of A and C.
+//   * Each matrix's process grid is read from ITS OWN descriptor context, and every grid cell is
+//     mapped to its process's rank in that communicator (Cblacs_pnum, MPI_Group_translate_ranks);
+//     the layouts are relabelled accordingly (grid_layout::reorder_ranks).  The reference builds
+//     both p?gemr2d layouts with the grid of ictxt (costa_pxgemr2d.cpp:47,144,157) and assumes
+//     grid rank = communicator rank, which mis-describes A or C whenever the grids differ.
+//   * A process outside A's (or C's) context passes desc[CTXT] = -1 and owns nothing of it; the
+//     grid shape, blocking and rank sources of that matrix come from the processes inside it
+//     (one MPI_Allreduce over the communicator).
 #include <mpi.h>
 
 #include <costa/mpi.hpp>
 #include <costa/scalapack.h>
 
+#include <algorithm>
 #include <cctype>
 #include <complex>
 #include <cstdio>
 #include <cstdlib>
+#include <map>
+#include <stdexcept>
+#include <utility>
+#include <vector>
 
 extern "C" {
 // BLACS, resolved from the application's ScaLAPACK (reference blacs.hpp:6-35)
 void Cblacs_gridinfo(int ictxt, int* nprow, int* npcol, int* myrow, int* mycol);
-void Cblacs_pcoord(int ictxt, int nodenum, int* prow, int* pcol);
+int Cblacs_pnum(int ictxt, int prow, int pcol);
 void Cblacs_get(int ictxt, int what, int* val);
 MPI_Comm Cblacs2sys_handle(int ictxt);
 }
@@ -37,43 +53,135 @@ namespace {
     std::abort();
 }
 
-MPI_Comm comm_of(int ctxt) {
+// the system communicator a BLACS context was made from: BLACS process numbers are its ranks
+MPI_Comm sys_comm(int ctxt) {
     int sys = 0;
     Cblacs_get(ctxt, 10, &sys);
     return Cblacs2sys_handle(sys);
 }
 
-// 'R' if rank 1 sits at (0, 1) of the grid, else 'C' (scalapack.cpp:3-16)
-char grid_order(int ctxt, int P) {
-    if (P <= 1) return 'C';
-    int r = -1, c = -1;
-    Cblacs_pcoord(ctxt, 1, &r, &c);
-    return (r == 0 && c == 1) ? 'R' : 'C';
-}
-
-struct grid {
-    int pm = 0, pn = 0;
-    char order = 'C';
+struct grid_info {
+    int pm = 0, pn = 0, myr = -1, myc = -1;
+    std::vector<int> pnum;  // BLACS process number of each grid cell, row-major
+    bool member() const { return pm > 0 && myr >= 0; }
 };
 
-grid grid_of(int ctxt, MPI_Comm comm) {
-    grid g;
-    int myr, myc;
-    Cblacs_gridinfo(ctxt, &g.pm, &g.pn, &myr, &myc);
-    int P = 1;
-    MPI_Comm_size(comm, &P);
-    if (g.pm < 1 || g.pn < 1)
-        throw std::runtime_error("this process is not part of the matrix's BLACS context");
-    g.order = grid_order(ctxt, P);
+grid_info grid_of(int ctxt) {
+    grid_info g;
+    if (ctxt < 0) return g;  // this process is outside the context
+    Cblacs_gridinfo(ctxt, &g.pm, &g.pn, &g.myr, &g.myc);
+    if (g.pm < 1 || g.pn < 1 || g.myr < 0) return grid_info{};
+    g.pnum.resize(size_t(g.pm) * size_t(g.pn));
+    for (int r = 0; r < g.pm; ++r)
+        for (int c = 0; c < g.pn; ++c) g.pnum[size_t(r) * g.pn + c] = Cblacs_pnum(ctxt, r, c);
     return g;
 }
 
+// The processes of `ctxt`'s grid as one communicator, rank k = grid cell k (row-major); made
+// once per (context, process set) and kept (its RCCL communicator is cached on it).
+MPI_Comm grid_comm(int ctxt, const grid_info& g) {
+    static std::map<std::pair<int, std::vector<int>>, MPI_Comm> cache;
+    auto key = std::make_pair(ctxt, g.pnum);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    MPI_Comm sys = sys_comm(ctxt), out = MPI_COMM_NULL;
+    MPI_Group all, grp;
+    MPI_Comm_group(sys, &all);
+    MPI_Group_incl(all, int(g.pnum.size()), g.pnum.data(), &grp);
+    MPI_Comm_create_group(sys, grp, 0x6c0d, &out);
+    MPI_Group_free(&grp);
+    MPI_Group_free(&all);
+    if (out == MPI_COMM_NULL) throw std::runtime_error("could not make the context's communicator");
+    cache.emplace(std::move(key), out);
+    return out;
+}
+
+// One matrix's distribution as seen in `comm`: its grid, blocking and rank sources, and the
+// rank in `comm` of every grid cell (row-major).
+struct dist {
+    int pm = 0, pn = 0, M = 0, N = 0, MB = 0, NB = 0, rsrc = 0, csrc = 0;
+    int my_cell = -1;        // this process's grid cell, -1 outside the grid
+    std::vector<int> rank;   // comm rank of each grid cell
+};
+
+// Collective over `comm`: the processes inside each matrix's context describe it, the others
+// learn it from them.
+std::vector<dist> distributions(MPI_Comm comm, const std::vector<const int*>& descs) {
+    int P = 1;
+    MPI_Comm_size(comm, &P);
+    MPI_Group cg;
+    MPI_Comm_group(comm, &cg);
+    const size_t W = 8 + size_t(P);
+    std::vector<int> buf(W * descs.size(), -1);
+    std::vector<int> mine(descs.size(), -1);
+    for (size_t d = 0; d < descs.size(); ++d) {
+        const int* desc = descs[d];
+        const grid_info g = grid_of(desc[1]);
+        if (!g.member()) continue;
+        const int cells = g.pm * g.pn;
+        if (cells > P) throw std::runtime_error("a matrix's grid is larger than the call's context");
+        int* b = &buf[W * d];
+        b[0] = g.pm;
+        b[1] = g.pn;
+        for (int k = 0; k < 6; ++k) b[2 + k] = desc[2 + k];  // M N MB NB RSRC CSRC
+        MPI_Group sg;
+        MPI_Comm_group(sys_comm(desc[1]), &sg);
+        MPI_Group_translate_ranks(sg, cells, g.pnum.data(), cg, b + 8);
+        MPI_Group_free(&sg);
+        for (int k = 0; k < cells; ++k)
+            if (b[8 + k] == MPI_UNDEFINED || b[8 + k] < 0)
+                throw std::runtime_error("a process of the matrix's grid is outside the call's context");
+        mine[d] = g.myr * g.pn + g.myc;
+    }
+    MPI_Group_free(&cg);
+    MPI_Allreduce(MPI_IN_PLACE, buf.data(), int(buf.size()), MPI_INT, MPI_MAX, comm);
+    std::vector<dist> out(descs.size());
+    for (size_t d = 0; d < descs.size(); ++d) {
+        const int* b = &buf[W * d];
+        dist& x = out[d];
+        x.pm = b[0], x.pn = b[1], x.M = b[2], x.N = b[3], x.MB = b[4], x.NB = b[5];
+        x.rsrc = b[6], x.csrc = b[7];
+        if (x.pm < 1 || x.pn < 1) throw std::runtime_error("no process holds the matrix's context");
+        x.rank.assign(b + 8, b + 8 + x.pm * x.pn);
+        x.my_cell = mine[d];
+    }
+    return out;
+}
+
+// block-cyclic layout of sub(X) in the call's communicator: built on the matrix's own grid
+// (row-major cells), then relabelled cell -> comm rank
 template <typename T>
-costa::grid_layout<T> layout_of(const int* desc, int i, int j, int sub_m, int sub_n,
-                                const grid& g, T* ptr, int rank) {
-    return costa::block_cyclic_layout<T>(desc[2], desc[3], desc[4], desc[5], i, j, sub_m, sub_n,
-                                         g.pm, g.pn, g.order, desc[6], desc[7], ptr, desc[8], 'C',
-                                         rank);
+costa::grid_layout<T> layout_of(const dist& x, int i, int j, int sub_m, int sub_n, T* ptr, int lld,
+                                int P) {
+    const int cells = x.pm * x.pn;
+    auto L = costa::block_cyclic_layout<T>(x.M, x.N, x.MB, x.NB, i, j, sub_m, sub_n, x.pm, x.pn, 'R',
+                                           x.rsrc, x.csrc, ptr, x.my_cell >= 0 ? lld : 1, 'C',
+                                           x.my_cell >= 0 ? x.my_cell : cells);
+    std::vector<int> perm(size_t(std::max(P, cells)));
+    std::vector<char> used(perm.size(), 0);
+    bool identity = true;
+    for (int k = 0; k < cells; ++k) {
+        perm[size_t(k)] = x.rank[size_t(k)];
+        used[size_t(x.rank[size_t(k)])] = 1;
+        identity = identity && x.rank[size_t(k)] == k;
+    }
+    for (size_t k = size_t(cells), r = 0; k < perm.size(); ++k) {  // the ranks outside the grid
+        while (used[r]) ++r;
+        perm[k] = int(r++);
+    }
+    if (!identity) L.reorder_ranks(perm);
+    return L;
+}
+
+template <typename T>
+void run(costa::grid_layout<T>& A, costa::grid_layout<T>& C, char op, T alpha, T beta, MPI_Comm comm) {
+#ifdef COSTA_SCALAPACK_TEST_HOOK  // CPU tests (tests/scalapack/layout_check.cpp): inspect the layouts
+    COSTA_SCALAPACK_TEST_HOOK(A, C, op, comm);
+    (void)alpha;
+    (void)beta;
+#else
+    costa::transform<T>(A, C, op, alpha, beta, costa::comm_from_mpi(comm));
+#endif
 }
 
 template <typename T>
@@ -81,13 +189,15 @@ void pxgemr2d(int m, int n, const T* a, int ia, int ja, const int* desca, T* c, 
               const int* descc, int ictxt) {
     if (m == 0 || n == 0) return;
     try {
-        MPI_Comm comm = comm_of(ictxt);
-        int rank = 0;
-        MPI_Comm_rank(comm, &rank);
-        const grid ga = grid_of(desca[1], comm), gc = grid_of(descc[1], comm);
-        auto A = layout_of<T>(desca, ia, ja, m, n, ga, const_cast<T*>(a), rank);
-        auto C = layout_of<T>(descc, ic, jc, m, n, gc, c, rank);
-        costa::transform<T>(A, C, costa::comm_from_mpi(comm));
+        const grid_info gi = grid_of(ictxt);
+        if (!gi.member()) return;  // not a process of the call's context: nothing to do
+        MPI_Comm comm = grid_comm(ictxt, gi);
+        int P = 1;
+        MPI_Comm_size(comm, &P);
+        const auto d = distributions(comm, {desca, descc});
+        auto A = layout_of<T>(d[0], ia, ja, m, n, const_cast<T*>(a), desca[8], P);
+        auto C = layout_of<T>(d[1], ic, jc, m, n, c, descc[8], P);
+        run<T>(A, C, 'N', T(1), T(0), comm);  // the no-scale transform (transform.cpp:130-160)
     } catch (const std::exception& e) {
         fatal("p?gemr2d", e);
     }
@@ -100,13 +210,15 @@ void pxtran(int m, int n, T alpha, const T* a, int ia, int ja, const int* desca,
     try {
         if (desca[1] != descc[1])
             throw std::runtime_error("A and C must share one BLACS context");  // scalapack.cpp:18-23
-        MPI_Comm comm = comm_of(desca[1]);
-        int rank = 0;
-        MPI_Comm_rank(comm, &rank);
-        const grid g = grid_of(desca[1], comm);
-        auto A = layout_of<T>(desca, ia, ja, n, m, g, const_cast<T*>(a), rank);  // n x m
-        auto C = layout_of<T>(descc, ic, jc, m, n, g, c, rank);
-        costa::transform<T>(A, C, op, alpha, beta, costa::comm_from_mpi(comm));
+        const grid_info g = grid_of(desca[1]);
+        if (!g.member()) return;
+        MPI_Comm comm = grid_comm(desca[1], g);
+        int P = 1;
+        MPI_Comm_size(comm, &P);
+        const auto d = distributions(comm, {desca, descc});
+        auto A = layout_of<T>(d[0], ia, ja, n, m, const_cast<T*>(a), desca[8], P);  // n x m
+        auto C = layout_of<T>(d[1], ic, jc, m, n, c, descc[8], P);
+        run<T>(A, C, op, alpha, beta, comm);
     } catch (const std::exception& e) {
         fatal("p?tran", e);
     }

@@ -1,5 +1,8 @@
 """ScaLAPACK drop-in: tests/scalapack/drop_in.c linked against libcosta_amd_prefixed_scalapack.so,
-MKL ScaLAPACK/BLACS and the image's MPICH (no GPU needed to link; running needs one)."""
+MKL ScaLAPACK/BLACS and the image's MPICH (no GPU needed to link; running needs one); and, on the
+CPU with 4 MPI ranks, the shims' process mapping between different BLACS grids
+(tests/scalapack/layout_check.cpp: the shim compiled with a hook that checks the layouts instead
+of transforming)."""
 import os
 import shutil
 import subprocess
@@ -56,4 +59,23 @@ def test_dropin_runs_on_gpu(tmp_path):
                         "-n", "1", str(exe)], capture_output=True, text=True, env=env,
                        timeout=300)
     print(r.stdout, r.stderr)
+    assert r.returncode == 0 and "ALL PASSED" in r.stdout, r.stdout + r.stderr
+
+
+@need_mpi
+def test_shim_process_mapping_4_ranks(tmp_path):
+    """p?gemr2d between a 2x2 grid and a 1x2 grid of two of the ranks (the other two pass
+    desc[CTXT] = -1), ictxt a permuted 1x4 grid; p?tran on a permuted column-major grid: every
+    block's owner is the communicator rank of the process BLACS puts it on, and every process's
+    local blocks are exactly the ones it owns (no GPU: the transform is replaced by the check)."""
+    exe = tmp_path / "layout_check"
+    mkl = [f"{CONDA}/lib/lib{x[2:]}.so" for x in MKL]
+    subprocess.run(["g++", "-std=c++17", "-O1", "-DCOSTA_PREFIXED", f"-I{ROOT}/include",
+                    f"-I{CONDA}/include", os.path.join(ROOT, "tests", "scalapack", "layout_check.cpp"),
+                    "-o", str(exe), f"-L{LIB}", "-lcosta_amd", *mkl, f"{CONDA}/lib/libmpi.so",
+                    f"-Wl,-rpath,{LIB}", f"-Wl,-rpath,/usr/lib/x86_64-linux-gnu:{CONDA}/lib"],
+                   check=True, timeout=300)
+    env = dict(os.environ, PATH=f"{CONDA}/bin:" + os.environ["PATH"])
+    r = subprocess.run([shutil.which("mpiexec", path=env["PATH"]) or f"{CONDA}/bin/mpiexec",
+                        "-n", "4", str(exe)], capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode == 0 and "ALL PASSED" in r.stdout, r.stdout + r.stderr
