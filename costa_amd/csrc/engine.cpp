@@ -212,11 +212,16 @@ int loopback_exchange() {
     return mode;
 }
 
+// Largest ncclSend / ncclRecv: 256 MiB by default (override COSTA_MAX_MSG_BYTES), never more
+// than 2^30 bytes.  A single self send/recv above 2^30 bytes delivered only its first half
+// (the failure starts exactly where the byte count crosses 2^30 and the lost part
+// is exactly the second of two halves, i.e. where twice the byte count passes INT32_MAX).
 size_t max_message_bytes() {
     static const size_t v = [] {
-        const char* s = std::getenv("COSTA_MAX_MSG_BYTES");  // tuning / reproduction override
+        const char* s = std::getenv("COSTA_MAX_MSG_BYTES");  // tuning override
         const long long x = s ? std::atoll(s) : 0;
-        return x > 0 ? size_t(x) : (size_t(1) << 28);       // 256 MiB
+        const size_t want = x > 0 ? size_t(x) : (size_t(1) << 28);
+        return std::min(want, size_t(1) << 30);
     }();
     return v;
 }
