@@ -175,10 +175,8 @@ costa::grid_layout<T> layout_of(const dist& x, int i, int j, int sub_m, int sub_
 
 template <typename T>
 void run(costa::grid_layout<T>& A, costa::grid_layout<T>& C, char op, T alpha, T beta, MPI_Comm comm) {
-#ifdef COSTA_SCALAPACK_TEST_HOOK  // CPU tests (tests/scalapack/layout_check.cpp): inspect the layouts
-    COSTA_SCALAPACK_TEST_HOOK(A, C, op, comm);
-    (void)alpha;
-    (void)beta;
+#ifdef COSTA_SCALAPACK_TEST_HOOK  // CPU tests (tests/scalapack/*.cpp): the layouts go to the test
+    COSTA_SCALAPACK_TEST_HOOK(A, C, op, alpha, beta, comm);
 #else
     costa::transform<T>(A, C, op, alpha, beta, costa::comm_from_mpi(comm));
 #endif

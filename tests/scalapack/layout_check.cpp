@@ -20,7 +20,7 @@
 
 template <typename T>
 void check_layouts(costa::grid_layout<T>& A, costa::grid_layout<T>& C, char op, MPI_Comm comm);
-#define COSTA_SCALAPACK_TEST_HOOK(A, C, op, comm) check_layouts(A, C, op, comm)
+#define COSTA_SCALAPACK_TEST_HOOK(A, C, op, alpha, beta, comm) check_layouts(A, C, op, comm)
 #include "../../costa_amd/csrc/scalapack.cpp"
 
 extern "C" {
