@@ -248,7 +248,11 @@ struct shape {
 template <typename T> struct shapes;
 template <> struct shapes<float> { using large = shape<float, 1024, 256, 128>; };
 template <> struct shapes<int> { using large = shape<int, 1024, 256, 128>; };
-template <> struct shapes<double> { using large = shape<double, 1024, 128, 128>; };
+#ifndef COSTA_LARGE_D_BF  // tuning builds only (tools/tiny_variants.sh)
+#define COSTA_LARGE_D_BF 128
+#define COSTA_LARGE_D_BS 128
+#endif
+template <> struct shapes<double> { using large = shape<double, 1024, COSTA_LARGE_D_BF, COSTA_LARGE_D_BS>; };
 template <> struct shapes<cpx<float>> { using large = shape<cpx<float>, 1024, 128, 128>; };
 template <> struct shapes<cpx<double>> { using large = shape<cpx<double>, 1024, 64, 128>; };
 
