@@ -413,13 +413,20 @@ struct wave_knobs {  // defaults, overridable for tuning runs
                      // unchanged; profiles/r11/c5_align_policy*.log).  Bigger unaligned ops stay
                      // on the large shape (its guarded path): cut into wavefront pieces, a
                      // 16384^2 fp32 op would become ~350 k pieces of host and device list.
-    int large_sort = 1;  // COSTA_LARGE_SORT 1: large ops in the order of the planner's locality
+    int large_sort = 3;  // COSTA_LARGE_SORT 1: large ops in the order of the planner's locality
                          // hint (column-major target order: consecutive ops continue down the
                          // same target columns, so the write stream is sequential in aggregate);
                          // 0: list order (the reference's message order: target row-major, every
                          // op a new target column at the same in-column offset, which camps on
                          // HBM channels; tools/copy_ceiling.hip "pat ... ord-1" 6.27 against 5.64
-                         // TB/s, "segcamp" 4.4-4.9 against 6.4)
+                         // TB/s, "segcamp" 4.4-4.9 against 6.4); 2: 1, then the sub-tiles by
+                         // the address of their first destination element (one sub-tile-wide
+                         // band of target columns at a time, instead of an op's 2-4 sub-tiles
+                         // side by side); 3 (default): 2 for lists whose large ops all transpose
+                         // 8-byte elements (fp64 / c64 'T' 16384^2: 0.710 against 0.747 ms with
+                         // 256^2 blocks, 0.709 against 0.797 with 512^2), else 1 (c128 with 128^2
+                         // blocks: 2.87 against 2.27 ms; fp32 even; copy lists untested under 2;
+                         // tools/order_run.sh, profiles/r2/order/)
     int sort = 4;    // COSTA_TINY_SORT 0: list order, 1: by source, 2: by destination address,
                      // 3: by the planner's locality hint (costa_tile_op_t::order), 4: 3 for
                      // copy-only lists, 2 for lists that transpose (cfg 5 'T' 3.88 against
@@ -467,7 +474,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     // shaped ops in hint order when every one carries a hint
     std::vector<uint32_t> sperm(shaped.size());
     for (size_t i = 0; i < shaped.size(); ++i) sperm[i] = uint32_t(i);
-    if (kn.large_sort == 1 && !shaped.empty()) {
+    if (kn.large_sort >= 1 && !shaped.empty()) {
         bool hints = true;
         for (uint32_t li : shaped) hints = hints && ops[li].order != 0;
         if (hints)
@@ -483,6 +490,26 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         const uint64_t n = uint64_t((op.nf + bfl - 1) / bfl) * uint64_t((op.ns + bsl - 1) / bsl);
         if (n > 0xFFFFFFFFull) throw error(COSTA_ERR_ARG, "costa: tile too large");
         for (uint64_t q = 0; q < n; ++q) work.push_back((i << 32) | q);
+    }
+    bool by_address = kn.large_sort == 2;
+    if (kn.large_sort == 3) {
+        by_address = E == 8 && !ordered.empty();
+        for (const auto& op : ordered) by_address = by_address && (op.flags & COSTA_TILE_TRANSPOSE);
+    }
+    if (by_address && work.size() > 1) {
+        // sub-tiles by the address of their first destination element (stable)
+        std::vector<std::pair<uint64_t, uint64_t>> key(work.size());
+        for (size_t x = 0; x < work.size(); ++x) {
+            const costa_tile_op_t& op = ordered[size_t(work[x] >> 32)];
+            const uint64_t q = work[x] & 0xFFFFFFFFull, nbf = uint64_t((op.nf + bfl - 1) / bfl);
+            const int64_t f0 = int64_t(q % nbf) * bfl, s0 = int64_t(q / nbf) * bsl;
+            const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
+            key[x] = {op.dst + uint64_t((tr ? f0 * op.ldd + s0 : s0 * op.ldd + f0) * E), uint64_t(x)};
+        }
+        std::sort(key.begin(), key.end());
+        std::vector<uint64_t> w2(work.size());
+        for (size_t x = 0; x < work.size(); ++x) w2[x] = work[size_t(key[x].second)];
+        work.swap(w2);
     }
     // ops are independent (disjoint destinations), so any order is valid; neighbours in
     // memory run at the same time and share the partially used cache lines at their edges.

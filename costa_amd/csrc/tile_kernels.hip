@@ -207,6 +207,11 @@ __device__ __forceinline__ void xround(const vec<T>& in, vec<T>& out, int lane) 
     for (int e = 0; e < V; ++e)
         if (e == from) out.e[e] = got;
 }
+// a[k] for a lane-dependent k in 0..3, as selects (a runtime-indexed vec<T> lives in scratch)
+template <typename T>
+__device__ __forceinline__ T sel4(int k, T a0, T a1, T a2, T a3) {
+    return k == 0 ? a0 : k == 1 ? a1 : k == 2 ? a2 : a3;
+}
 template <typename T>
 __device__ __forceinline__ vec<T> lane_transpose(const vec<T>& in, int lane) {
     constexpr int V = vec<T>::V;
@@ -214,13 +219,34 @@ __device__ __forceinline__ vec<T> lane_transpose(const vec<T>& in, int lane) {
     vec<T> out;
     if constexpr (V == 1) {
         out = in;
-    } else {
+    } else if constexpr (V == 2) {
         xround<T, 0>(in, out, lane);
         xround<T, 1>(in, out, lane);
-        if constexpr (V == 4) {
-            xround<T, 2>(in, out, lane);
-            xround<T, 3>(in, out, lane);
-        }
+    } else {
+        // V = 4 (4-byte elements), every index compile-time: lane k rotates its row by k
+        // (r[e] = in[(e + k) & 3]), so in round R every lane offers r[R] and lane k receives
+        // in_{k-R}[k]; out[e] = g[(k - e) & 3] un-rotates (r13: the runtime-indexed form of
+        // xround kept 144 bytes per lane in scratch and ran fp32 transposes at 3.3 TB/s)
+        const int k = lane & 3;
+        const T r0 = sel4(k, in.e[0], in.e[1], in.e[2], in.e[3]);
+        const T r1 = sel4(k, in.e[1], in.e[2], in.e[3], in.e[0]);
+        const T r2 = sel4(k, in.e[2], in.e[3], in.e[0], in.e[1]);
+        const T r3 = sel4(k, in.e[3], in.e[0], in.e[1], in.e[2]);
+#if COSTA_DPP_XCHG
+        const T g0 = r0;
+        const T g1 = dpp_move<quad_ctrl<4, 3>()>(r1);  // from lane (k - 1) & 3
+        const T g2 = dpp_move<quad_ctrl<4, 2>()>(r2);  // from lane (k - 2) & 3
+        const T g3 = dpp_move<quad_ctrl<4, 1>()>(r3);  // from lane (k - 3) & 3
+#else
+        const T g0 = r0;
+        const T g1 = shfl(r1, lane - k + ((k + 3) & 3));
+        const T g2 = shfl(r2, lane - k + ((k + 2) & 3));
+        const T g3 = shfl(r3, lane - k + ((k + 1) & 3));
+#endif
+        out.e[0] = sel4(k, g0, g1, g2, g3);
+        out.e[1] = sel4(k, g3, g0, g1, g2);
+        out.e[2] = sel4(k, g2, g3, g0, g1);
+        out.e[3] = sel4(k, g1, g2, g3, g0);
     }
     return out;
 }
@@ -246,7 +272,11 @@ struct shape {
 
 // the large shape per element size (1024 threads, LDS ~130 KiB, 128 KiB of data)
 template <typename T> struct shapes;
-template <> struct shapes<float> { using large = shape<float, 1024, 256, 128>; };
+#ifndef COSTA_LARGE_F_BF  // tuning builds only (tools/tiny_variants.sh)
+#define COSTA_LARGE_F_BF 256
+#define COSTA_LARGE_F_BS 128
+#endif
+template <> struct shapes<float> { using large = shape<float, 1024, COSTA_LARGE_F_BF, COSTA_LARGE_F_BS>; };
 template <> struct shapes<int> { using large = shape<int, 1024, 256, 128>; };
 #ifndef COSTA_LARGE_D_BF  // tuning builds only (tools/tiny_variants.sh)
 #define COSTA_LARGE_D_BF 128
