@@ -447,7 +447,8 @@ const wave_knobs& knobs() {
 work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops,
                       std::vector<costa_tile_op_t>& ordered, std::vector<uint64_t>& work) {
     int bfl = 0, bsl = 0;
-    tile_shapes(dtype, &bfl, &bsl);
+    const bool tr_shape = any_transpose(ops);
+    tile_shapes(dtype, tr_shape, &bfl, &bsl);
     const int64_t E = int64_t(dtype_size(dtype));
     const wave_knobs& kn = knobs();
     ordered.clear();
@@ -579,6 +580,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     for (size_t i = 0; i < nw; ++i)
         at_piece[i + 1] = at_piece[i] + size_t(grid[i].nfc * grid[i].nsc);
     work_split w;
+    w.tr_shape = tr_shape;
     w.n_large = int64_t(work.size());
     w.tiny_first = int64_t(ordered.size());
     w.n_tiny = int64_t(at_piece[nw]);
@@ -605,6 +607,7 @@ launch_args make_launch(const work_split& w, const void* d_ordered, const void* 
     a.scalars = d_scalars;
     a.any_transpose = transpose;
     a.any_axpby = axpby;
+    a.tr_shape = w.tr_shape;
     return a;
 }
 

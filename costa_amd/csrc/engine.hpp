@@ -186,18 +186,21 @@ struct launch_args {
     const void* scalars;    // device: n_slots x (alpha, beta) of the dtype
     bool any_transpose;     // false: copy-mode ops only, launch without the LDS tile
     bool any_axpby;         // false: no op reads its destination (beta == 0 everywhere)
+    bool tr_shape;          // the work items are sub-tiles of the transposing lists' shape
 };
 bool any_transpose(const std::vector<costa_tile_op_t>& ops);
 bool any_axpby(const std::vector<costa_tile_op_t>& ops);
 void launch_tiles(costa_dtype_t dtype, const launch_args& a, void* stream /* hipStream_t */);
-// sub-tile shapes (elements along the source's fast dim, along its slow dim)
-void tile_shapes(costa_dtype_t dtype, int* bf_large, int* bs_large);
+// sub-tile shape (elements along the source's fast dim, along its slow dim) of a copy-only list
+// or of a list with transposing ops
+void tile_shapes(costa_dtype_t dtype, bool transposing_list, int* bf_large, int* bs_large);
 // Execution order of an op list: `ordered` = [sub-tiled ops | tiny ops] (tiny ops sorted by the
 // planner's locality hint, so wavefronts running at the same time share partially used cache
 // lines),
 // `work` = [large-shape sub-tiles | small-shape sub-tiles], indices into `ordered`.
 struct work_split {
     int64_t n_large = 0, tiny_first = 0, n_tiny = 0;
+    bool tr_shape = false;  // sub-tiles cut with tile_shapes(dtype, true, ...)
     int64_t n_items() const { return n_large + n_tiny; }
 };
 work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops,

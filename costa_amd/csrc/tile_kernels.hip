@@ -18,11 +18,11 @@
 //   store  a lane reads one 16-byte LDS slot (V elements along f for one s); V lanes then
 //          transpose their V x V block through cross-lane shuffles, so every lane stores one
 //          16-byte vector along the destination's contiguous dimension
-// Two paths: the "large" shape (1024 threads, ~130 KiB LDS, 1 KiB load segments) for ops with at
-// least half a large sub-tile of data, aligned on both sides; the wavefront path (one op per
-// wavefront, ops cut to wavefront size on the host) for the rest.
-// Measured on MI355X (tools/tune_transpose.hip): the large shape moves cfg-2 transposes at
-// 91 % of the best flat 16-byte copy of the same bytes.
+// Two paths: the "large" shape (512 or 1024 threads, 64 or 128 KiB sub-tiles, 512 B - 1 KiB load
+// segments; `shapes` below) for ops with at least half a large sub-tile of data, aligned on both
+// sides; the wavefront path (one op per wavefront, ops cut to wavefront size on the host) for
+// the rest.  Measured on MI355X: cfg 2's transposes run at the rate a plain copy with the same
+// access pattern reaches (tools/copy_ceiling.hip "pat").
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -270,21 +270,48 @@ struct shape {
     static constexpr size_t lds_bytes = size_t(BS) * P * sizeof(T);
 };
 
-// the large shape per element size (1024 threads, LDS ~130 KiB, 128 KiB of data)
-template <typename T> struct shapes;
-#ifndef COSTA_LARGE_F_BF  // tuning builds only (tools/tiny_variants.sh)
-#define COSTA_LARGE_F_BF 256
+// the large shapes per element size: `large` for copy-only lists, `large_tr` for lists that
+// transpose.  Transposes of fp64 / fp32 / int32 take 512 threads and 64 KiB sub-tiles (~67 KiB
+// of LDS: two workgroups per CU, whose load and store phases overlap); copies, and c64 / c128,
+// 1024 threads and 128 KiB (copies stream 1 KiB column segments; c64 and c128 gained nothing
+// from the halving).  Measured on 16384^2 (r2, tools/shape_sweep.sh, profiles/r2/shapes/):
+// fp64 'T' 64 x 128 against 128 x 128 / 1024 threads 0.698 against 0.712 ms with 256^2 and
+// 128^2 blocks, 0.779 against 1.057 with 64^2 blocks (those went to the wavefront path);
+// 128 x 64 slower (0.765-0.811); fp32 'T' 128 x 128 against 256 x 128 / 1024 threads 0.367
+// against 0.578 ms with 128^2 blocks (half-filled sub-tiles before), 0.397 against 0.402 with
+// 256^2; the copy of BASELINE cfg 3 (fp64, 128^2 blocks) 3.17 ms with 64 x 128 against 2.87 with
+// 128 x 128.  COSTA_LARGE_{D,F}_{NT,BF,BS}: tuning builds only (tools/tiny_variants.sh).
+#ifndef COSTA_LARGE_F_BF
+#define COSTA_LARGE_F_NT 512
+#define COSTA_LARGE_F_BF 128
 #define COSTA_LARGE_F_BS 128
 #endif
-template <> struct shapes<float> { using large = shape<float, 1024, COSTA_LARGE_F_BF, COSTA_LARGE_F_BS>; };
-template <> struct shapes<int> { using large = shape<int, 1024, 256, 128>; };
-#ifndef COSTA_LARGE_D_BF  // tuning builds only (tools/tiny_variants.sh)
-#define COSTA_LARGE_D_BF 128
+#ifndef COSTA_LARGE_D_BF
+#define COSTA_LARGE_D_NT 512
+#define COSTA_LARGE_D_BF 64
 #define COSTA_LARGE_D_BS 128
 #endif
-template <> struct shapes<double> { using large = shape<double, 1024, COSTA_LARGE_D_BF, COSTA_LARGE_D_BS>; };
-template <> struct shapes<cpx<float>> { using large = shape<cpx<float>, 1024, 128, 128>; };
-template <> struct shapes<cpx<double>> { using large = shape<cpx<double>, 1024, 64, 128>; };
+template <typename T> struct shapes;
+template <> struct shapes<float> {
+    using large = shape<float, 1024, 256, 128>;
+    using large_tr = shape<float, COSTA_LARGE_F_NT, COSTA_LARGE_F_BF, COSTA_LARGE_F_BS>;
+};
+template <> struct shapes<int> {
+    using large = shape<int, 1024, 256, 128>;
+    using large_tr = shape<int, COSTA_LARGE_F_NT, COSTA_LARGE_F_BF, COSTA_LARGE_F_BS>;
+};
+template <> struct shapes<double> {
+    using large = shape<double, 1024, 128, 128>;
+    using large_tr = shape<double, COSTA_LARGE_D_NT, COSTA_LARGE_D_BF, COSTA_LARGE_D_BS>;
+};
+template <> struct shapes<cpx<float>> {
+    using large = shape<cpx<float>, 1024, 128, 128>;
+    using large_tr = large;
+};
+template <> struct shapes<cpx<double>> {
+    using large = shape<cpx<double>, 1024, 64, 128>;
+    using large_tr = large;
+};
 
 // One sub-tile.  FULL: the sub-tile is a whole BF x BS block with 16-byte aligned rows on
 // both sides, so every guard below folds away and each thread issues its loads and stores
@@ -670,34 +697,43 @@ void launch_shape(const launch_args& a, const uint64_t* work, int64_t n, hipStre
 
 template <typename T>
 void launch_t(const launch_args& a, hipStream_t stream) {
-    // work list: the large shape's sub-tiles, then the wavefront ops
-    launch_shape<T, typename shapes<T>::large>(a, a.work, a.n_large, stream);
+    // work list: the large shape's sub-tiles (the list's shape: build_work cut them with
+    // tile_shapes(dtype, tr_shape)), then the wavefront ops
+    if (a.tr_shape)
+        launch_shape<T, typename shapes<T>::large_tr>(a, a.work, a.n_large, stream);
+    else
+        launch_shape<T, typename shapes<T>::large>(a, a.work, a.n_large, stream);
     launch_tiny<T>(a, stream);
 }
 
 template <typename T>
-void shape_of(int* bf_l, int* bs_l) {
-    *bf_l = shapes<T>::large::BF;
-    *bs_l = shapes<T>::large::BS;
+void shape_of(bool tr, int* bf_l, int* bs_l) {
+    *bf_l = tr ? shapes<T>::large_tr::BF : shapes<T>::large::BF;
+    *bs_l = tr ? shapes<T>::large_tr::BS : shapes<T>::large::BS;
 }
 
+template <typename T, typename S>
+void set_lds_limit() {
+    // the large shapes need more than the default dynamic-LDS limit
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tile_kernel<T, S>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, int(S::lds_bytes));
+}
 template <typename T>
 void set_lds_limits() {
-    // the large shape needs more than the default dynamic-LDS limit
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tile_kernel<T, typename shapes<T>::large>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                              int(shapes<T>::large::lds_bytes));
+    set_lds_limit<T, typename shapes<T>::large>();
+    set_lds_limit<T, typename shapes<T>::large_tr>();
 }
 
 }  // namespace
 
-void tile_shapes(costa_dtype_t dtype, int* bf_large, int* bs_large) {
+void tile_shapes(costa_dtype_t dtype, bool transposing_list, int* bf_large, int* bs_large) {
+    const bool t = transposing_list;
     switch (dtype) {
-    case COSTA_FLOAT: shape_of<float>(bf_large, bs_large); return;
-    case COSTA_DOUBLE: shape_of<double>(bf_large, bs_large); return;
-    case COSTA_CFLOAT: shape_of<cpx<float>>(bf_large, bs_large); return;
-    case COSTA_CDOUBLE: shape_of<cpx<double>>(bf_large, bs_large); return;
-    case COSTA_INT32: shape_of<int>(bf_large, bs_large); return;
+    case COSTA_FLOAT: shape_of<float>(t, bf_large, bs_large); return;
+    case COSTA_DOUBLE: shape_of<double>(t, bf_large, bs_large); return;
+    case COSTA_CFLOAT: shape_of<cpx<float>>(t, bf_large, bs_large); return;
+    case COSTA_CDOUBLE: shape_of<cpx<double>>(t, bf_large, bs_large); return;
+    case COSTA_INT32: shape_of<int>(t, bf_large, bs_large); return;
     }
     throw error(COSTA_ERR_ARG, "unknown dtype");
 }

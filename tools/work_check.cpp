@@ -143,7 +143,7 @@ int main() {
         elayout ea = erase(A), ec = erase(C);
         auto p = plan_of(ea, ec, 'T', 1.f, 0.f);
         int bf = 0, bs = 0;
-        tile_shapes(COSTA_FLOAT, &bf, &bs);
+        tile_shapes(COSTA_FLOAT, true, &bf, &bs);  // a transposing list
         const int64_t elems = int64_t(nb) * nb, sub_elems = int64_t(bf) * bs;
         const int64_t expect = elems > kUnalignedWaveCap * sub_elems ? int64_t(p->local_ops.size()) : 0;
         if (!check_list("unaligned " + std::to_string(nb) + "^2 blocks", p->dtype, p->local_ops, expect))
