@@ -446,9 +446,9 @@ const wave_knobs& knobs() {
 
 work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops,
                       std::vector<costa_tile_op_t>& ordered, std::vector<uint64_t>& work) {
-    int bfl = 0, bsl = 0;
     const bool tr_shape = any_transpose(ops);
-    tile_shapes(dtype, tr_shape, &bfl, &bsl);
+    shape_dims sh;
+    tile_shapes(dtype, tr_shape, &sh);
     const int64_t E = int64_t(dtype_size(dtype));
     const wave_knobs& kn = knobs();
     ordered.clear();
@@ -456,61 +456,83 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     std::vector<const costa_tile_op_t*> wave_ops;  // ops for the wavefront path, in list order
     wave_ops.reserve(ops.size());
     const uint32_t vec_both = COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST;
-    const int64_t sub_elems = int64_t(bfl) * bsl;  // one large sub-tile
-    // classify: wavefront path, or the large shape
-    std::vector<uint32_t> shaped;
+    const int64_t sub_elems = int64_t(sh.bf) * sh.bs;                // one large sub-tile
+    const int64_t med_elems = int64_t(sh.bf_m) * sh.bs_m;            // one medium sub-tile (0: none)
+    // classify: wavefront path, the medium shape (aligned ops of at least half its sub-tile, in
+    // lists that transpose) or the large shape
+    // (a medium launch of fewer than kMinMediumOps ops costs more than it saves: it runs ahead of
+    // the wavefront kernel, not beside it; cfg 5 'T' with its 969 medium ops 0.802 against 0.791
+    // ms without, profiles/r2/shapes/ab_medium_cfg5T.log)
+    constexpr size_t kMinMediumOps = 4096;
+    std::vector<uint8_t> cls(ops.size(), 3);  // 0 large, 1 medium, 2 wavefront, 3 empty
+    size_t n_med = 0;
     for (size_t li = 0; li < ops.size(); ++li) {
         const costa_tile_op_t& op = ops[li];
         if (op.nf <= 0 || op.ns <= 0) continue;
         const int64_t elems = int64_t(op.nf) * op.ns;
+        const bool aligned = (op.flags & vec_both) == vec_both;
         bool large = 2 * elems >= sub_elems;
-        if (kn.policy == 2 && (op.flags & vec_both) != vec_both && elems <= kUnalignedWaveCap * sub_elems)
-            large = false;
-        if (is_tiny(op, E) || !large) {
-            wave_ops.push_back(&op);
-            continue;
+        if (kn.policy == 2 && !aligned && elems <= kUnalignedWaveCap * sub_elems) large = false;
+        if (large && !is_tiny(op, E))
+            cls[li] = 0;
+        else if (med_elems > 0 && aligned && 2 * elems >= med_elems && (op.flags & COSTA_TILE_TRANSPOSE))
+            cls[li] = 1, ++n_med;
+        else
+            cls[li] = 2;
+    }
+    std::vector<uint32_t> shaped[2];  // [0] large, [1] medium
+    for (size_t li = 0; li < ops.size(); ++li) {
+        const int c = cls[li] == 1 && n_med < kMinMediumOps ? 2 : cls[li];
+        if (c < 2) shaped[c].push_back(uint32_t(li));
+        else if (c == 2) wave_ops.push_back(&ops[li]);
+    }
+    // each shape's ops in hint order when every one carries a hint; lists whose shaped ops all
+    // transpose 8-byte elements then take the sub-tiles in destination-address order (wave_knobs)
+    int64_t n_work[2] = {0, 0};
+    for (int c = 0; c < 2; ++c) {
+        const int bf = c ? sh.bf_m : sh.bf, bs = c ? sh.bs_m : sh.bs;
+        const std::vector<uint32_t>& sel = shaped[c];
+        std::vector<uint32_t> sperm(sel.size());
+        for (size_t i = 0; i < sel.size(); ++i) sperm[i] = uint32_t(i);
+        if (kn.large_sort >= 1 && !sel.empty()) {
+            bool hints = true;
+            for (uint32_t li : sel) hints = hints && ops[li].order != 0;
+            if (hints)
+                std::stable_sort(sperm.begin(), sperm.end(), [&](uint32_t x, uint32_t y) {
+                    return ops[sel[x]].order < ops[sel[y]].order;
+                });
         }
-        shaped.push_back(uint32_t(li));
-    }
-    // shaped ops in hint order when every one carries a hint
-    std::vector<uint32_t> sperm(shaped.size());
-    for (size_t i = 0; i < shaped.size(); ++i) sperm[i] = uint32_t(i);
-    if (kn.large_sort >= 1 && !shaped.empty()) {
-        bool hints = true;
-        for (uint32_t li : shaped) hints = hints && ops[li].order != 0;
-        if (hints)
-            std::stable_sort(sperm.begin(), sperm.end(), [&](uint32_t a, uint32_t b) {
-                return ops[shaped[a]].order < ops[shaped[b]].order;
-            });
-    }
-    for (const uint32_t k : sperm) {
-        const costa_tile_op_t& op = ops[shaped[k]];
-        const uint64_t i = ordered.size();
-        if (i > 0xFFFFFFFFull) throw error(COSTA_ERR_ARG, "costa: too many tiles in one list");
-        ordered.push_back(op);
-        const uint64_t n = uint64_t((op.nf + bfl - 1) / bfl) * uint64_t((op.ns + bsl - 1) / bsl);
-        if (n > 0xFFFFFFFFull) throw error(COSTA_ERR_ARG, "costa: tile too large");
-        for (uint64_t q = 0; q < n; ++q) work.push_back((i << 32) | q);
-    }
-    bool by_address = kn.large_sort == 2;
-    if (kn.large_sort == 3) {
-        by_address = E == 8 && !ordered.empty();
-        for (const auto& op : ordered) by_address = by_address && (op.flags & COSTA_TILE_TRANSPOSE);
-    }
-    if (by_address && work.size() > 1) {
-        // sub-tiles by the address of their first destination element (stable)
-        std::vector<std::pair<uint64_t, uint64_t>> key(work.size());
-        for (size_t x = 0; x < work.size(); ++x) {
-            const costa_tile_op_t& op = ordered[size_t(work[x] >> 32)];
-            const uint64_t q = work[x] & 0xFFFFFFFFull, nbf = uint64_t((op.nf + bfl - 1) / bfl);
-            const int64_t f0 = int64_t(q % nbf) * bfl, s0 = int64_t(q / nbf) * bsl;
-            const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
-            key[x] = {op.dst + uint64_t((tr ? f0 * op.ldd + s0 : s0 * op.ldd + f0) * E), uint64_t(x)};
+        const size_t op0 = ordered.size(), w0 = work.size();
+        for (const uint32_t k : sperm) {
+            const costa_tile_op_t& op = ops[sel[k]];
+            const uint64_t i = ordered.size();
+            if (i > 0xFFFFFFFFull) throw error(COSTA_ERR_ARG, "costa: too many tiles in one list");
+            ordered.push_back(op);
+            const uint64_t n = uint64_t((op.nf + bf - 1) / bf) * uint64_t((op.ns + bs - 1) / bs);
+            if (n > 0xFFFFFFFFull) throw error(COSTA_ERR_ARG, "costa: tile too large");
+            for (uint64_t q = 0; q < n; ++q) work.push_back((i << 32) | q);
         }
-        std::sort(key.begin(), key.end());
-        std::vector<uint64_t> w2(work.size());
-        for (size_t x = 0; x < work.size(); ++x) w2[x] = work[size_t(key[x].second)];
-        work.swap(w2);
+        bool by_address = kn.large_sort == 2;
+        if (kn.large_sort == 3) {
+            by_address = E == 8 && ordered.size() > op0;
+            for (size_t i = op0; i < ordered.size(); ++i)
+                by_address = by_address && (ordered[i].flags & COSTA_TILE_TRANSPOSE);
+        }
+        if (by_address && work.size() - w0 > 1) {
+            // sub-tiles by the address of their first destination element (stable)
+            std::vector<std::pair<uint64_t, uint64_t>> key(work.size() - w0);
+            for (size_t x = 0; x < key.size(); ++x) {
+                const uint64_t wx = work[w0 + x];
+                const costa_tile_op_t& op = ordered[size_t(wx >> 32)];
+                const uint64_t q = wx & 0xFFFFFFFFull, nbf = uint64_t((op.nf + bf - 1) / bf);
+                const int64_t f0 = int64_t(q % nbf) * bf, s0 = int64_t(q / nbf) * bs;
+                const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
+                key[x] = {op.dst + uint64_t((tr ? f0 * op.ldd + s0 : s0 * op.ldd + f0) * E), wx};
+            }
+            std::sort(key.begin(), key.end());
+            for (size_t x = 0; x < key.size(); ++x) work[w0 + x] = key[x].second;
+        }
+        n_work[c] = int64_t(work.size() - w0);
     }
     // ops are independent (disjoint destinations), so any order is valid; neighbours in
     // memory run at the same time and share the partially used cache lines at their edges.
@@ -581,7 +603,8 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         at_piece[i + 1] = at_piece[i] + size_t(grid[i].nfc * grid[i].nsc);
     work_split w;
     w.tr_shape = tr_shape;
-    w.n_large = int64_t(work.size());
+    w.n_large = n_work[0];
+    w.n_medium = n_work[1];
     w.tiny_first = int64_t(ordered.size());
     w.n_tiny = int64_t(at_piece[nw]);
     const size_t base = ordered.size();
@@ -600,6 +623,7 @@ launch_args make_launch(const work_split& w, const void* d_ordered, const void* 
     a.ops = static_cast<const costa_tile_op_t*>(d_ordered);
     a.work = static_cast<const uint64_t*>(d_work);
     a.n_large = w.n_large;
+    a.n_medium = w.n_medium;
     a.tiny_first = w.tiny_first;
     a.n_tiny = w.n_tiny;
     a.src_base = src_base;

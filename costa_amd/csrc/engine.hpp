@@ -179,6 +179,7 @@ struct launch_args {
     const costa_tile_op_t* ops;  // device, in build_work order: [sub-tiled ops | tiny ops]
     const uint64_t* work;   // per sub-tile: (op index << 32) | sub-tile index
     int64_t n_large;        // work items using the large sub-tile shape
+    int64_t n_medium;       // then work[n_large, n_large + n_medium): the medium shape
     int64_t tiny_first;     // ops[tiny_first, tiny_first + n_tiny) run one per wavefront
     int64_t n_tiny;
     const char* src_base;
@@ -191,17 +192,20 @@ struct launch_args {
 bool any_transpose(const std::vector<costa_tile_op_t>& ops);
 bool any_axpby(const std::vector<costa_tile_op_t>& ops);
 void launch_tiles(costa_dtype_t dtype, const launch_args& a, void* stream /* hipStream_t */);
-// sub-tile shape (elements along the source's fast dim, along its slow dim) of a copy-only list
-// or of a list with transposing ops
-void tile_shapes(costa_dtype_t dtype, bool transposing_list, int* bf_large, int* bs_large);
+// sub-tile shapes (elements along the source's fast dim, along its slow dim) of a copy-only list
+// or of a list with transposing ops: the large shape, and the medium one (bf_m = bs_m = 0: none)
+struct shape_dims {
+    int bf = 0, bs = 0, bf_m = 0, bs_m = 0;
+};
+void tile_shapes(costa_dtype_t dtype, bool transposing_list, shape_dims* out);
 // Execution order of an op list: `ordered` = [sub-tiled ops | tiny ops] (tiny ops sorted by the
 // planner's locality hint, so wavefronts running at the same time share partially used cache
 // lines),
 // `work` = [large-shape sub-tiles | small-shape sub-tiles], indices into `ordered`.
 struct work_split {
-    int64_t n_large = 0, tiny_first = 0, n_tiny = 0;
+    int64_t n_large = 0, n_medium = 0, tiny_first = 0, n_tiny = 0;
     bool tr_shape = false;  // sub-tiles cut with tile_shapes(dtype, true, ...)
-    int64_t n_items() const { return n_large + n_tiny; }
+    int64_t n_items() const { return n_large + n_medium + n_tiny; }
 };
 work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops,
                       std::vector<costa_tile_op_t>& ordered, std::vector<uint64_t>& work);

@@ -291,26 +291,43 @@ struct shape {
 #define COSTA_LARGE_D_BF 64
 #define COSTA_LARGE_D_BS 128
 #endif
+// `medium_tr`: 256 threads, 16 KiB sub-tiles, for aligned transposing ops of at least half of
+// one that are below half a large sub-tile (before: cut into wavefront pieces of ~128-byte
+// runs): fp32 64^2 blocks 3.60 -> 4.77 TB/s, 96^2 4.18 -> 4.60; fp64 32^2 4.27 -> 4.97, 48^2
+// 4.27 -> 5.26 (profiles/r2/shapes/medium.log).  None for c64 / c128 (has_medium).
+#ifndef COSTA_MEDIUM  // 0: no medium tier (tuning builds only)
+#define COSTA_MEDIUM 1
+#endif
 template <typename T> struct shapes;
 template <> struct shapes<float> {
     using large = shape<float, 1024, 256, 128>;
     using large_tr = shape<float, COSTA_LARGE_F_NT, COSTA_LARGE_F_BF, COSTA_LARGE_F_BS>;
+    using medium_tr = shape<float, 256, 64, 64>;
+    static constexpr bool has_medium = COSTA_MEDIUM;
 };
 template <> struct shapes<int> {
     using large = shape<int, 1024, 256, 128>;
     using large_tr = shape<int, COSTA_LARGE_F_NT, COSTA_LARGE_F_BF, COSTA_LARGE_F_BS>;
+    using medium_tr = shape<int, 256, 64, 64>;
+    static constexpr bool has_medium = COSTA_MEDIUM;
 };
 template <> struct shapes<double> {
     using large = shape<double, 1024, 128, 128>;
     using large_tr = shape<double, COSTA_LARGE_D_NT, COSTA_LARGE_D_BF, COSTA_LARGE_D_BS>;
+    using medium_tr = shape<double, 256, 32, 64>;
+    static constexpr bool has_medium = COSTA_MEDIUM;
 };
 template <> struct shapes<cpx<float>> {
     using large = shape<cpx<float>, 1024, 128, 128>;
     using large_tr = large;
+    using medium_tr = large;
+    static constexpr bool has_medium = false;
 };
 template <> struct shapes<cpx<double>> {
     using large = shape<cpx<double>, 1024, 64, 128>;
     using large_tr = large;
+    using medium_tr = large;
+    static constexpr bool has_medium = false;
 };
 
 // One sub-tile.  FULL: the sub-tile is a whole BF x BS block with 16-byte aligned rows on
@@ -703,13 +720,20 @@ void launch_t(const launch_args& a, hipStream_t stream) {
         launch_shape<T, typename shapes<T>::large_tr>(a, a.work, a.n_large, stream);
     else
         launch_shape<T, typename shapes<T>::large>(a, a.work, a.n_large, stream);
+    if (a.n_medium > 0) {
+        if (!shapes<T>::has_medium || !a.tr_shape) throw error(COSTA_ERR_INTERNAL, "costa: medium shape");
+        launch_shape<T, typename shapes<T>::medium_tr>(a, a.work + a.n_large, a.n_medium, stream);
+    }
     launch_tiny<T>(a, stream);
 }
 
 template <typename T>
-void shape_of(bool tr, int* bf_l, int* bs_l) {
-    *bf_l = tr ? shapes<T>::large_tr::BF : shapes<T>::large::BF;
-    *bs_l = tr ? shapes<T>::large_tr::BS : shapes<T>::large::BS;
+void shape_of(bool tr, shape_dims* d) {
+    d->bf = tr ? shapes<T>::large_tr::BF : shapes<T>::large::BF;
+    d->bs = tr ? shapes<T>::large_tr::BS : shapes<T>::large::BS;
+    const bool med = tr && shapes<T>::has_medium;
+    d->bf_m = med ? shapes<T>::medium_tr::BF : 0;
+    d->bs_m = med ? shapes<T>::medium_tr::BS : 0;
 }
 
 template <typename T, typename S>
@@ -722,24 +746,25 @@ template <typename T>
 void set_lds_limits() {
     set_lds_limit<T, typename shapes<T>::large>();
     set_lds_limit<T, typename shapes<T>::large_tr>();
+    set_lds_limit<T, typename shapes<T>::medium_tr>();
 }
 
 }  // namespace
 
-void tile_shapes(costa_dtype_t dtype, bool transposing_list, int* bf_large, int* bs_large) {
+void tile_shapes(costa_dtype_t dtype, bool transposing_list, shape_dims* d) {
     const bool t = transposing_list;
     switch (dtype) {
-    case COSTA_FLOAT: shape_of<float>(t, bf_large, bs_large); return;
-    case COSTA_DOUBLE: shape_of<double>(t, bf_large, bs_large); return;
-    case COSTA_CFLOAT: shape_of<cpx<float>>(t, bf_large, bs_large); return;
-    case COSTA_CDOUBLE: shape_of<cpx<double>>(t, bf_large, bs_large); return;
-    case COSTA_INT32: shape_of<int>(t, bf_large, bs_large); return;
+    case COSTA_FLOAT: shape_of<float>(t, d); return;
+    case COSTA_DOUBLE: shape_of<double>(t, d); return;
+    case COSTA_CFLOAT: shape_of<cpx<float>>(t, d); return;
+    case COSTA_CDOUBLE: shape_of<cpx<double>>(t, d); return;
+    case COSTA_INT32: shape_of<int>(t, d); return;
     }
     throw error(COSTA_ERR_ARG, "unknown dtype");
 }
 
 void launch_tiles(costa_dtype_t dtype, const launch_args& a, void* stream) {
-    if (a.n_large + a.n_tiny <= 0) return;
+    if (a.n_large + a.n_medium + a.n_tiny <= 0) return;
     static bool once = [] {
         set_lds_limits<float>();
         set_lds_limits<double>();

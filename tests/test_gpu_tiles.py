@@ -1,6 +1,6 @@
 """GPU parity of one batched tile launch against the oracle, on random op lists that mix every
-work class of the executor: tiny ops (one wavefront each, copy and LDS transpose), small and
-large sub-tile shapes, the class boundaries (engine.cpp tiny_copy_budget / kTinyLdsBytes), thin
+work class of the executor: tiny ops (one wavefront each, copy and LDS transpose), the medium
+and large sub-tile shapes (copy and transposing lists), the class boundaries (engine.cpp tiny_copy_budget / kTinyLdsBytes), thin
 ops (nf = 1, ns = 1), padded strides, unaligned offsets, and every scale kind.
 
 Each op is the reference's copy_and_transform (memory_utils.hpp:339-412); the oracle executes
@@ -43,7 +43,7 @@ def _values(rng, dt, n):
 
 def _shape(rng, E, transpose):
     """(nf, ns) drawn to hit every class and the boundaries between them"""
-    pick = rng.integers(0, 7)
+    pick = rng.integers(0, 8)
     if pick == 0:  # tiny, ragged
         return int(rng.integers(1, 70)), int(rng.integers(1, 70))
     if pick == 1:  # at the tiny boundary
@@ -59,6 +59,8 @@ def _shape(rng, E, transpose):
         return int(rng.integers(60, 200)), int(rng.integers(40, 140))
     if pick == 5:  # large shape, ragged edge
         return int(rng.integers(200, 600)), int(rng.integers(100, 300))
+    if pick == 6:  # around the medium shape (256 threads, 16 KiB sub-tiles) of transposing lists
+        return int(rng.integers(16, 100)), int(rng.integers(16, 100))
     return int(rng.integers(1, 400)), int(rng.integers(1, 400))
 
 
@@ -127,4 +129,46 @@ def test_mixed_tile_list(gpu, code, seed):
     E = np.dtype(dt).itemsize
     bad = np.flatnonzero((got.view(np.uint8).reshape(n_dst, E)
                           != exp.view(np.uint8).reshape(n_dst, E)).any(1))
+    assert bad.size == 0, f"{bad.size} elements differ, first at {bad[0]}: {got[bad[0]]} vs {exp[bad[0]]}"
+
+
+@pytest.mark.parametrize("code,nb", [(0, 64), (1, 32), (1, 48), (4, 64), (0, 80)],
+                         ids=["f32-64", "f64-32", "f64-48", "i32-64", "f32-80"])
+def test_medium_shape_list(gpu, code, nb):
+    """a transposing list of >= 4096 aligned ops between half a medium and half a large
+    sub-tile (engine.cpp kMinMediumOps: the medium shape only runs for lists this long), with
+    every scale kind and padded strides; bit-exact against the oracle"""
+    rng = np.random.default_rng(77 + code + nb)
+    dt = oracle.NP[code]
+    E = np.dtype(dt).itemsize
+    n_ops = 4200
+    ops = np.zeros(n_ops, costa_amd.TILE_OP_DTYPE)
+    src_off = dst_off = 0
+    for i in range(n_ops):
+        # full, or (above 32) one 16-byte vector short: every op stays in the medium class
+        nf = nb - (int(rng.integers(0, 2)) * (16 // E) if nb > 32 else 0)
+        ns = nb
+        lds = nf + int(rng.integers(0, 2)) * (16 // E)
+        ldd = ns + int(rng.integers(0, 2)) * (16 // E)
+        kind = int(rng.integers(1, 4))
+        slot = (0, 1, 2, 3)[kind] if kind != 2 else int(rng.choice([0, 2]))
+        ops[i] = (src_off * E, dst_off * E, nf, ns, lds, ldd, 1 | 4 | 8 | (kind << 4) | (slot << 16), 0)
+        src_off += -(-((ns - 1) * lds + nf) * E // 16) * 16 // E
+        dst_off += -(-((nf - 1) * ldd + ns) * E // 16) * 16 // E
+    src = _values(rng, dt, src_off)
+    dst0 = _values(rng, dt, dst_off)
+    if dt == np.int32:
+        scal = np.array([1, 0, 0, 0, 2, 0, -3, 5], dt)
+    else:
+        a, b = _values(rng, dt, 2)
+        scal = np.array([1, 0, 0, 0, a, 0, a, b], dt)
+    exp = dst0.copy()
+    oracle.exec_tile_ops(code, ops, scal, src.ctypes.data, exp.ctypes.data)
+    d_src = torch.from_numpy(src.view(np.uint8).copy()).cuda()
+    d_dst = torch.from_numpy(dst0.view(np.uint8).copy()).cuda()
+    gpu.execute_tiles(code, ops, scal, d_src.data_ptr(), d_dst.data_ptr())
+    torch.cuda.synchronize()
+    got = d_dst.cpu().numpy().view(dt)
+    bad = np.flatnonzero((got.view(np.uint8).reshape(dst_off, E)
+                          != exp.view(np.uint8).reshape(dst_off, E)).any(1))
     assert bad.size == 0, f"{bad.size} elements differ, first at {bad[0]}: {got[bad[0]]} vs {exp[bad[0]]}"

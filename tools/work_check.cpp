@@ -1,7 +1,8 @@
 // Invariants of the work lists (engine.cpp build_work), without a GPU (block addresses are never
 // touched).  Run by tests/test_work_lists.py.
 //   cfg 5 'N' (copy list) and 'T' (transposing list) on BASELINE cfg 5's geometry:
-//     * no op takes the large shape (every cfg 5 tile is below the large threshold);
+//     * the ops that take a sub-tiled shape are the ones the classification rules name (the
+//       'T' list's aligned ops of at least half a medium sub-tile);
 //     * every piece fits the wavefront budget the library uses (tiny_copy_budget,
 //       tiny_lds_budget; staged pitch nf | 1);
 //     * the pieces of every op (found by its unique locality hint) lie inside it and add up to it;
@@ -57,7 +58,29 @@ static grid_layout<float> layout(const std::vector<int>& rs, const std::vector<i
         }                                              \
     } while (0)
 
-// `ops` must carry unique, non-zero hints; expect_large: ops that must stay on the large shape
+// the shaped ops (large or medium sub-tiles) the classification rules give: aligned ops of at
+// least half a large sub-tile, unaligned ones above kUnalignedWaveCap sub-tiles, and in lists
+// that transpose, aligned transposing ops of at least half a medium sub-tile
+static int64_t expected_shaped(costa_dtype_t dt, const std::vector<costa_tile_op_t>& ops) {
+    bool tr = false;
+    for (const auto& o : ops) tr = tr || (o.flags & COSTA_TILE_TRANSPOSE);
+    shape_dims sh;
+    tile_shapes(dt, tr, &sh);
+    const int64_t E = int64_t(dtype_size(dt)), big = int64_t(sh.bf) * sh.bs, med = int64_t(sh.bf_m) * sh.bs_m;
+    const uint32_t both = COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST;
+    int64_t n_large = 0, n_med = 0;
+    for (const auto& o : ops) {
+        const int64_t e = int64_t(o.nf) * o.ns;
+        const bool al = (o.flags & both) == both, t = o.flags & COSTA_TILE_TRANSPOSE;
+        const bool tiny = (t ? int64_t(o.nf | 1) * o.ns * E <= tiny_lds_budget() : e * E <= tiny_copy_budget(E));
+        const bool large = 2 * e >= big && (al || e > kUnalignedWaveCap * big) && !tiny;
+        n_large += large;
+        n_med += !large && med > 0 && al && t && 2 * e >= med;
+    }
+    return n_large + (n_med >= 4096 ? n_med : 0);  // engine.cpp kMinMediumOps
+}
+
+// `ops` must carry unique, non-zero hints; expect_large: ops that must go to a sub-tiled shape
 static bool check_list(const std::string& name, costa_dtype_t dt, const std::vector<costa_tile_op_t>& ops,
                        int64_t expect_large_ops) {
     const int64_t E = int64_t(dtype_size(dt));
@@ -73,10 +96,12 @@ static bool check_list(const std::string& name, costa_dtype_t dt, const std::vec
     std::map<uint32_t, const costa_tile_op_t*> parent;
     for (const auto& o : ops) CHECK(o.order > 0 && parent.emplace(o.order, &o).second, "hint %u not unique", o.order);
     std::map<uint32_t, int64_t> area;
-    for (int64_t i = 0; i < w.tiny_first; ++i) {  // large-shape ops: whole, in hint order
+    int restarts = 0;  // the large ops, then the medium ones: each run whole, in hint order
+    for (int64_t i = 0; i < w.tiny_first; ++i) {
         const costa_tile_op_t& s = ord[size_t(i)];
-        CHECK(parent.count(s.order) && std::memcmp(&s, parent[s.order], sizeof(s)) == 0, "large op %lld", (long long)i);
-        CHECK(i == 0 || ord[size_t(i) - 1].order < s.order, "large op %lld out of hint order", (long long)i);
+        CHECK(parent.count(s.order) && std::memcmp(&s, parent[s.order], sizeof(s)) == 0, "shaped op %lld", (long long)i);
+        restarts += i > 0 && ord[size_t(i) - 1].order > s.order;
+        CHECK(restarts <= 1, "shaped op %lld out of hint order", (long long)i);
         area[s.order] += int64_t(s.nf) * s.ns;
     }
     bool tr_list = false;
@@ -127,11 +152,13 @@ int main() {
     elayout a = erase(LA), c = erase(LC);
     for (char op : {'N', 'T'}) {
         auto p = plan_of(a, c, op, op == 'N' ? 1.f : -0.5f, op == 'N' ? 0.f : 2.f);
-        if (!check_list(std::string("cfg5 ") + op, p->dtype, p->local_ops, 0)) return 1;
+        const int64_t shaped = expected_shaped(p->dtype, p->local_ops);
+        if (!check_list(std::string("cfg5 ") + op, p->dtype, p->local_ops, shaped)) return 1;
         // one exchange round's share of a list: every 8th op (hints sparse)
         std::vector<costa_tile_op_t> sub;
         for (size_t i = 0; i < p->local_ops.size(); i += 8) sub.push_back(p->local_ops[i]);
-        if (!check_list(std::string("cfg5 sub-list ") + op, p->dtype, sub, 0)) return 1;
+        if (!check_list(std::string("cfg5 sub-list ") + op, p->dtype, sub, expected_shaped(p->dtype, sub)))
+            return 1;
     }
     // unaligned large ops: fp32 4096^2 'T' with lld = 4097 (columns 4-byte aligned only)
     for (int nb : {256, 1024}) {
@@ -142,9 +169,9 @@ int main() {
                                             reinterpret_cast<float*>(uint64_t(1) << 41), lld, 'C', 0);
         elayout ea = erase(A), ec = erase(C);
         auto p = plan_of(ea, ec, 'T', 1.f, 0.f);
-        int bf = 0, bs = 0;
-        tile_shapes(COSTA_FLOAT, true, &bf, &bs);  // a transposing list
-        const int64_t elems = int64_t(nb) * nb, sub_elems = int64_t(bf) * bs;
+        shape_dims sh;
+        tile_shapes(COSTA_FLOAT, true, &sh);  // a transposing list
+        const int64_t elems = int64_t(nb) * nb, sub_elems = int64_t(sh.bf) * sh.bs;
         const int64_t expect = elems > kUnalignedWaveCap * sub_elems ? int64_t(p->local_ops.size()) : 0;
         if (!check_list("unaligned " + std::to_string(nb) + "^2 blocks", p->dtype, p->local_ops, expect))
             return 1;
