@@ -33,6 +33,28 @@ for rel in ["prof/trace_kernel_stats.csv", "bench.log", "pytest_gpu.log", "smoke
         shutil.copy(p, os.path.join(dst, name))
 
 
+def dispatch_summary():
+    """per kernel and grid size: dispatch count, mean and median duration (ns), from each
+    kernel trace of the session (a kernel's rocprofv3 stats average mixes every launch size of
+    it; the workload's own launches are the largest grid)"""
+    out = {}
+    for sub in ("prof", "c5N_prof", "c5T_prof"):
+        p = os.path.join(src, sub, "trace_kernel_trace.csv")
+        if not os.path.exists(p):
+            continue
+        by = {}
+        for r in csv.DictReader(open(p)):
+            if "costa" not in r["Kernel_Name"]:
+                continue
+            k = (r["Kernel_Name"], int(r["Grid_Size_X"]), int(r["Workgroup_Size_X"]))
+            by.setdefault(k, []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        out[sub] = [{"kernel": k[0], "grid": k[1], "workgroup": k[2], "dispatches": len(v),
+                     "mean_ns": round(statistics.mean(v), 1), "median_ns": statistics.median(v)}
+                    for k, v in sorted(by.items(), key=lambda kv: -sum(kv[1]))]
+    if out:
+        json.dump(out, open(os.path.join(dst, "kernel_dispatches.json"), "w"), indent=1)
+
+
 def bench_line(path):
     try:
         return json.loads([l for l in open(path) if l.startswith("{")][-1])
@@ -78,6 +100,7 @@ def derive(prefix, dtype, out_name):
     print(out_name, json.dumps({k: v for k, v in out.items() if not k.startswith("kernels")}))
 
 
+dispatch_summary()
 derive("", "double", "pmc_tile_kernel.json")
 derive("c5N_", "float", "pmc_cfg5_N.json")
 derive("c5T_", "float", "pmc_cfg5_T.json")
