@@ -658,8 +658,13 @@ __device__ __forceinline__ void tiny_op(const costa_tile_op_t& op, int lane, T* 
 // locality-ordered list, and neighbouring ops (which share partially written cache lines) meet
 // in one L2 (r11: cfg 5 'N' 3.77 against 3.58 TB/s, 'T' 3.07 against 3.00;
 // profiles/r11/c5_order.log).  Placement only changes speed, never results.
+// Real types: 8 wavefronts per SIMD.  The transposing, beta-reading variant needed 66 VGPRs,
+// one over the 8-wave budget, so 7 fitted (cfg 5 'T' 0.790 -> 0.774 ms with the bound, no
+// spills; profiles/r2/w8ab/).  Complex types would spill under it (tests/test_kernel_resources.py).
+template <typename T> struct tiny_min_waves { static constexpr int value = 8; };
+template <typename R> struct tiny_min_waves<cpx<R>> { static constexpr int value = 1; };
 template <typename T, int W, int UB, bool TR, bool AX, int UC>
-__global__ __launch_bounds__(64 * W) void tiny_kernel(const costa_tile_op_t* __restrict__ ops,
+__global__ __launch_bounds__(64 * W, tiny_min_waves<T>::value) void tiny_kernel(const costa_tile_op_t* __restrict__ ops,
                                                       int64_t n_ops, const char* src_base,
                                                       char* dst_base, const T* __restrict__ scalars,
                                                       int lds_per_wave) {
