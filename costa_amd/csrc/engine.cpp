@@ -422,11 +422,13 @@ struct wave_knobs {  // defaults, overridable for tuning runs
                          // TB/s, "segcamp" 4.4-4.9 against 6.4); 2: 1, then the sub-tiles by
                          // the address of their first destination element (one sub-tile-wide
                          // band of target columns at a time, instead of an op's 2-4 sub-tiles
-                         // side by side); 3 (default): 2 for lists whose large ops all transpose
-                         // 8-byte elements (fp64 / c64 'T' 16384^2: 0.710 against 0.747 ms with
-                         // 256^2 blocks, 0.709 against 0.797 with 512^2), else 1 (c128 with 128^2
-                         // blocks: 2.87 against 2.27 ms; fp32 even; copy lists untested under 2;
-                         // tools/order_run.sh, profiles/r2/order/)
+                         // side by side); 3 (default): 2 for lists whose shaped ops all transpose
+                         // 4- or 8-byte elements (fp64 / c64 'T' 16384^2: 0.710 against 0.747 ms
+                         // with 256^2 blocks, 0.709 against 0.797 with 512^2; fp32 with its
+                         // 128 x 128 sub-tiles 0.366 against 0.396 with 256^2, 0.366 against
+                         // 0.454 with 512^2), else 1 (c128 with 128^2 blocks: 2.87 against 2.27
+                         // ms; copy lists untested under 2; tools/order_run.sh,
+                         // tools/f32_order_run.sh, profiles/r2/order/)
     int sort = 4;    // COSTA_TINY_SORT 0: list order, 1: by source, 2: by destination address,
                      // 3: by the planner's locality hint (costa_tile_op_t::order), 4: 3 for
                      // copy-only lists, 2 for lists that transpose (cfg 5 'T' 3.88 against
@@ -514,7 +516,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         }
         bool by_address = kn.large_sort == 2;
         if (kn.large_sort == 3) {
-            by_address = E == 8 && ordered.size() > op0;
+            by_address = (E == 4 || E == 8) && ordered.size() > op0;
             for (size_t i = op0; i < ordered.size(); ++i)
                 by_address = by_address && (ordered[i].flags & COSTA_TILE_TRANSPOSE);
         }
