@@ -27,7 +27,7 @@ step() {  # step <name> <seconds> <cmd...>
 rocm-smi --showproductname > "$OUT/gpu.txt" 2>&1 || true
 nproc > "$OUT/nproc.txt"; lscpu | grep -E "Model name|^CPU\(s\)" >> "$OUT/nproc.txt"
 step smoke 400 python3 -c "import __graft_entry__ as g; g.smoke()"
-step pytest_gpu 900 python3 -m pytest tests -m gpu -q --maxfail=20
+step pytest_gpu 900 python3 -u -m pytest tests -m gpu -q --maxfail=20 --timeout 120 --timeout-method thread
 step bench 600 python3 bench.py --steps 20 --warmup 3
 step rocprof_trace 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o trace --output-format csv \
     -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-e2e
