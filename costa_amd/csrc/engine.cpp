@@ -429,10 +429,17 @@ struct wave_knobs {  // defaults, overridable for tuning runs
                          // 0.454 with 512^2), else 1 (c128 with 128^2 blocks: 2.87 against 2.27
                          // ms; copy lists untested under 2; tools/order_run.sh,
                          // tools/f32_order_run.sh, profiles/r2/order/)
-    int sort = 4;    // COSTA_TINY_SORT 0: list order, 1: by source, 2: by destination address,
+    int sort = 5;    // COSTA_TINY_SORT 0: list order, 1: by source, 2: by destination address,
                      // 3: by the planner's locality hint (costa_tile_op_t::order), 4: 3 for
                      // copy-only lists, 2 for lists that transpose (cfg 5 'T' 3.88 against
-                     // 3.79 TB/s, 'N' equal; profiles/r11/c5_env.log), else as 2
+                     // 3.79 TB/s, 'N' equal; profiles/r11/c5_env.log), else as 2; 5 (default):
+                     // pack lists by source address (their destinations, the dense package,
+                     // are contiguous per op in any order), every other list by destination
+                     // address.  cfg 5 under 5 against 4 on one lease (tools/c5_sort_probe.py,
+                     // profiles/r2c/c5_sort.log): local 'N' 0.497 / 0.499-0.502 ms, 'T' equal;
+                     // with every tile through the exchange (COSTA_LOOPBACK=1) 'N' pack 0.557-0.561
+                     // / 0.596-0.600, unpack 0.556-0.558 / 0.606-0.610, 'T' pack 0.725-0.729 /
+                     // 0.751-0.761, unpack equal
 };
 const wave_knobs& knobs() {
     static wave_knobs k = [] {
@@ -447,7 +454,8 @@ const wave_knobs& knobs() {
 }  // namespace
 
 work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops,
-                      std::vector<costa_tile_op_t>& ordered, std::vector<uint64_t>& work) {
+                      std::vector<costa_tile_op_t>& ordered, std::vector<uint64_t>& work,
+                      bool pack_list) {
     const bool tr_shape = any_transpose(ops);
     shape_dims sh;
     tile_shapes(dtype, tr_shape, &sh);
@@ -547,7 +555,9 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         top = std::max(top, o->order);
         tr = tr || (o->flags & COSTA_TILE_TRANSPOSE);
     }
-    const int mode = kn.sort == 4 ? (tr || top == 0 ? 2 : 3) : kn.sort == 3 && top == 0 ? 2 : kn.sort;
+    const int mode = kn.sort == 5   ? (pack_list ? 1 : 2)
+                     : kn.sort == 4 ? (tr || top == 0 ? 2 : 3)
+                     : kn.sort == 3 && top == 0 ? 2 : kn.sort;
     std::vector<uint32_t> perm(nw);
     if (mode == 3 && size_t(top) <= 4 * nw + 1024) {
         // the planner's hints are ranks within the list: a stable counting sort
@@ -1087,7 +1097,7 @@ cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
         auto x = std::make_unique<cached_plan::xround>();
         x->tr_unpack = any_transpose(up[size_t(r)]);
         x->ax_unpack = any_axpby(up[size_t(r)]);
-        x->l_pack = build_work(p.dtype, pk[size_t(r)], ord_p[size_t(r)], w_p[size_t(r)]);
+        x->l_pack = build_work(p.dtype, pk[size_t(r)], ord_p[size_t(r)], w_p[size_t(r)], true);
         x->l_unpack = build_work(p.dtype, up[size_t(r)], ord_u[size_t(r)], w_u[size_t(r)]);
         cp->rounds.push_back(std::move(x));
     }

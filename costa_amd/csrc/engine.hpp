@@ -207,8 +207,11 @@ struct work_split {
     bool tr_shape = false;  // sub-tiles cut with tile_shapes(dtype, true, ...)
     int64_t n_items() const { return n_large + n_medium + n_tiny; }
 };
+// pack_list: the ops write the dense send package (their destinations are contiguous whatever
+// their order), which changes the wavefront ops' order (wave_knobs::sort)
 work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops,
-                      std::vector<costa_tile_op_t>& ordered, std::vector<uint64_t>& work);
+                      std::vector<costa_tile_op_t>& ordered, std::vector<uint64_t>& work,
+                      bool pack_list = false);
 // launch arguments of one ordered op list
 launch_args make_launch(const work_split& w, const void* d_ordered, const void* d_work,
                         const char* src_base, char* dst_base, const void* d_scalars, bool transpose,

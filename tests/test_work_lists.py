@@ -1,8 +1,8 @@
 """Work lists (engine.cpp build_work) on the CPU: BASELINE cfg 5's geometry ('N' copy list, 'T'
 transposing list, and a sparse sub-list like one exchange round's), and unaligned large ops
 (fp32, lld % 4 != 0) below and above the wavefront cap.  Every piece within the budget the
-library uses, the pieces of each op inside it and adding up to it, copy lists in locality-hint
-order, transposing lists in destination order, large-shape ops whole and in hint order, two
+library uses, the pieces of each op inside it and adding up to it, in destination-address
+order, large-shape ops whole and in hint order, two
 builds identical (the cut runs on several host threads).  The checks live in
 tools/work_check.cpp, built here with g++ against the in-tree libcosta_amd.so; block addresses
 are never dereferenced."""

@@ -6,7 +6,8 @@
 //     * every piece fits the wavefront budget the library uses (tiny_copy_budget,
 //       tiny_lds_budget; staged pitch nf | 1);
 //     * the pieces of every op (found by its unique locality hint) lie inside it and add up to it;
-//     * order: copy lists by hint, transposing lists by the op's destination address;
+//     * order: by the op's destination address (copy and transposing lists alike), pack lists
+//       by the op's source address;
 //     * two builds give byte-identical lists (the threaded cut is deterministic).
 //   a sub-list of every 8th cfg 5 op (what one exchange round's pack / unpack list looks like:
 //     hints sparse in the list, so the comparison sort replaces the counting sort): the same.
@@ -82,12 +83,12 @@ static int64_t expected_shaped(costa_dtype_t dt, const std::vector<costa_tile_op
 
 // `ops` must carry unique, non-zero hints; expect_large: ops that must go to a sub-tiled shape
 static bool check_list(const std::string& name, costa_dtype_t dt, const std::vector<costa_tile_op_t>& ops,
-                       int64_t expect_large_ops) {
+                       int64_t expect_large_ops, bool pack = false) {
     const int64_t E = int64_t(dtype_size(dt));
     std::vector<costa_tile_op_t> ord, ord2;
     std::vector<uint64_t> work, work2;
-    const work_split w = build_work(dt, ops, ord, work);
-    build_work(dt, ops, ord2, work2);
+    const work_split w = build_work(dt, ops, ord, work, pack);
+    build_work(dt, ops, ord2, work2, pack);
     CHECK(w.tiny_first == expect_large_ops, "%lld ops on the large shape, expected %lld",
           (long long)w.tiny_first, (long long)expect_large_ops);
     CHECK(ord.size() == ord2.size() && work == work2 &&
@@ -104,9 +105,6 @@ static bool check_list(const std::string& name, costa_dtype_t dt, const std::vec
         CHECK(restarts <= 1, "shaped op %lld out of hint order", (long long)i);
         area[s.order] += int64_t(s.nf) * s.ns;
     }
-    bool tr_list = false;
-    for (int64_t i = w.tiny_first; i < w.tiny_first + w.n_tiny; ++i)
-        tr_list = tr_list || (ord[size_t(i)].flags & COSTA_TILE_TRANSPOSE);
     uint64_t last_key = 0;
     for (int64_t i = w.tiny_first; i < w.tiny_first + w.n_tiny; ++i) {
         const costa_tile_op_t& s = ord[size_t(i)];
@@ -123,7 +121,7 @@ static bool check_list(const std::string& name, costa_dtype_t dt, const std::vec
         const uint64_t dst = q.dst + uint64_t((tr ? f0 * q.ldd + s0 : s0 * q.ldd + f0) * E);
         CHECK(s.dst == dst, "piece %lld destination", (long long)i);
         area[s.order] += int64_t(s.nf) * s.ns;
-        const uint64_t key = tr_list ? q.dst : uint64_t(q.order);
+        const uint64_t key = pack ? q.src : q.dst;  // wave_knobs::sort 5
         CHECK(key >= last_key, "piece %lld out of order", (long long)i);
         last_key = key;
     }
@@ -158,6 +156,9 @@ int main() {
         std::vector<costa_tile_op_t> sub;
         for (size_t i = 0; i < p->local_ops.size(); i += 8) sub.push_back(p->local_ops[i]);
         if (!check_list(std::string("cfg5 sub-list ") + op, p->dtype, sub, expected_shaped(p->dtype, sub)))
+            return 1;
+        // the same as a pack list (wavefront ops by source address)
+        if (!check_list(std::string("cfg5 pack sub-list ") + op, p->dtype, sub, expected_shaped(p->dtype, sub), true))
             return 1;
     }
     // unaligned large ops: fp32 4096^2 'T' with lld = 4097 (columns 4-byte aligned only)
