@@ -172,3 +172,60 @@ def test_medium_shape_list(gpu, code, nb):
     bad = np.flatnonzero((got.view(np.uint8).reshape(dst_off, E)
                           != exp.view(np.uint8).reshape(dst_off, E)).any(1))
     assert bad.size == 0, f"{bad.size} elements differ, first at {bad[0]}: {got[bad[0]]} vs {exp[bad[0]]}"
+
+
+@pytest.mark.parametrize("code", [0, 1, 2, 3, 4], ids=["f32", "f64", "c64", "c128", "i32"])
+@pytest.mark.parametrize("copy_only", [False, True], ids=["mixed", "copy"])
+def test_unaligned_large_list(gpu, code, copy_only):
+    """large ops whose columns are not 16-byte aligned on one side or both (odd lld for 8-byte
+    types, lld % 4 != 0 for 4-byte ones): the large shape's element-wise path
+    (tile_kernels.hip run_tile_elem), full and ragged sub-tiles, every scale kind; bit-exact
+    against the oracle"""
+    rng = np.random.default_rng(4242 + code + 10 * copy_only)
+    dt = oracle.NP[code]
+    E = np.dtype(dt).itemsize
+    cplx = np.issubdtype(dt, np.complexfloating)
+    n_ops = 40
+    ops = np.zeros(n_ops, costa_amd.TILE_OP_DTYPE)
+    src_off = dst_off = 0
+    for i in range(n_ops):
+        tr = bool(rng.integers(0, 2)) and not copy_only
+        nf, ns = int(rng.integers(100, 420)), int(rng.integers(100, 300))
+        side = int(rng.integers(0, 3))  # 0: source unaligned, 1: destination, 2: both
+        lds = nf + (int(rng.integers(0, 3)) * 2 + 1 if side != 1 else 16 // E)
+        dn, d_slow = (ns, nf) if tr else (nf, ns)
+        ldd = dn + (int(rng.integers(0, 3)) * 2 + 1 if side != 0 else 16 // E)
+        src_off = -(-src_off * E // 16) * 16 // E + (int(rng.integers(0, 2)) if side != 1 else 0)
+        dst_off = -(-dst_off * E // 16) * 16 // E + (int(rng.integers(0, 2)) if side != 0 else 0)
+        conj = bool(cplx and rng.integers(0, 2))
+        kind = int(rng.integers(0, 4))
+        if kind == 0 and (tr or conj):
+            kind = 2
+            slot = 0
+        else:
+            slot = (0, 1, 2, 3)[kind] if kind != 2 else int(rng.choice([0, 2]))
+        flags = (1 if tr else 0) | (2 if conj else 0) | (kind << 4) | (slot << 16)
+        if (src_off * E) % 16 == 0 and (lds * E) % 16 == 0:
+            flags |= 4
+        if (dst_off * E) % 16 == 0 and (ldd * E) % 16 == 0:
+            flags |= 8
+        ops[i] = (src_off * E, dst_off * E, nf, ns, lds, ldd, flags, 0)
+        src_off += (ns - 1) * lds + nf
+        dst_off += (d_slow - 1) * ldd + dn
+    src = _values(rng, dt, src_off)
+    dst0 = _values(rng, dt, dst_off)
+    if dt == np.int32:
+        scal = np.array([1, 0, 0, 0, 2, 0, -3, 5], dt)
+    else:
+        a, b = _values(rng, dt, 2)
+        scal = np.array([1, 0, 0, 0, a, 0, a, b], dt)
+    exp = dst0.copy()
+    oracle.exec_tile_ops(code, ops, scal, src.ctypes.data, exp.ctypes.data)
+    d_src = torch.from_numpy(src.view(np.uint8).copy()).cuda()
+    d_dst = torch.from_numpy(dst0.view(np.uint8).copy()).cuda()
+    gpu.execute_tiles(code, ops, scal, d_src.data_ptr(), d_dst.data_ptr())
+    torch.cuda.synchronize()
+    got = d_dst.cpu().numpy().view(dt)
+    bad = np.flatnonzero((got.view(np.uint8).reshape(dst_off, E)
+                          != exp.view(np.uint8).reshape(dst_off, E)).any(1))
+    assert bad.size == 0, f"{bad.size} elements differ, first at {bad[0]}: {got[bad[0]]} vs {exp[bad[0]]}"

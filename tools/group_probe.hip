@@ -12,7 +12,7 @@
 // thread issuing all its loads before its LDS writes; then it writes the C chunks in memory order.
 // The result is checked on the host against the definition, element by element.
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/group_probe.hip -o tools/group_probe
-//   tools/group_probe [N|T] [cap elements] [steps] [waves per workgroup 4|8] [elements per lane 8|16]
+//   tools/group_probe [N|T] [cap elements] [steps] [waves per workgroup 4|8] [elements per lane 8|16] [group order 0|1|2]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -247,6 +247,14 @@ int main(int argc, char** argv) {
             }
         }
     }
+    // group order: 0 as built, 1 by the address of the first C piece, 2 by the first A piece
+    const int order = argc > 6 ? std::atoi(argv[6]) : 0;
+    if (order) {
+        std::stable_sort(G.begin(), G.end(), [&](const group& x, const group& y) {
+            return order == 1 ? PC[size_t(x.pc)].addr < PC[size_t(y.pc)].addr
+                              : PC[size_t(x.pa)].addr < PC[size_t(y.pa)].addr;
+        });
+    }
     const int64_t el = int64_t(n) * n;
     const bool ax = op == 'T';
     const float alpha = ax ? -0.5f : 1.f, beta = ax ? 2.f : 0.f;
@@ -320,7 +328,7 @@ int main(int argc, char** argv) {
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
     ms /= float(steps);
-    std::printf("op %c cap %d waves %d U %d: kernel %.4f ms  %.1f GB/s\n", op, cap, NW, U, ms,
+    std::printf("op %c cap %d waves %d U %d order %d: kernel %.4f ms  %.1f GB/s\n", op, cap, NW, U, order, ms,
                 bytes / (ms * 1e-3) / 1e9);
     return 0;
 }
