@@ -299,34 +299,55 @@ struct shape {
 #define COSTA_MEDIUM 1
 #endif
 template <typename T> struct shapes;
+#ifndef COSTA_COPY_F_BF
+#define COSTA_COPY_F_NT 1024
+#define COSTA_COPY_F_BF 256
+#define COSTA_COPY_F_BS 128
+#endif
 template <> struct shapes<float> {
-    using large = shape<float, 1024, 256, 128>;
+    using large = shape<float, COSTA_COPY_F_NT, COSTA_COPY_F_BF, COSTA_COPY_F_BS>;
     using large_tr = shape<float, COSTA_LARGE_F_NT, COSTA_LARGE_F_BF, COSTA_LARGE_F_BS>;
     using medium_tr = shape<float, 256, 64, 64>;
     static constexpr bool has_medium = COSTA_MEDIUM;
 };
 template <> struct shapes<int> {
-    using large = shape<int, 1024, 256, 128>;
+    using large = shape<int, COSTA_COPY_F_NT, COSTA_COPY_F_BF, COSTA_COPY_F_BS>;
     using large_tr = shape<int, COSTA_LARGE_F_NT, COSTA_LARGE_F_BF, COSTA_LARGE_F_BS>;
     using medium_tr = shape<int, 256, 64, 64>;
     static constexpr bool has_medium = COSTA_MEDIUM;
 };
+// Copy lists of fp64 take 256 threads per 128 KiB sub-tile (each thread 32 16-byte loads in
+// flight, one workgroup per CU), c128 512 threads: BASELINE cfg 3's copy (32768^2 fp64, 128^2
+// blocks) 2.80-2.81 ms against 2.89-3.06 with 1024 threads, c128 16384^2 copies 1.469 against
+// 1.577 ms; fp64 256^2 blocks, fp32 and c64 unchanged or slower that way (tools/copy_probe.py,
+// profiles/r2c/copy_shapes/).  COSTA_COPY_{D,F}_{NT,BF,BS}, COSTA_COPY_{C,Z}_NT: tuning builds.
+#ifndef COSTA_COPY_D_BF
+#define COSTA_COPY_D_NT 256
+#define COSTA_COPY_D_BF 128
+#define COSTA_COPY_D_BS 128
+#endif
 template <> struct shapes<double> {
-    using large = shape<double, 1024, 128, 128>;
+    using large = shape<double, COSTA_COPY_D_NT, COSTA_COPY_D_BF, COSTA_COPY_D_BS>;
     using large_tr = shape<double, COSTA_LARGE_D_NT, COSTA_LARGE_D_BF, COSTA_LARGE_D_BS>;
     using medium_tr = shape<double, 256, 32, 64>;
     static constexpr bool has_medium = COSTA_MEDIUM;
 };
+#ifndef COSTA_COPY_C_NT
+#define COSTA_COPY_C_NT 1024
+#endif
+#ifndef COSTA_COPY_Z_NT
+#define COSTA_COPY_Z_NT 512
+#endif
 template <> struct shapes<cpx<float>> {
-    using large = shape<cpx<float>, 1024, 128, 128>;
-    using large_tr = large;
-    using medium_tr = large;
+    using large = shape<cpx<float>, COSTA_COPY_C_NT, 128, 128>;
+    using large_tr = shape<cpx<float>, 1024, 128, 128>;
+    using medium_tr = large_tr;
     static constexpr bool has_medium = false;
 };
 template <> struct shapes<cpx<double>> {
-    using large = shape<cpx<double>, 1024, 64, 128>;
-    using large_tr = large;
-    using medium_tr = large;
+    using large = shape<cpx<double>, COSTA_COPY_Z_NT, 64, 128>;
+    using large_tr = shape<cpx<double>, 1024, 64, 128>;
+    using medium_tr = large_tr;
     static constexpr bool has_medium = false;
 };
 
