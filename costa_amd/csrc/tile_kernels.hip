@@ -338,15 +338,21 @@ template <> struct shapes<double> {
 #ifndef COSTA_COPY_Z_NT
 #define COSTA_COPY_Z_NT 512
 #endif
+#ifndef COSTA_TR_C_NT  // transposing-list shapes of complex types (tuning builds only)
+#define COSTA_TR_C_NT 1024
+#endif
+#ifndef COSTA_TR_Z_NT  // c128 transposes: 256 threads (BASELINE cfg 4's slice 2.205 against
+#define COSTA_TR_Z_NT 256  // 2.261-2.265 ms; 16384^2 128^2 / 256^2 blocks 2-3 % faster; c64 and
+#endif                     // fp32 slower that way: profiles/r2c/tr_shapes/)
 template <> struct shapes<cpx<float>> {
     using large = shape<cpx<float>, COSTA_COPY_C_NT, 128, 128>;
-    using large_tr = shape<cpx<float>, 1024, 128, 128>;
+    using large_tr = shape<cpx<float>, COSTA_TR_C_NT, 128, 128>;
     using medium_tr = large_tr;
     static constexpr bool has_medium = false;
 };
 template <> struct shapes<cpx<double>> {
     using large = shape<cpx<double>, COSTA_COPY_Z_NT, 64, 128>;
-    using large_tr = shape<cpx<double>, 1024, 64, 128>;
+    using large_tr = shape<cpx<double>, COSTA_TR_Z_NT, 64, 128>;
     using medium_tr = large_tr;
     static constexpr bool has_medium = false;
 };
