@@ -519,11 +519,11 @@ __global__ __launch_bounds__(S::NT) void tile_kernel(const costa_tile_op_t* __re
 // ragged edges.  Variants measured slower and removed: 16-byte copy accesses,
 // several ops per wavefront (strided, chunked, moved together), a persistent pipelined kernel
 // (next op's loads in flight while this op stores: 2.9 against 4.4 TB/s), nt cache policy here.
-// Wavefronts per workgroup: 2 for lists that transpose (4 KiB of LDS per wavefront), 8 for
+// Wavefronts per workgroup: 4 for lists that transpose (4 KiB of LDS per wavefront), 8 for
 // copy-only lists (no LDS) (profiles/r06/c5_knobs.log).
 #ifndef COSTA_TINY_WAVES_TR  // build-time overrides for tuning builds (tools/tiny_variants.sh)
-#define COSTA_TINY_WAVES_TR 2
-#endif
+#define COSTA_TINY_WAVES_TR 4  // r2: cfg 5 'T' 0.7733 -> 0.7629 ms against 2 (1: 0.7637, 8: 0.800;
+#endif                         // profiles/r2d/c5T_waves/)
 #ifndef COSTA_TINY_WAVES_COPY
 #define COSTA_TINY_WAVES_COPY 8
 #endif
