@@ -490,6 +490,16 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         else
             cls[li] = 2;
     }
+    // a transposing list whose large ops all fit the square variant of the large shape runs them
+    // on it (one sub-tile per op instead of a half-filled large one: fp64 64^2 blocks)
+    bool sq = sh.bf_q > 0;
+    size_t n_large_ops = 0;
+    for (size_t li = 0; li < ops.size(); ++li)
+        if (cls[li] == 0) {
+            ++n_large_ops;
+            sq = sq && ops[li].nf <= sh.bf_q && ops[li].ns <= sh.bs_q;
+        }
+    sq = sq && n_large_ops > 0;
     std::vector<uint32_t> shaped[2];  // [0] large, [1] medium
     for (size_t li = 0; li < ops.size(); ++li) {
         const int c = cls[li] == 1 && n_med < kMinMediumOps ? 2 : cls[li];
@@ -500,7 +510,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     // transpose 8-byte elements then take the sub-tiles in destination-address order (wave_knobs)
     int64_t n_work[2] = {0, 0};
     for (int c = 0; c < 2; ++c) {
-        const int bf = c ? sh.bf_m : sh.bf, bs = c ? sh.bs_m : sh.bs;
+        const int bf = c ? sh.bf_m : sq ? sh.bf_q : sh.bf, bs = c ? sh.bs_m : sq ? sh.bs_q : sh.bs;
         const std::vector<uint32_t>& sel = shaped[c];
         std::vector<uint32_t> sperm(sel.size());
         for (size_t i = 0; i < sel.size(); ++i) sperm[i] = uint32_t(i);
@@ -615,6 +625,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         at_piece[i + 1] = at_piece[i] + size_t(grid[i].nfc * grid[i].nsc);
     work_split w;
     w.tr_shape = tr_shape;
+    w.sq = sq;
     w.n_large = n_work[0];
     w.n_medium = n_work[1];
     w.tiny_first = int64_t(ordered.size());
@@ -644,6 +655,7 @@ launch_args make_launch(const work_split& w, const void* d_ordered, const void* 
     a.any_transpose = transpose;
     a.any_axpby = axpby;
     a.tr_shape = w.tr_shape;
+    a.sq = w.sq;
     return a;
 }
 

@@ -188,14 +188,16 @@ struct launch_args {
     bool any_transpose;     // false: copy-mode ops only, launch without the LDS tile
     bool any_axpby;         // false: no op reads its destination (beta == 0 everywhere)
     bool tr_shape;          // the work items are sub-tiles of the transposing lists' shape
+    bool sq;                // ... of its square variant (work_split::sq)
 };
 bool any_transpose(const std::vector<costa_tile_op_t>& ops);
 bool any_axpby(const std::vector<costa_tile_op_t>& ops);
 void launch_tiles(costa_dtype_t dtype, const launch_args& a, void* stream /* hipStream_t */);
 // sub-tile shapes (elements along the source's fast dim, along its slow dim) of a copy-only list
-// or of a list with transposing ops: the large shape, and the medium one (bf_m = bs_m = 0: none)
+// or of a list with transposing ops: the large shape, the medium one (bf_m = bs_m = 0: none) and
+// the large shape's square variant for lists whose large ops all fit it (bf_q = bs_q = 0: none)
 struct shape_dims {
-    int bf = 0, bs = 0, bf_m = 0, bs_m = 0;
+    int bf = 0, bs = 0, bf_m = 0, bs_m = 0, bf_q = 0, bs_q = 0;
 };
 void tile_shapes(costa_dtype_t dtype, bool transposing_list, shape_dims* out);
 // Execution order of an op list: `ordered` = [sub-tiled ops | tiny ops] (tiny ops sorted by the
@@ -205,6 +207,7 @@ void tile_shapes(costa_dtype_t dtype, bool transposing_list, shape_dims* out);
 struct work_split {
     int64_t n_large = 0, n_medium = 0, tiny_first = 0, n_tiny = 0;
     bool tr_shape = false;  // sub-tiles cut with tile_shapes(dtype, true, ...)
+    bool sq = false;        // ... the large ops with its square variant (bf_q x bs_q)
     int64_t n_items() const { return n_large + n_medium + n_tiny; }
 };
 // pack_list: the ops write the dense send package (their destinations are contiguous whatever

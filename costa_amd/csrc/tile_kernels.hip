@@ -304,17 +304,25 @@ template <typename T> struct shapes;
 #define COSTA_COPY_F_BF 256
 #define COSTA_COPY_F_BS 128
 #endif
+// `small_tr` (fp64): the square 64 x 64 variant of the large transposing shape, 512 threads, for
+// transposing lists whose large ops all fit in it (engine.cpp build_work): a 64^2 block then fills
+// one sub-tile instead of half of a 64 x 128 one, and four workgroups fit a CU.  fp64 16384^2 'T'
+// with 64^2 blocks 0.683-0.726 ms against 0.783 (profiles/r2d/small_blocks/).
 template <> struct shapes<float> {
     using large = shape<float, COSTA_COPY_F_NT, COSTA_COPY_F_BF, COSTA_COPY_F_BS>;
     using large_tr = shape<float, COSTA_LARGE_F_NT, COSTA_LARGE_F_BF, COSTA_LARGE_F_BS>;
     using medium_tr = shape<float, 256, 64, 64>;
     static constexpr bool has_medium = COSTA_MEDIUM;
+    using small_tr = large_tr;
+    static constexpr bool has_small = false;
 };
 template <> struct shapes<int> {
     using large = shape<int, COSTA_COPY_F_NT, COSTA_COPY_F_BF, COSTA_COPY_F_BS>;
     using large_tr = shape<int, COSTA_LARGE_F_NT, COSTA_LARGE_F_BF, COSTA_LARGE_F_BS>;
     using medium_tr = shape<int, 256, 64, 64>;
     static constexpr bool has_medium = COSTA_MEDIUM;
+    using small_tr = large_tr;
+    static constexpr bool has_small = false;
 };
 // Copy lists of fp64 take 256 threads per 128 KiB sub-tile (each thread 32 16-byte loads in
 // flight, one workgroup per CU), c128 512 threads: BASELINE cfg 3's copy (32768^2 fp64, 128^2
@@ -331,6 +339,8 @@ template <> struct shapes<double> {
     using large_tr = shape<double, COSTA_LARGE_D_NT, COSTA_LARGE_D_BF, COSTA_LARGE_D_BS>;
     using medium_tr = shape<double, 256, 32, 64>;
     static constexpr bool has_medium = COSTA_MEDIUM;
+    using small_tr = shape<double, 512, 64, 64>;
+    static constexpr bool has_small = true;
 };
 #ifndef COSTA_COPY_C_NT
 #define COSTA_COPY_C_NT 1024
@@ -349,12 +359,16 @@ template <> struct shapes<cpx<float>> {
     using large_tr = shape<cpx<float>, COSTA_TR_C_NT, 128, 128>;
     using medium_tr = large_tr;
     static constexpr bool has_medium = false;
+    using small_tr = large_tr;
+    static constexpr bool has_small = false;
 };
 template <> struct shapes<cpx<double>> {
     using large = shape<cpx<double>, COSTA_COPY_Z_NT, 64, 128>;
     using large_tr = shape<cpx<double>, COSTA_TR_Z_NT, 64, 128>;
     using medium_tr = large_tr;
     static constexpr bool has_medium = false;
+    using small_tr = large_tr;
+    static constexpr bool has_small = false;
 };
 
 // One sub-tile.  FULL: the sub-tile is a whole BF x BS block with 16-byte aligned rows on
@@ -748,7 +762,10 @@ template <typename T>
 void launch_t(const launch_args& a, hipStream_t stream) {
     // work list: the large shape's sub-tiles (the list's shape: build_work cut them with
     // tile_shapes(dtype, tr_shape)), then the wavefront ops
-    if (a.tr_shape)
+    if (a.sq) {
+        if (!shapes<T>::has_small || !a.tr_shape) throw error(COSTA_ERR_INTERNAL, "costa: square shape");
+        launch_shape<T, typename shapes<T>::small_tr>(a, a.work, a.n_large, stream);
+    } else if (a.tr_shape)
         launch_shape<T, typename shapes<T>::large_tr>(a, a.work, a.n_large, stream);
     else
         launch_shape<T, typename shapes<T>::large>(a, a.work, a.n_large, stream);
@@ -766,6 +783,9 @@ void shape_of(bool tr, shape_dims* d) {
     const bool med = tr && shapes<T>::has_medium;
     d->bf_m = med ? shapes<T>::medium_tr::BF : 0;
     d->bs_m = med ? shapes<T>::medium_tr::BS : 0;
+    const bool sq = tr && shapes<T>::has_small;
+    d->bf_q = sq ? shapes<T>::small_tr::BF : 0;
+    d->bs_q = sq ? shapes<T>::small_tr::BS : 0;
 }
 
 template <typename T, typename S>
@@ -779,6 +799,7 @@ void set_lds_limits() {
     set_lds_limit<T, typename shapes<T>::large>();
     set_lds_limit<T, typename shapes<T>::large_tr>();
     set_lds_limit<T, typename shapes<T>::medium_tr>();
+    set_lds_limit<T, typename shapes<T>::small_tr>();
 }
 
 }  // namespace
