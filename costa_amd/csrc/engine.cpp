@@ -475,31 +475,42 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     // ms without, profiles/r2/shapes/ab_medium_cfg5T.log)
     constexpr size_t kMinMediumOps = 4096;
     std::vector<uint8_t> cls(ops.size(), 3);  // 0 large, 1 medium, 2 wavefront, 3 empty
+    auto is_large = [&](const costa_tile_op_t& op, int64_t lo) {
+        const int64_t elems = int64_t(op.nf) * op.ns;
+        const bool aligned = (op.flags & vec_both) == vec_both;
+        bool large = 2 * elems >= lo;
+        if (kn.policy == 2 && !aligned && elems <= kUnalignedWaveCap * sub_elems) large = false;
+        return large && !is_tiny(op, E);
+    };
+    // A transposing list whose large ops all fit the square variant of the large shape (bf_q x
+    // bs_q) runs them on it: one sub-tile per op instead of a half-filled large one (fp64 / c64 /
+    // c128 64^2 blocks).  Without a medium tier (complex types) the large class then starts at
+    // half a square sub-tile.
+    const int64_t q_elems = int64_t(sh.bf_q) * sh.bs_q;
+    const int64_t q_lo = med_elems > 0 ? sub_elems : q_elems;
+    bool sq = q_elems > 0;
+    size_t n_cand = 0;
+    for (size_t li = 0; sq && li < ops.size(); ++li) {
+        const costa_tile_op_t& op = ops[li];
+        if (op.nf <= 0 || op.ns <= 0 || !is_large(op, q_lo)) continue;
+        ++n_cand;
+        sq = op.nf <= sh.bf_q && op.ns <= sh.bs_q;
+    }
+    sq = sq && n_cand > 0;
+    const int64_t large_lo = sq ? q_lo : sub_elems;
     size_t n_med = 0;
     for (size_t li = 0; li < ops.size(); ++li) {
         const costa_tile_op_t& op = ops[li];
         if (op.nf <= 0 || op.ns <= 0) continue;
         const int64_t elems = int64_t(op.nf) * op.ns;
         const bool aligned = (op.flags & vec_both) == vec_both;
-        bool large = 2 * elems >= sub_elems;
-        if (kn.policy == 2 && !aligned && elems <= kUnalignedWaveCap * sub_elems) large = false;
-        if (large && !is_tiny(op, E))
+        if (is_large(op, large_lo))
             cls[li] = 0;
         else if (med_elems > 0 && aligned && 2 * elems >= med_elems && (op.flags & COSTA_TILE_TRANSPOSE))
             cls[li] = 1, ++n_med;
         else
             cls[li] = 2;
     }
-    // a transposing list whose large ops all fit the square variant of the large shape runs them
-    // on it (one sub-tile per op instead of a half-filled large one: fp64 64^2 blocks)
-    bool sq = sh.bf_q > 0;
-    size_t n_large_ops = 0;
-    for (size_t li = 0; li < ops.size(); ++li)
-        if (cls[li] == 0) {
-            ++n_large_ops;
-            sq = sq && ops[li].nf <= sh.bf_q && ops[li].ns <= sh.bs_q;
-        }
-    sq = sq && n_large_ops > 0;
     std::vector<uint32_t> shaped[2];  // [0] large, [1] medium
     for (size_t li = 0; li < ops.size(); ++li) {
         const int c = cls[li] == 1 && n_med < kMinMediumOps ? 2 : cls[li];
@@ -626,6 +637,11 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     work_split w;
     w.tr_shape = tr_shape;
     w.sq = sq;
+    w.full = tr_shape && !sq && !shaped[0].empty();
+    for (const uint32_t li : shaped[0]) {
+        const costa_tile_op_t& op = ops[li];
+        w.full = w.full && (op.flags & vec_both) == vec_both && op.nf % sh.bf == 0 && op.ns % sh.bs == 0;
+    }
     w.n_large = n_work[0];
     w.n_medium = n_work[1];
     w.tiny_first = int64_t(ordered.size());
@@ -656,6 +672,7 @@ launch_args make_launch(const work_split& w, const void* d_ordered, const void* 
     a.any_axpby = axpby;
     a.tr_shape = w.tr_shape;
     a.sq = w.sq;
+    a.full = w.full;
     return a;
 }
 

@@ -189,6 +189,7 @@ struct launch_args {
     bool any_axpby;         // false: no op reads its destination (beta == 0 everywhere)
     bool tr_shape;          // the work items are sub-tiles of the transposing lists' shape
     bool sq;                // ... of its square variant (work_split::sq)
+    bool full;              // work_split::full
 };
 bool any_transpose(const std::vector<costa_tile_op_t>& ops);
 bool any_axpby(const std::vector<costa_tile_op_t>& ops);
@@ -208,6 +209,8 @@ struct work_split {
     int64_t n_large = 0, n_medium = 0, tiny_first = 0, n_tiny = 0;
     bool tr_shape = false;  // sub-tiles cut with tile_shapes(dtype, true, ...)
     bool sq = false;        // ... the large ops with its square variant (bf_q x bs_q)
+    bool full = false;      // every large op of a transposing list is aligned and a whole number
+                            // of large sub-tiles (the launch may then take fewer threads)
     int64_t n_items() const { return n_large + n_medium + n_tiny; }
 };
 // pack_list: the ops write the dense send package (their destinations are contiguous whatever

@@ -308,6 +308,9 @@ template <typename T> struct shapes;
 // transposing lists whose large ops all fit in it (engine.cpp build_work): a 64^2 block then fills
 // one sub-tile instead of half of a 64 x 128 one, and four workgroups fit a CU.  fp64 16384^2 'T'
 // with 64^2 blocks 0.683-0.726 ms against 0.783 (profiles/r2d/small_blocks/).
+#ifndef COSTA_SQ_COMPLEX  // 0: no square variant for complex types (tuning builds only)
+#define COSTA_SQ_COMPLEX 1
+#endif
 template <> struct shapes<float> {
     using large = shape<float, COSTA_COPY_F_NT, COSTA_COPY_F_BF, COSTA_COPY_F_BS>;
     using large_tr = shape<float, COSTA_LARGE_F_NT, COSTA_LARGE_F_BF, COSTA_LARGE_F_BS>;
@@ -315,6 +318,7 @@ template <> struct shapes<float> {
     static constexpr bool has_medium = COSTA_MEDIUM;
     using small_tr = large_tr;
     static constexpr bool has_small = false;
+    using large_tr_full = large_tr;
 };
 template <> struct shapes<int> {
     using large = shape<int, COSTA_COPY_F_NT, COSTA_COPY_F_BF, COSTA_COPY_F_BS>;
@@ -323,6 +327,7 @@ template <> struct shapes<int> {
     static constexpr bool has_medium = COSTA_MEDIUM;
     using small_tr = large_tr;
     static constexpr bool has_small = false;
+    using large_tr_full = large_tr;
 };
 // Copy lists of fp64 take 256 threads per 128 KiB sub-tile (each thread 32 16-byte loads in
 // flight, one workgroup per CU), c128 512 threads: BASELINE cfg 3's copy (32768^2 fp64, 128^2
@@ -341,6 +346,7 @@ template <> struct shapes<double> {
     static constexpr bool has_medium = COSTA_MEDIUM;
     using small_tr = shape<double, 512, 64, 64>;
     static constexpr bool has_small = true;
+    using large_tr_full = large_tr;
 };
 #ifndef COSTA_COPY_C_NT
 #define COSTA_COPY_C_NT 1024
@@ -351,24 +357,28 @@ template <> struct shapes<double> {
 #ifndef COSTA_TR_C_NT  // transposing-list shapes of complex types (tuning builds only)
 #define COSTA_TR_C_NT 1024
 #endif
-#ifndef COSTA_TR_Z_NT  // c128 transposes: 256 threads (BASELINE cfg 4's slice 2.205 against
-#define COSTA_TR_Z_NT 256  // 2.261-2.265 ms; 16384^2 128^2 / 256^2 blocks 2-3 % faster; c64 and
-#endif                     // fp32 slower that way: profiles/r2c/tr_shapes/)
+#ifndef COSTA_TR_Z_NT  // c128 transposes: 1024 threads.  256 gain 3 % when every op is a whole
+#define COSTA_TR_Z_NT 1024  // number of sub-tiles (cfg 4's 128^2 blocks: 2.19 against 2.26 ms; the
+#endif                      // `large_tr_full` launch, engine.cpp work_split::full) and lose 35-55 %
+                            // with blocks that half-fill them (80^2 3.05 against 1.98 ms, 96^2 2.35
+                            // against 1.74; profiles/r2c/tr_shapes/, profiles/r2d/c128_threads.log)
 template <> struct shapes<cpx<float>> {
     using large = shape<cpx<float>, COSTA_COPY_C_NT, 128, 128>;
     using large_tr = shape<cpx<float>, COSTA_TR_C_NT, 128, 128>;
     using medium_tr = large_tr;
     static constexpr bool has_medium = false;
-    using small_tr = large_tr;
-    static constexpr bool has_small = false;
+    using small_tr = shape<cpx<float>, 512, 64, 64>;
+    static constexpr bool has_small = COSTA_SQ_COMPLEX;
+    using large_tr_full = large_tr;
 };
 template <> struct shapes<cpx<double>> {
     using large = shape<cpx<double>, COSTA_COPY_Z_NT, 64, 128>;
     using large_tr = shape<cpx<double>, COSTA_TR_Z_NT, 64, 128>;
     using medium_tr = large_tr;
     static constexpr bool has_medium = false;
-    using small_tr = large_tr;
-    static constexpr bool has_small = false;
+    using small_tr = shape<cpx<double>, 256, 64, 64>;
+    static constexpr bool has_small = COSTA_SQ_COMPLEX;
+    using large_tr_full = shape<cpx<double>, 256, 64, 128>;
 };
 
 // One sub-tile.  FULL: the sub-tile is a whole BF x BS block with 16-byte aligned rows on
@@ -765,7 +775,9 @@ void launch_t(const launch_args& a, hipStream_t stream) {
     if (a.sq) {
         if (!shapes<T>::has_small || !a.tr_shape) throw error(COSTA_ERR_INTERNAL, "costa: square shape");
         launch_shape<T, typename shapes<T>::small_tr>(a, a.work, a.n_large, stream);
-    } else if (a.tr_shape)
+    } else if (a.tr_shape && a.full)
+        launch_shape<T, typename shapes<T>::large_tr_full>(a, a.work, a.n_large, stream);
+    else if (a.tr_shape)
         launch_shape<T, typename shapes<T>::large_tr>(a, a.work, a.n_large, stream);
     else
         launch_shape<T, typename shapes<T>::large>(a, a.work, a.n_large, stream);
@@ -800,6 +812,7 @@ void set_lds_limits() {
     set_lds_limit<T, typename shapes<T>::large_tr>();
     set_lds_limit<T, typename shapes<T>::medium_tr>();
     set_lds_limit<T, typename shapes<T>::small_tr>();
+    set_lds_limit<T, typename shapes<T>::large_tr_full>();
 }
 
 }  // namespace

@@ -231,20 +231,24 @@ def test_unaligned_large_list(gpu, code, copy_only):
     assert bad.size == 0, f"{bad.size} elements differ, first at {bad[0]}: {got[bad[0]]} vs {exp[bad[0]]}"
 
 
+@pytest.mark.parametrize("code", [1, 2, 3], ids=["f64", "c64", "c128"])
 @pytest.mark.parametrize("seed", [1, 2])
-def test_square_shape_list(gpu, seed):
-    """an fp64 transposing list whose large ops all fit 64 x 64 (nb = 64 blocks): the large ops
-    run on the square variant of the transposing shape (engine.cpp build_work, tile_kernels.hip
-    small_tr); copy-mode ops, padded and unaligned strides, every scale kind, plus small ops on
-    the wavefront path; bit-exact against the oracle"""
-    rng = np.random.default_rng(640 + seed)
-    code, dt, E = 1, np.float64, 8
+def test_square_shape_list(gpu, code, seed):
+    """a transposing list whose large ops all fit 64 x 64 (nb = 64 blocks): the large ops run on
+    the square variant of the transposing shape (engine.cpp build_work, tile_kernels.hip
+    small_tr); copy-mode ops, padded and unaligned strides, every scale kind (conjugation for
+    complex types), plus small ops on the wavefront path; bit-exact against the oracle"""
+    rng = np.random.default_rng(640 + seed + 10 * code)
+    dt = oracle.NP[code]
+    E = np.dtype(dt).itemsize
+    cplx = np.issubdtype(dt, np.complexfloating)
     n_ops = 600
     ops = np.zeros(n_ops, costa_amd.TILE_OP_DTYPE)
     src_off = dst_off = 0
     for i in range(n_ops):
         tr = rng.integers(0, 4) != 0
-        nf, ns = (64, 64) if rng.integers(0, 5) else (int(rng.integers(1, 40)), int(rng.integers(1, 40)))
+        nf, ns = ((64, 64) if rng.integers(0, 3) else (int(rng.integers(46, 65)), int(rng.integers(46, 65)))) \
+            if rng.integers(0, 5) else (int(rng.integers(1, 40)), int(rng.integers(1, 40)))
         lds = nf + int(rng.integers(0, 3)) * int(rng.integers(0, 2))
         dn, d_slow = (ns, nf) if tr else (nf, ns)
         ldd = dn + int(rng.integers(0, 3)) * int(rng.integers(0, 2))
@@ -252,14 +256,15 @@ def test_square_shape_list(gpu, seed):
             src_off += 1
             dst_off += 1
         else:
-            src_off += src_off % 2
-            dst_off += dst_off % 2
+            src_off = -(-src_off * E // 16) * 16 // E
+            dst_off = -(-dst_off * E // 16) * 16 // E
+        conj = bool(cplx and rng.integers(0, 2))
         kind = int(rng.integers(0, 4))
-        if kind == 0 and tr:
+        if kind == 0 and (tr or conj):
             kind, slot = 2, 0
         else:
             slot = (0, 1, 2, 3)[kind] if kind != 2 else int(rng.choice([0, 2]))
-        flags = (1 if tr else 0) | (kind << 4) | (slot << 16)
+        flags = (1 if tr else 0) | (2 if conj else 0) | (kind << 4) | (slot << 16)
         if (src_off * E) % 16 == 0 and (lds * E) % 16 == 0:
             flags |= 4
         if (dst_off * E) % 16 == 0 and (ldd * E) % 16 == 0:
@@ -267,6 +272,50 @@ def test_square_shape_list(gpu, seed):
         ops[i] = (src_off * E, dst_off * E, nf, ns, lds, ldd, flags, 0)
         src_off += (ns - 1) * lds + nf
         dst_off += (d_slow - 1) * ldd + dn
+    src = _values(rng, dt, src_off)
+    dst0 = _values(rng, dt, dst_off)
+    a, b = _values(rng, dt, 2)
+    scal = np.array([1, 0, 0, 0, a, 0, a, b], dt)
+    exp = dst0.copy()
+    oracle.exec_tile_ops(code, ops, scal, src.ctypes.data, exp.ctypes.data)
+    d_src = torch.from_numpy(src.view(np.uint8).copy()).cuda()
+    d_dst = torch.from_numpy(dst0.view(np.uint8).copy()).cuda()
+    gpu.execute_tiles(code, ops, scal, d_src.data_ptr(), d_dst.data_ptr())
+    torch.cuda.synchronize()
+    got = d_dst.cpu().numpy().view(dt)
+    bad = np.flatnonzero((got.view(np.uint8).reshape(dst_off, E)
+                          != exp.view(np.uint8).reshape(dst_off, E)).any(1))
+    assert bad.size == 0, f"{bad.size} elements differ, first at {bad[0]}: {got[bad[0]]} vs {exp[bad[0]]}"
+
+
+@pytest.mark.parametrize("code", [3, 1], ids=["c128", "f64"])
+def test_full_tile_list(gpu, code):
+    """a transposing list whose ops are all aligned whole multiples of the large sub-tile (c128
+    64 x 128, fp64 64 x 128): the `large_tr_full` launch (engine.cpp work_split::full); copy and
+    transpose ops, every scale kind (conjugation for c128); bit-exact against the oracle"""
+    rng = np.random.default_rng(9100 + code)
+    dt = oracle.NP[code]
+    E = np.dtype(dt).itemsize
+    cplx = np.issubdtype(dt, np.complexfloating)
+    n_ops = 40
+    ops = np.zeros(n_ops, costa_amd.TILE_OP_DTYPE)
+    src_off = dst_off = 0
+    for i in range(n_ops):
+        tr = i == 0 or rng.integers(0, 4) != 0
+        nf, ns = 64 * int(rng.integers(1, 4)), 128 * int(rng.integers(1, 3))
+        lds = nf + (16 // E) * int(rng.integers(0, 2))
+        dn, d_slow = (ns, nf) if tr else (nf, ns)
+        ldd = dn + (16 // E) * int(rng.integers(0, 2))
+        conj = bool(cplx and rng.integers(0, 2))
+        kind = int(rng.integers(0, 4))
+        if kind == 0 and (tr or conj):
+            kind, slot = 2, 0
+        else:
+            slot = (0, 1, 2, 3)[kind] if kind != 2 else int(rng.choice([0, 2]))
+        ops[i] = (src_off * E, dst_off * E, nf, ns, lds, ldd,
+                  (1 if tr else 0) | (2 if conj else 0) | 4 | 8 | (kind << 4) | (slot << 16), 0)
+        src_off += -(-((ns - 1) * lds + nf) * E // 16) * 16 // E
+        dst_off += -(-((d_slow - 1) * ldd + dn) * E // 16) * 16 // E
     src = _values(rng, dt, src_off)
     dst0 = _values(rng, dt, dst_off)
     a, b = _values(rng, dt, 2)
