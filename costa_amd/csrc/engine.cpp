@@ -642,6 +642,9 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         const costa_tile_op_t& op = ops[li];
         w.full = w.full && (op.flags & vec_both) == vec_both && op.nf % sh.bf == 0 && op.ns % sh.bs == 0;
     }
+    w.med_full = !shaped[1].empty() && n_work[1] > 0;
+    for (const uint32_t li : shaped[1])
+        w.med_full = w.med_full && ops[li].nf % sh.bf_m == 0 && ops[li].ns % sh.bs_m == 0;
     w.n_large = n_work[0];
     w.n_medium = n_work[1];
     w.tiny_first = int64_t(ordered.size());
@@ -673,6 +676,7 @@ launch_args make_launch(const work_split& w, const void* d_ordered, const void* 
     a.tr_shape = w.tr_shape;
     a.sq = w.sq;
     a.full = w.full;
+    a.med_full = w.med_full;
     return a;
 }
 

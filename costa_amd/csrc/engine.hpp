@@ -190,6 +190,7 @@ struct launch_args {
     bool tr_shape;          // the work items are sub-tiles of the transposing lists' shape
     bool sq;                // ... of its square variant (work_split::sq)
     bool full;              // work_split::full
+    bool med_full;          // work_split::med_full
 };
 bool any_transpose(const std::vector<costa_tile_op_t>& ops);
 bool any_axpby(const std::vector<costa_tile_op_t>& ops);
@@ -211,6 +212,7 @@ struct work_split {
     bool sq = false;        // ... the large ops with its square variant (bf_q x bs_q)
     bool full = false;      // every large op of a transposing list is aligned and a whole number
                             // of large sub-tiles (the launch may then take fewer threads)
+    bool med_full = false;  // the same for the medium ops and the medium sub-tile
     int64_t n_items() const { return n_large + n_medium + n_tiny; }
 };
 // pack_list: the ops write the dense send package (their destinations are contiguous whatever

@@ -308,26 +308,39 @@ template <typename T> struct shapes;
 // transposing lists whose large ops all fit in it (engine.cpp build_work): a 64^2 block then fills
 // one sub-tile instead of half of a 64 x 128 one, and four workgroups fit a CU.  fp64 16384^2 'T'
 // with 64^2 blocks 0.683-0.726 ms against 0.783 (profiles/r2d/small_blocks/).
+// medium shapes' threads (tuning builds only).  4-byte types take 128 threads when every medium op
+// of the list is a whole number of sub-tiles (`medium_tr_full`, engine.cpp work_split::med_full):
+// fp32 64^2 blocks 0.455 -> 0.408 ms (beta = 0 only: with C read 0.628 against 0.610); with
+// ragged ops 128 / 512 threads lost 12-21 % (48^2, 80^2)
+// and fp64 lost 12-14 % at 32^2 / 48^2 (profiles/r2d/medium_threads.log)
+#ifndef COSTA_MED_F_NT
+#define COSTA_MED_F_NT 256
+#endif
+#ifndef COSTA_MED_D_NT
+#define COSTA_MED_D_NT 256
+#endif
 #ifndef COSTA_SQ_COMPLEX  // 0: no square variant for complex types (tuning builds only)
 #define COSTA_SQ_COMPLEX 1
 #endif
 template <> struct shapes<float> {
     using large = shape<float, COSTA_COPY_F_NT, COSTA_COPY_F_BF, COSTA_COPY_F_BS>;
     using large_tr = shape<float, COSTA_LARGE_F_NT, COSTA_LARGE_F_BF, COSTA_LARGE_F_BS>;
-    using medium_tr = shape<float, 256, 64, 64>;
+    using medium_tr = shape<float, COSTA_MED_F_NT, 64, 64>;
     static constexpr bool has_medium = COSTA_MEDIUM;
     using small_tr = large_tr;
     static constexpr bool has_small = false;
     using large_tr_full = large_tr;
+    using medium_tr_full = shape<float, 128, 64, 64>;
 };
 template <> struct shapes<int> {
     using large = shape<int, COSTA_COPY_F_NT, COSTA_COPY_F_BF, COSTA_COPY_F_BS>;
     using large_tr = shape<int, COSTA_LARGE_F_NT, COSTA_LARGE_F_BF, COSTA_LARGE_F_BS>;
-    using medium_tr = shape<int, 256, 64, 64>;
+    using medium_tr = shape<int, COSTA_MED_F_NT, 64, 64>;
     static constexpr bool has_medium = COSTA_MEDIUM;
     using small_tr = large_tr;
     static constexpr bool has_small = false;
     using large_tr_full = large_tr;
+    using medium_tr_full = shape<int, 128, 64, 64>;
 };
 // Copy lists of fp64 take 256 threads per 128 KiB sub-tile (each thread 32 16-byte loads in
 // flight, one workgroup per CU), c128 512 threads: BASELINE cfg 3's copy (32768^2 fp64, 128^2
@@ -342,11 +355,12 @@ template <> struct shapes<int> {
 template <> struct shapes<double> {
     using large = shape<double, COSTA_COPY_D_NT, COSTA_COPY_D_BF, COSTA_COPY_D_BS>;
     using large_tr = shape<double, COSTA_LARGE_D_NT, COSTA_LARGE_D_BF, COSTA_LARGE_D_BS>;
-    using medium_tr = shape<double, 256, 32, 64>;
+    using medium_tr = shape<double, COSTA_MED_D_NT, 32, 64>;
     static constexpr bool has_medium = COSTA_MEDIUM;
     using small_tr = shape<double, 512, 64, 64>;
     static constexpr bool has_small = true;
     using large_tr_full = large_tr;
+    using medium_tr_full = medium_tr;
 };
 #ifndef COSTA_COPY_C_NT
 #define COSTA_COPY_C_NT 1024
@@ -370,6 +384,7 @@ template <> struct shapes<cpx<float>> {
     using small_tr = shape<cpx<float>, 512, 64, 64>;
     static constexpr bool has_small = COSTA_SQ_COMPLEX;
     using large_tr_full = large_tr;
+    using medium_tr_full = medium_tr;
 };
 template <> struct shapes<cpx<double>> {
     using large = shape<cpx<double>, COSTA_COPY_Z_NT, 64, 128>;
@@ -379,6 +394,7 @@ template <> struct shapes<cpx<double>> {
     using small_tr = shape<cpx<double>, 256, 64, 64>;
     static constexpr bool has_small = COSTA_SQ_COMPLEX;
     using large_tr_full = shape<cpx<double>, 256, 64, 128>;
+    using medium_tr_full = medium_tr;
 };
 
 // One sub-tile.  FULL: the sub-tile is a whole BF x BS block with 16-byte aligned rows on
@@ -783,7 +799,10 @@ void launch_t(const launch_args& a, hipStream_t stream) {
         launch_shape<T, typename shapes<T>::large>(a, a.work, a.n_large, stream);
     if (a.n_medium > 0) {
         if (!shapes<T>::has_medium || !a.tr_shape) throw error(COSTA_ERR_INTERNAL, "costa: medium shape");
-        launch_shape<T, typename shapes<T>::medium_tr>(a, a.work + a.n_large, a.n_medium, stream);
+        if (a.med_full && !a.any_axpby)  // every medium op a whole number of sub-tiles, C not read
+            launch_shape<T, typename shapes<T>::medium_tr_full>(a, a.work + a.n_large, a.n_medium, stream);
+        else
+            launch_shape<T, typename shapes<T>::medium_tr>(a, a.work + a.n_large, a.n_medium, stream);
     }
     launch_tiny<T>(a, stream);
 }
@@ -813,6 +832,7 @@ void set_lds_limits() {
     set_lds_limit<T, typename shapes<T>::medium_tr>();
     set_lds_limit<T, typename shapes<T>::small_tr>();
     set_lds_limit<T, typename shapes<T>::large_tr_full>();
+    set_lds_limit<T, typename shapes<T>::medium_tr_full>();
 }
 
 }  // namespace

@@ -132,12 +132,14 @@ def test_mixed_tile_list(gpu, code, seed):
     assert bad.size == 0, f"{bad.size} elements differ, first at {bad[0]}: {got[bad[0]]} vs {exp[bad[0]]}"
 
 
-@pytest.mark.parametrize("code,nb", [(0, 64), (1, 32), (1, 48), (4, 64), (0, 80)],
-                         ids=["f32-64", "f64-32", "f64-48", "i32-64", "f32-80"])
-def test_medium_shape_list(gpu, code, nb):
+@pytest.mark.parametrize("code,nb,full", [(0, 64, False), (1, 32, False), (1, 48, False), (4, 64, False),
+                                          (0, 80, False), (0, 64, True), (4, 64, True)],
+                         ids=["f32-64", "f64-32", "f64-48", "i32-64", "f32-80", "f32-64-full", "i32-64-full"])
+def test_medium_shape_list(gpu, code, nb, full):
     """a transposing list of >= 4096 aligned ops between half a medium and half a large
     sub-tile (engine.cpp kMinMediumOps: the medium shape only runs for lists this long), with
-    every scale kind and padded strides; bit-exact against the oracle"""
+    every scale kind and padded strides; full: every op a whole medium sub-tile (the
+    `medium_tr_full` launch); bit-exact against the oracle"""
     rng = np.random.default_rng(77 + code + nb)
     dt = oracle.NP[code]
     E = np.dtype(dt).itemsize
@@ -146,7 +148,7 @@ def test_medium_shape_list(gpu, code, nb):
     src_off = dst_off = 0
     for i in range(n_ops):
         # full, or (above 32) one 16-byte vector short: every op stays in the medium class
-        nf = nb - (int(rng.integers(0, 2)) * (16 // E) if nb > 32 else 0)
+        nf = nb - (int(rng.integers(0, 2)) * (16 // E) if nb > 32 and not full else 0)
         ns = nb
         lds = nf + int(rng.integers(0, 2)) * (16 // E)
         ldd = ns + int(rng.integers(0, 2)) * (16 // E)
