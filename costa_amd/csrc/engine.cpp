@@ -511,6 +511,31 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         else
             cls[li] = 2;
     }
+    // the medium class on 32 x 32 sub-tiles (nb = 32 blocks): in a transposing list whose
+    // aligned transposing ops outside the large class that hold at least half a 32 x 32 sub-tile
+    // all fit one, and are at least kMinMediumOps many
+    bool med_sq = tr_shape && sh.bf_s > 0;
+    size_t n_msq = 0;
+    const int64_t s_elems = int64_t(sh.bf_s) * sh.bs_s;
+    for (size_t li = 0; med_sq && li < ops.size(); ++li) {
+        const costa_tile_op_t& op = ops[li];
+        if (cls[li] == 0 || cls[li] == 3 || (op.flags & vec_both) != vec_both || !(op.flags & COSTA_TILE_TRANSPOSE))
+            continue;
+        if (2 * int64_t(op.nf) * op.ns < s_elems) continue;
+        if (op.nf > sh.bf_s || op.ns > sh.bs_s) med_sq = false;
+        ++n_msq;
+    }
+    med_sq = med_sq && n_msq >= kMinMediumOps;
+    if (med_sq) {
+        n_med = n_msq;
+        for (size_t li = 0; li < ops.size(); ++li) {
+            const costa_tile_op_t& op = ops[li];
+            if (cls[li] == 0 || cls[li] == 3) continue;
+            const bool m = (op.flags & vec_both) == vec_both && (op.flags & COSTA_TILE_TRANSPOSE) &&
+                           2 * int64_t(op.nf) * op.ns >= s_elems;
+            cls[li] = m ? 1 : 2;
+        }
+    }
     std::vector<uint32_t> shaped[2];  // [0] large, [1] medium
     for (size_t li = 0; li < ops.size(); ++li) {
         const int c = cls[li] == 1 && n_med < kMinMediumOps ? 2 : cls[li];
@@ -521,7 +546,8 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     // transpose 8-byte elements then take the sub-tiles in destination-address order (wave_knobs)
     int64_t n_work[2] = {0, 0};
     for (int c = 0; c < 2; ++c) {
-        const int bf = c ? sh.bf_m : sq ? sh.bf_q : sh.bf, bs = c ? sh.bs_m : sq ? sh.bs_q : sh.bs;
+        const int bf = c ? (med_sq ? sh.bf_s : sh.bf_m) : sq ? sh.bf_q : sh.bf;
+        const int bs = c ? (med_sq ? sh.bs_s : sh.bs_m) : sq ? sh.bs_q : sh.bs;
         const std::vector<uint32_t>& sel = shaped[c];
         std::vector<uint32_t> sperm(sel.size());
         for (size_t i = 0; i < sel.size(); ++i) sperm[i] = uint32_t(i);
@@ -642,7 +668,8 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         const costa_tile_op_t& op = ops[li];
         w.full = w.full && (op.flags & vec_both) == vec_both && op.nf % sh.bf == 0 && op.ns % sh.bs == 0;
     }
-    w.med_full = !shaped[1].empty() && n_work[1] > 0;
+    w.med_sq = med_sq && !shaped[1].empty();
+    w.med_full = !shaped[1].empty() && n_work[1] > 0 && !w.med_sq;
     for (const uint32_t li : shaped[1])
         w.med_full = w.med_full && ops[li].nf % sh.bf_m == 0 && ops[li].ns % sh.bs_m == 0;
     w.n_large = n_work[0];
@@ -677,6 +704,7 @@ launch_args make_launch(const work_split& w, const void* d_ordered, const void* 
     a.sq = w.sq;
     a.full = w.full;
     a.med_full = w.med_full;
+    a.med_sq = w.med_sq;
     return a;
 }
 

@@ -191,15 +191,17 @@ struct launch_args {
     bool sq;                // ... of its square variant (work_split::sq)
     bool full;              // work_split::full
     bool med_full;          // work_split::med_full
+    bool med_sq;            // work_split::med_sq
 };
 bool any_transpose(const std::vector<costa_tile_op_t>& ops);
 bool any_axpby(const std::vector<costa_tile_op_t>& ops);
 void launch_tiles(costa_dtype_t dtype, const launch_args& a, void* stream /* hipStream_t */);
 // sub-tile shapes (elements along the source's fast dim, along its slow dim) of a copy-only list
 // or of a list with transposing ops: the large shape, the medium one (bf_m = bs_m = 0: none) and
-// the large shape's square variant for lists whose large ops all fit it (bf_q = bs_q = 0: none)
+// the large shape's square variant for lists whose large ops all fit it (bf_q = bs_q = 0: none),
+// and the 32 x 32 shape the medium class takes when its ops all fit it (bf_s x bs_s)
 struct shape_dims {
-    int bf = 0, bs = 0, bf_m = 0, bs_m = 0, bf_q = 0, bs_q = 0;
+    int bf = 0, bs = 0, bf_m = 0, bs_m = 0, bf_q = 0, bs_q = 0, bf_s = 0, bs_s = 0;
 };
 void tile_shapes(costa_dtype_t dtype, bool transposing_list, shape_dims* out);
 // Execution order of an op list: `ordered` = [sub-tiled ops | tiny ops] (tiny ops sorted by the
@@ -213,6 +215,7 @@ struct work_split {
     bool full = false;      // every large op of a transposing list is aligned and a whole number
                             // of large sub-tiles (the launch may then take fewer threads)
     bool med_full = false;  // the same for the medium ops and the medium sub-tile
+    bool med_sq = false;    // the medium class runs on 32 x 32 sub-tiles (bf_s x bs_s)
     int64_t n_items() const { return n_large + n_medium + n_tiny; }
 };
 // pack_list: the ops write the dense send package (their destinations are contiguous whatever

@@ -263,10 +263,12 @@ struct shape {
     static constexpr int CPP = NT / LPC;            // source columns per load pass
     static constexpr int PL = BS / CPP;             // load passes
     static constexpr int NW = NT / 64;              // wavefronts
-    static constexpr int UNITS = (BS / 64) * (BF / V);  // store units: 64 s x one f slot
+    static constexpr int SW = BS < 64 ? BS : 64;    // s values of one store unit per f slot
+    static constexpr int FW = 64 / SW;              // f slots of one store unit (a wavefront)
+    static constexpr int UNITS = (BS / SW) * (BF / V) / FW;  // store units: SW s x FW f slots
     static constexpr int PS = UNITS / NW;           // store passes
     static_assert(LPC <= NT && NT % LPC == 0 && BS % CPP == 0, "load mapping");
-    static_assert(BS % 64 == 0 && UNITS % NW == 0, "store mapping");
+    static_assert(BS % SW == 0 && SW % V == 0 && (BF / V) % FW == 0 && UNITS % NW == 0, "store mapping");
     static constexpr size_t lds_bytes = size_t(BS) * P * sizeof(T);
 };
 
@@ -331,6 +333,7 @@ template <> struct shapes<float> {
     static constexpr bool has_small = false;
     using large_tr_full = large_tr;
     using medium_tr_full = shape<float, 128, 64, 64>;
+    using small32_tr = shape<float, 128, 32, 32>;
 };
 template <> struct shapes<int> {
     using large = shape<int, COSTA_COPY_F_NT, COSTA_COPY_F_BF, COSTA_COPY_F_BS>;
@@ -341,6 +344,7 @@ template <> struct shapes<int> {
     static constexpr bool has_small = false;
     using large_tr_full = large_tr;
     using medium_tr_full = shape<int, 128, 64, 64>;
+    using small32_tr = shape<int, 128, 32, 32>;
 };
 // Copy lists of fp64 take 256 threads per 128 KiB sub-tile (each thread 32 16-byte loads in
 // flight, one workgroup per CU), c128 512 threads: BASELINE cfg 3's copy (32768^2 fp64, 128^2
@@ -361,6 +365,7 @@ template <> struct shapes<double> {
     static constexpr bool has_small = true;
     using large_tr_full = large_tr;
     using medium_tr_full = medium_tr;
+    using small32_tr = shape<double, 128, 32, 32>;
 };
 #ifndef COSTA_COPY_C_NT
 #define COSTA_COPY_C_NT 1024
@@ -385,6 +390,7 @@ template <> struct shapes<cpx<float>> {
     static constexpr bool has_small = COSTA_SQ_COMPLEX;
     using large_tr_full = large_tr;
     using medium_tr_full = medium_tr;
+    using small32_tr = shape<cpx<float>, 128, 32, 32>;
 };
 template <> struct shapes<cpx<double>> {
     using large = shape<cpx<double>, COSTA_COPY_Z_NT, 64, 128>;
@@ -395,6 +401,7 @@ template <> struct shapes<cpx<double>> {
     static constexpr bool has_small = COSTA_SQ_COMPLEX;
     using large_tr_full = shape<cpx<double>, 256, 64, 128>;
     using medium_tr_full = medium_tr;
+    using small32_tr = shape<cpx<double>, 128, 32, 32>;
 };
 
 // One sub-tile.  FULL: the sub-tile is a whole BF x BS block with 16-byte aligned rows on
@@ -458,15 +465,15 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
     // ---- transpose mode: dst(s, f) = g(src(f, s)) through LDS
     T* dst = reinterpret_cast<T*>(dst_base + op.dst) + int64_t(f0) * ldd + s0;
     const int lane = int(threadIdx.x) % 64, wave = int(threadIdx.x) / 64;
-    constexpr int FSLOTS = BF / V;
-    // store unit k of this lane: 64 s values x one f slot; after the lane exchange lane
-    // (base + j) stores f = q*V + j for s = sc*64 + base .. +V-1
+    constexpr int SW = S::SW, FW = S::FW, QG = BF / V / FW;  // QG: f-slot groups per s chunk
+    // store unit k of this lane: SW s values x FW f slots (64 x 1 for BS >= 64); after the lane
+    // exchange lane (base + j) stores f = q*V + j for s = sc*SW + base .. +V-1
     auto unit = [&](int k, int& f, int& sb, int& n) {
         const int u = wave + S::NW * k;
-        const int sc = u / FSLOTS, q = u % FSLOTS;
+        const int sc = u / QG, q = (u % QG) * FW + lane / SW;
         const int j = lane & (V - 1);
         f = q * V + j;
-        sb = sc * 64 + (lane - j);
+        sb = sc * SW + (lane % SW - j);
         n = FULL ? V : ts - sb;
         return FULL || (f < tf && n > 0);
     };
@@ -494,9 +501,9 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
     vec<T> y[S::PS];
 #pragma unroll
     for (int k = 0; k < S::PS; ++k) {
-        const int u = wave + S::NW * k;             // store unit: 64 s values x one f slot
-        const int sc = u / FSLOTS, q = u % FSLOTS;  // s chunk, f slot
-        const int s = sc * 64 + lane;
+        const int u = wave + S::NW * k;                         // store unit
+        const int sc = u / QG, q = (u % QG) * FW + lane / SW;   // s chunk, f slot
+        const int s = sc * SW + lane % SW;
         if (FULL || (s < ts && q * V < tf)) {
             raw16 r = *reinterpret_cast<const raw16*>(tile + s * P + q * V);
             __builtin_memcpy(&y[k], &r, 16);
@@ -797,7 +804,10 @@ void launch_t(const launch_args& a, hipStream_t stream) {
         launch_shape<T, typename shapes<T>::large_tr>(a, a.work, a.n_large, stream);
     else
         launch_shape<T, typename shapes<T>::large>(a, a.work, a.n_large, stream);
-    if (a.n_medium > 0) {
+    if (a.n_medium > 0 && a.med_sq) {  // the medium class on 32 x 32 sub-tiles (nb = 32 blocks)
+        if (!a.tr_shape) throw error(COSTA_ERR_INTERNAL, "costa: 32 x 32 shape");
+        launch_shape<T, typename shapes<T>::small32_tr>(a, a.work + a.n_large, a.n_medium, stream);
+    } else if (a.n_medium > 0) {
         if (!shapes<T>::has_medium || !a.tr_shape) throw error(COSTA_ERR_INTERNAL, "costa: medium shape");
         if (a.med_full && !a.any_axpby)  // every medium op a whole number of sub-tiles, C not read
             launch_shape<T, typename shapes<T>::medium_tr_full>(a, a.work + a.n_large, a.n_medium, stream);
@@ -817,6 +827,8 @@ void shape_of(bool tr, shape_dims* d) {
     const bool sq = tr && shapes<T>::has_small;
     d->bf_q = sq ? shapes<T>::small_tr::BF : 0;
     d->bs_q = sq ? shapes<T>::small_tr::BS : 0;
+    d->bf_s = tr ? shapes<T>::small32_tr::BF : 0;
+    d->bs_s = tr ? shapes<T>::small32_tr::BS : 0;
 }
 
 template <typename T, typename S>
@@ -833,6 +845,7 @@ void set_lds_limits() {
     set_lds_limit<T, typename shapes<T>::small_tr>();
     set_lds_limit<T, typename shapes<T>::large_tr_full>();
     set_lds_limit<T, typename shapes<T>::medium_tr_full>();
+    set_lds_limit<T, typename shapes<T>::small32_tr>();
 }
 
 }  // namespace

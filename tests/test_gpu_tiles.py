@@ -133,13 +133,16 @@ def test_mixed_tile_list(gpu, code, seed):
 
 
 @pytest.mark.parametrize("code,nb,full", [(0, 64, False), (1, 32, False), (1, 48, False), (4, 64, False),
-                                          (0, 80, False), (0, 64, True), (4, 64, True)],
-                         ids=["f32-64", "f64-32", "f64-48", "i32-64", "f32-80", "f32-64-full", "i32-64-full"])
+                                          (0, 80, False), (0, 64, True), (4, 64, True), (0, 32, False),
+                                          (2, 32, False), (3, 32, False), (4, 24, False)],
+                         ids=["f32-64", "f64-32", "f64-48", "i32-64", "f32-80", "f32-64-full", "i32-64-full",
+                              "f32-32", "c64-32", "c128-32", "i32-24"])
 def test_medium_shape_list(gpu, code, nb, full):
     """a transposing list of >= 4096 aligned ops between half a medium and half a large
     sub-tile (engine.cpp kMinMediumOps: the medium shape only runs for lists this long), with
     every scale kind and padded strides; full: every op a whole medium sub-tile (the
-    `medium_tr_full` launch); bit-exact against the oracle"""
+    `medium_tr_full` launch); nb <= 32: the medium class on 32 x 32 sub-tiles (`small32_tr`,
+    every type); bit-exact against the oracle"""
     rng = np.random.default_rng(77 + code + nb)
     dt = oracle.NP[code]
     E = np.dtype(dt).itemsize
