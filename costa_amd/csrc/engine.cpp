@@ -1456,8 +1456,10 @@ void transform(const std::vector<job>& jobs, comm* c, void* user_stream, bool as
     }
 
     if (async) {
-        HIP_CHECK(hipEventRecord(dc.ev_done, dc.main));
-        if (user) HIP_CHECK(hipStreamWaitEvent(user, dc.ev_done, 0));
+        if (user) {  // (no marker without a caller stream: each one widened the gap between calls)
+            HIP_CHECK(hipEventRecord(dc.ev_done, dc.main));
+            HIP_CHECK(hipStreamWaitEvent(user, dc.ev_done, 0));
+        }
         return;
     }
     HIP_CHECK(hipStreamSynchronize(dc.main));
