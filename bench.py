@@ -18,6 +18,12 @@ Workload (one "step" = one costa::transform over all local tiles, data already i
 Timing: W untimed steps; then barrier + device sync, K steps, device sync + barrier; max over
 ranks.  value = algorithmic bytes of all ranks / that time (read + write of every
 element moved, + read of C when beta != 0).  Rank 0 prints ONE JSON line.
+Launch: with N > 1 and no WORLD_SIZE in the environment, bench.py starts the N ranks itself as a
+child `torch.distributed.run` and relays rank 0's line and the exit code (launch_decision).
+Correctness: every element's value is a hash of its global position (pos_values); after the
+transform each rank compares 100 k random positions of its C with the value that position must
+hold (bit for bit; beta*C0 + alpha*op(A) rounded like the reference when beta != 0) and the
+mismatch counts are summed over the ranks -> "verified".
 
 roofline: the dominant kernel's algorithmic bytes per launch / its average duration from
 HIP events recorded on the stream it runs on (costa_hip_get_stats), against 8 TB/s.  Those
@@ -48,6 +54,163 @@ def grid_for(n: int):
     while n % pm:
         pm -= 1
     return pm, n // pm
+
+
+# ------------------------------------------------------------------ N-rank launch
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_decision(gpus: int, env, argv, port=None):
+    """How this process runs `bench.py --gpus N`.
+    -> ("self", None): this process is the bench (N = 1, or a rank started by a launcher);
+    -> ("spawn", cmd): start N ranks as a child `torch.distributed.run` (never an exec: the parent
+       has not touched the GPU and stays to relay rank 0's line and the exit code).
+    Raises SystemExit(2) when a launcher's WORLD_SIZE disagrees with --gpus."""
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            print(f"bench.py: WORLD_SIZE={ws} but --gpus {gpus}", file=sys.stderr)
+            raise SystemExit(2)
+        return "self", None
+    if gpus <= 1:
+        return "self", None
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={port if port else _free_port()}",
+           os.path.abspath(__file__)] + list(argv)
+    return "spawn", cmd
+
+
+def run_ranks(cmd) -> int:
+    """Run the N-rank child and relay its output: JSON lines (rank 0's result) to stdout,
+    everything else to stderr, as it arrives.  Returns the child's exit code."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                         env=env, bufsize=1)
+    for line in p.stdout:
+        if line.startswith("{"):
+            sys.stdout.write(line)
+            sys.stdout.flush()
+        else:
+            sys.stderr.write(line)
+    return p.wait()
+
+
+# ------------------------------------------------------------------ synthetic data
+# Every element's value is a hash of its GLOBAL position (row, col) and a seed: uniform on
+# +-[1, 2) with a 52-bit (fp64) / 23-bit (fp32) pseudo-random mantissa.  Any rank can then
+# compute the value any global element must hold after the transform, so the checks below sample
+# positions of the local C and compare bit for bit, without moving data between ranks.
+# Integer arithmetic only, below 2^63 at every step, so CPU and GPU agree exactly.
+_HP = 2147483647  # 2^31 - 1
+
+
+def pos_hash(i, j, seed: int):
+    """int64 tensors (broadcastable) -> int64 in [0, 2^31)"""
+    h = (i * 1000003 + j * 998244353 + (seed % _HP)) % _HP
+    h = (h * 48271) % _HP
+    h = h ^ (h >> 11)
+    return (h * 69621) % _HP
+
+
+def pos_values(i, j, seed: int, kind: str):
+    """the synthetic value of global element (i, j) for element kind 'f64' | 'f32' | 'c128'"""
+    import torch
+    if kind == "c128":
+        return torch.complex(pos_values(i, j, seed, "f64"), pos_values(i, j, seed + 7, "f64"))
+    h1 = pos_hash(i, j, seed)
+    h2 = pos_hash(i, j, seed + 1)
+    sign = 1.0 - 2.0 * (h2 & 1).to(torch.float64)
+    if kind == "f64":
+        mant = (h1 << 21) + (h2 >> 10)                           # < 2^52
+        return (1.0 + mant.to(torch.float64) * 2.0 ** -52) * sign  # exact
+    mant = h1 >> 8                                               # < 2^23
+    return ((1.0 + mant.to(torch.float64) * 2.0 ** -23) * sign).to(torch.float32)  # exact
+
+
+def bc_global(local, b: int, p: int, q: int):
+    """global index of local row (or column) `local` on process row (column) q of p, block b,
+    source process 0 (scalapack_layout.cpp:152-177 for ia = 1)"""
+    return (local // b * p + q) * b + local % b
+
+
+def fill_bc(t, lr: int, lc: int, b: int, pm: int, pr: int, pn: int, pc: int, seed: int,
+            kind: str, chunk_elems: int = 1 << 26):
+    """fill the column-major lr x lc local matrix `t` (flat, ld = lr) of a block-cyclic layout
+    with pos_values of its global positions, a column panel at a time"""
+    import torch
+    dev = t.device
+    gi = bc_global(torch.arange(lr, device=dev, dtype=torch.int64), b, pm, pr)
+    cols = max(1, chunk_elems // max(lr, 1))
+    for c0 in range(0, lc, cols):
+        c1 = min(lc, c0 + cols)
+        gj = bc_global(torch.arange(c0, c1, device=dev, dtype=torch.int64), b, pn, pc)
+        t[c0 * lr:c1 * lr] = pos_values(gi[None, :], gj[:, None], seed, kind).reshape(-1)
+
+
+class Arena:
+    """a rank's blocks of a custom layout stored one after another (bench cfg 5): maps arena
+    element indices to global (row, col)"""
+
+    def __init__(self, blocks, rs, cs, size, device):
+        import torch
+        self.size = size
+        off = [o for o, r, i, j in blocks]
+        self.off = torch.tensor(off + [size], dtype=torch.int64, device=device)
+        self.rows = torch.tensor([r for o, r, i, j in blocks] + [1], dtype=torch.int64, device=device)
+        self.cols = torch.tensor([cs[j + 1] - cs[j] for o, r, i, j in blocks] + [0],
+                                 dtype=torch.int64, device=device)
+        self.r0 = torch.tensor([rs[i] for o, r, i, j in blocks] + [0], dtype=torch.int64, device=device)
+        self.c0 = torch.tensor([cs[j] for o, r, i, j in blocks] + [0], dtype=torch.int64, device=device)
+
+    def global_of(self, e):
+        """-> (valid, gi, gj) for arena indices e (int64 tensor)"""
+        import torch
+        k = torch.searchsorted(self.off, e, right=True) - 1
+        o = e - self.off[k]
+        r, c = o % self.rows[k], o // self.rows[k]
+        return c < self.cols[k], self.r0[k] + r, self.c0[k] + c
+
+    def fill(self, t, seed, kind, chunk=1 << 26):
+        import torch
+        for e0 in range(0, self.size, chunk):
+            e = torch.arange(e0, min(self.size, e0 + chunk), device=t.device, dtype=torch.int64)
+            ok, gi, gj = self.global_of(e)
+            v = pos_values(gi, gj, seed, kind)
+            t[e0:e0 + e.numel()] = torch.where(ok, v, torch.zeros_like(v))
+
+
+def expected_axpby(al, be, c0, a):
+    """beta * c0 + alpha * a with the reference's roundings (no FMA): every product
+    and sum is its own torch op; complex products as (ac - bd, ad + bc)"""
+    import torch
+    if not torch.is_complex(a):
+        return (be * c0) + (al * a)
+    ar, ai, cr, ci = a.real, a.imag, c0.real, c0.imag
+    pr = (be.real * cr) - (be.imag * ci)
+    pi = (be.real * ci) + (be.imag * cr)
+    qr = (al.real * ar) - (al.imag * ai)
+    qi = (al.real * ai) + (al.imag * ar)
+    return torch.complex(pr + qr, pi + qi)
+
+
+def count_mismatch(got, exp) -> int:
+    """elements whose bit patterns differ"""
+    import torch
+    iv = {4: torch.int32, 8: torch.int64}
+    if torch.is_complex(got):
+        got, exp = torch.view_as_real(got), torch.view_as_real(exp)
+    g = got.contiguous().view(iv[got.element_size()])
+    e = exp.contiguous().view(iv[exp.element_size()])
+    return int((g != e).sum().item())
 
 
 def measured_traffic(alg_bytes: int):
@@ -204,10 +367,12 @@ def cfg5_workload(costa, torch, rank, world, op):
 
     ab, an = arena(ars, acs, aown)
     cb, cn = arena(crs, ccs, cown)
-    g = torch.Generator(device="cuda")
-    g.manual_seed(99 + rank)
-    A = torch.rand(an, dtype=torch.float32, device="cuda", generator=g)
-    C = torch.rand(cn, dtype=torch.float32, device="cuda", generator=g)
+    aa = Arena(ab, ars, acs, an, "cuda")
+    ca = Arena(cb, crs, ccs, cn, "cuda")
+    A = torch.empty(an, dtype=torch.float32, device="cuda")
+    C = torch.empty(cn, dtype=torch.float32, device="cuda")
+    aa.fill(A, SEED_A, "f32")
+    ca.fill(C, SEED_C, "f32")
     pa, pc = A.data_ptr(), C.data_ptr()
     LA = costa.custom_layout(len(ars) - 1, len(acs) - 1, ars, acs, aown,
                              [(pa + 4 * o, r, i, j) for o, r, i, j in ab], "C", costa.FLOAT)
@@ -225,7 +390,45 @@ def cfg5_workload(costa, torch, rank, world, op):
             m[o + r * (cs[j + 1] - cs[j])] -= 1
         return torch.from_numpy(np.cumsum(m[:size]) > 0).cuda()
     masks = (mask(ab, acs, an), mask(cb, ccs, cn))
-    return LA, LC, A, C, op, al, be, wl, masks
+    return LA, LC, A, C, op, al, be, wl, masks, ca
+
+
+SEED_A, SEED_C = 0xC057A0, 0xC057C0  # SURVEY §8d's seeds, here keys of the position hash
+N_SAMPLES = 100_000
+
+
+def mismatch_bc(Cm, lr_c, lc_c, b, cgrid, a_of, gen, axpby=False, al=1.0, be=0.0, kind="f64",
+                n=None):
+    """position check of a block-cyclic target (source process 0, 'C' storage, ld = lr_c): n
+    random local elements of C against the value their global position must hold, bit for bit
+    -> the number that differ.  cgrid = (p_rows, my_row, p_cols, my_col) of C's rank grid;
+    a_of(gi, gj) -> the (row, col) of A the element comes from; axpby: C held pos_values(SEED_C)
+    before the call, expect beta*C0 + alpha*A"""
+    import torch
+    pm_c, pr_c, pn_c, pc_c = cgrid
+    k = torch.randint(0, lr_c * lc_c, (n or N_SAMPLES,), device=Cm.device, generator=gen)
+    gi = bc_global(k % lr_c, b, pm_c, pr_c)
+    gj = bc_global(k // lr_c, b, pn_c, pc_c)
+    ai, aj = a_of(gi, gj)
+    exp = pos_values(ai, aj, SEED_A, kind)
+    if axpby:
+        exp = expected_axpby(al, be, pos_values(gi, gj, SEED_C, kind), exp)
+    return count_mismatch(Cm[k], exp)
+
+
+def mismatch_arena(Cm, ca, op, gen, C0=None, al=1.0, be=0.0, n=None):
+    """the same for a custom-layout arena (bench cfg 5, fp32): positions of the local C arena
+    (padding skipped); C0: C before the call when beta != 0"""
+    import torch
+    n = n or N_SAMPLES
+    e = torch.randint(0, ca.size, (2 * n,), device=Cm.device, generator=gen)
+    ok, gi, gj = ca.global_of(e)
+    e, gi, gj = e[ok][:n], gi[ok][:n], gj[ok][:n]
+    ai, aj = (gi, gj) if op == "N" else (gj, gi)
+    exp = pos_values(ai, aj, SEED_A, "f32")
+    if C0 is not None:
+        exp = expected_axpby(al, be, C0[e], exp)
+    return count_mismatch(Cm[e], exp)
 
 
 def main():
@@ -251,6 +454,17 @@ def main():
                          "'cfg3,cfg4:32768,cfg5:N' (rehearsal of the multi-GPU entries)")
     args = ap.parse_args()
 
+    # `bench.py --gpus N` with N > 1 and no launcher around it: start the N ranks as a child
+    # torch.distributed.run (before anything here touches the GPU), relay rank 0's line
+    how, cmd = launch_decision(args.gpus, os.environ, sys.argv[1:])
+    if how == "spawn":
+        import torch
+        have = torch.cuda.device_count()  # counts devices without initialising the GPU
+        if have < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but {have} GPU(s) visible", file=sys.stderr)
+            raise SystemExit(2)
+        raise SystemExit(run_ranks(cmd))
+
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -262,7 +476,11 @@ def main():
     import costa_amd as costa
 
     costa.lib()
-    device = local_rank % max(1, torch.cuda.device_count())
+    if torch.cuda.device_count() < world:
+        print(f"bench.py: {world} ranks but {torch.cuda.device_count()} GPU(s) visible",
+              file=sys.stderr)
+        raise SystemExit(2)
+    device = local_rank
     torch.cuda.set_device(device)
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -291,7 +509,8 @@ def main():
     # ---- workloads
     def checksum(t, mask=None):
         """order-independent checksum of a tensor's bit patterns (equal for any permutation of
-        the same elements), summed over the ranks"""
+        the same elements), summed over the ranks: cfg 5 'N''s bijection check, beside the
+        position samples"""
         x = t.view(torch.int32 if t.element_size() == 4 else torch.int64).reshape(-1)
         if mask is not None:
             x = x[mask]
@@ -301,18 +520,40 @@ def main():
             dist.all_reduce(v)
         return v.tolist()
 
+    def sum_over_ranks(x: int) -> int:
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.int64)
+        dist.all_reduce(t)
+        return int(t.item())
+
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(777 + rank)
+
+    def bc_check(Cm, lr_c, lc_c, b, cgrid, a_of, axpby=False, al=1.0, be=0.0, kind="f64"):
+        return lambda: sum_over_ranks(mismatch_bc(Cm, lr_c, lc_c, b, cgrid, a_of, gen, axpby,
+                                                  al, be, kind)) == 0
+
     def build(kind, edge=None):
-        """-> dict: layouts, tensors, op / alpha / beta, description, correctness check"""
+        """-> dict: layouts, tensors, op / alpha / beta, description, correctness check.
+        Data: pos_values of every element's global position (seeds SEED_A / SEED_C)"""
         n, b = args.edge, args.block
         pm, pn = grid_for(world)
+        pr, pc = rank // pn, rank % pn  # 'R' rank order on the pm x pn grid
         w = {"kind": kind, "check": None, "repeatable": True}
         if kind == "cfg5":
-            LA, LC, A, Cm, op, al, be, wl, masks = cfg5_workload(costa, torch, rank, world,
-                                                               args.cfg5_op if edge is None else edge)
-            w.update(LA=LA, LC=LC, A=A, C=Cm, op=op, al=al, be=be, wl=wl)
-            if op == "N":  # a bit permutation of A's block elements into C's blocks
-                ref = checksum(A, masks[0])
-                w["check"] = lambda: checksum(Cm, masks[1]) == ref
+            LA, LC, A, Cm, op, al, be, wl, masks, ca = cfg5_workload(
+                costa, torch, rank, world, args.cfg5_op if edge is None else edge)
+            w.update(LA=LA, LC=LC, A=A, C=Cm, op=op, al=al, be=be, wl=wl, repeatable=be == 0)
+            C0 = Cm.clone() if be != 0 else None
+            ref = checksum(A, masks[0]) if op == "N" else None
+
+            def check():
+                good = sum_over_ranks(mismatch_arena(Cm, ca, op, gen, C0, al, be)) == 0
+                if ref is not None:  # and a bit permutation of A's block elements into C's
+                    good = good and checksum(Cm, masks[1]) == ref
+                return good
+            w["check"] = check
             return w
         if kind == "cfg3":
             # BASELINE configs[2] (SURVEY §8d): pxgemr2d fp64 'N' (bit copy), 128^2 blocks, A on
@@ -322,9 +563,8 @@ def main():
             M, N = e3 * pm, e3 * pn
             lr_a, lc_a = M // pm, N // pn
             lr_c, lc_c = M // world, N
-            g = torch.Generator(device="cuda")
-            g.manual_seed(3333 + rank)
-            A = torch.rand(lr_a * lc_a, dtype=torch.float64, device="cuda", generator=g)
+            A = torch.empty(lr_a * lc_a, dtype=torch.float64, device="cuda")
+            fill_bc(A, lr_a, lc_a, b, pm, pr, pn, pc, SEED_A, "f64")
             Cm = torch.zeros(lr_c * lc_c, dtype=torch.float64, device="cuda")
             LA = costa.block_cyclic_layout(M, N, b, b, 1, 1, M, N, pm, pn, "R", 0, 0,
                                            A.data_ptr(), lr_a, "C", rank)
@@ -334,10 +574,10 @@ def main():
                   f"op N (BASELINE configs[2])" if world > 1 else
                   f"copy slice of BASELINE configs[2]: pxgemr2d fp64 {M}x{N}, 128x128 blocks on "
                   f"one rank (1x1 -> 1x1: every tile is a local bit copy, no remap)")
-            ref = checksum(A)
             w.update(LA=LA, LC=LC, A=A, C=Cm, op="N", al=1.0, be=0.0, wl=wl, grid=f"{pm}x{pn}",
                      m=M, n=N, block=b)
-            w["check"] = (lambda: torch.equal(Cm, A)) if world == 1 else (lambda: checksum(Cm) == ref)
+            sampled = bc_check(Cm, lr_c, lc_c, b, (world, rank, 1, 0), lambda i, j: (i, j))
+            w["check"] = (lambda: torch.equal(Cm, A) and sampled()) if world == 1 else sampled
             return w
         if kind == "cfg4":
             # BASELINE configs[3]: pztranu, c128, 128^2 blocks, alpha=(0.75,-0.5),
@@ -347,10 +587,10 @@ def main():
             M, N = (edge, edge) if edge else (n * pm, n * pn)
             lr_a, lc_a = M // pm, N // pn
             lr_c, lc_c = N // pm, M // pn
-            g = torch.Generator(device="cuda")
-            g.manual_seed(4321 + rank)
-            A = torch.rand(lr_a * lc_a, dtype=torch.complex128, device="cuda", generator=g)
-            Cm = torch.rand(lr_c * lc_c, dtype=torch.complex128, device="cuda", generator=g)
+            A = torch.empty(lr_a * lc_a, dtype=torch.complex128, device="cuda")
+            Cm = torch.empty(lr_c * lc_c, dtype=torch.complex128, device="cuda")
+            fill_bc(A, lr_a, lc_a, b, pm, pr, pn, pc, SEED_A, "c128")
+            fill_bc(Cm, lr_c, lc_c, b, pm, pr, pn, pc, SEED_C, "c128")
             LA = costa.block_cyclic_layout(M, N, b, b, 1, 1, M, N, pm, pn, "R", 0, 0,
                                            A.data_ptr(), lr_a, "C", rank, dtype=costa.CDOUBLE)
             LC = costa.block_cyclic_layout(N, M, b, b, 1, 1, N, M, pm, pn, "R", 0, 0,
@@ -362,24 +602,16 @@ def main():
                   f"{', weak-scaled 16384^2 per rank' if world > 1 and not edge else ''})")
             w.update(LA=LA, LC=LC, A=A, C=Cm, op="T", al=al, be=be, wl=wl, grid=f"{pm}x{pn}",
                      m=M, n=N, block=b, repeatable=False)
-            if world == 1:
-                C0 = Cm.clone()
-                nn = M
-
-                def check():  # after the first call only (beta != 0: every step changes C)
-                    k = torch.randint(0, nn * nn, (100000,), device="cuda")
-                    i, j = k % nn, k // nn  # C(i, j) at i + j*n; A(j, i) at j + i*n
-                    exp = be * C0[k] + al * A[j + i * nn]
-                    return bool(torch.allclose(Cm[k], exp, rtol=1e-13, atol=1e-13))
-                w["check"] = check
+            # after the first call only (beta != 0: every step changes C): C = beta*C0 + alpha*A^T
+            w["check"] = bc_check(Cm, lr_c, lc_c, b, (pm, pr, pn, pc), lambda i, j: (j, i),
+                                  axpby=True, al=al, be=be, kind="c128")
             return w
         # pxtran: BASELINE configs[1] at one rank, weak-scaled 16384^2 per rank beyond
         M, N = n * pm, n * pn  # A: M x N on pm x pn; C = A^T: N x M on the same rank grid
         lr_a, lc_a = M // pm, N // pn
         lr_c, lc_c = N // pm, M // pn
-        g = torch.Generator(device="cuda")
-        g.manual_seed(1234 + rank)
-        A = torch.rand(lr_a * lc_a, dtype=torch.float64, device="cuda", generator=g)
+        A = torch.empty(lr_a * lc_a, dtype=torch.float64, device="cuda")
+        fill_bc(A, lr_a, lc_a, b, pm, pr, pn, pc, SEED_A, "f64")
         Cm = torch.zeros(lr_c * lc_c, dtype=torch.float64, device="cuda")
         LA = costa.block_cyclic_layout(M, N, b, b, 1, 1, M, N, pm, pn, "R", 0, 0, A.data_ptr(),
                                        lr_a, "C", rank)
@@ -389,11 +621,11 @@ def main():
                "1x1 grid (BASELINE configs[1])") if world == 1 else
               (f"pxtran fp64 weak-scaled: {M}x{N} on a {pm}x{pn} rank grid "
                f"(16384^2 per rank), 256x256 blocks, op T, alpha=1 beta=0"))
-        ref = checksum(A)
         w.update(LA=LA, LC=LC, A=A, C=Cm, op="T", al=1.0, be=0.0, wl=wl, grid=f"{pm}x{pn}",
                  m=M, n=N, block=b)
-        w["check"] = ((lambda: torch.equal(Cm.view(n, n), A.view(n, n).t())) if world == 1
-                      else (lambda: checksum(Cm) == ref))
+        sampled = bc_check(Cm, lr_c, lc_c, b, (pm, pr, pn, pc), lambda i, j: (j, i))
+        w["check"] = ((lambda: torch.equal(Cm.view(n, n), A.view(n, n).t()) and sampled())
+                      if world == 1 else sampled)
         return w
 
     def measure(w, steps, warmup, planning_modes=False):
@@ -642,7 +874,8 @@ def main():
             "scaling": "strong" if args.workload == "cfg5" else "weak",
             "vs_baseline": None,
             "dtype": {"pxtran": "f64", "cfg3": "f64", "cfg4": "c128", "cfg5": "f32"}[args.workload],
-            "data": "synthetic (uniform random, device-resident)",
+            "data": ("synthetic, device-resident: every element a hash of its global (row, col), "
+                     "uniform on +-[1, 2); checks sample positions bit for bit"),
             "config": cfg,
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -115,10 +115,11 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
-    try:
-        import torch  # noqa: F401  (see docstring)
-    except Exception:  # pragma: no cover - torch absent is fine for pure C users
-        pass
+    if not os.environ.get("COSTA_NO_TORCH"):  # COSTA_NO_TORCH=1: the system HIP / RCCL only
+        try:                                      # (tests/rccl_system_child.py)
+            import torch  # noqa: F401  (see docstring)
+        except Exception:  # pragma: no cover - torch absent is fine for pure C users
+            pass
     if not os.path.exists(LIB_PATH):
         raise CostaError(-1, f"native library missing: {LIB_PATH} (run __graft_entry__.build())")
     L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
@@ -149,6 +150,7 @@ def lib():
                                                 vp, vp, vp]),
         "costa_hip_synchronize": (i, [vp]),
         "costa_hip_device_count": (i, [C.POINTER(i)]),
+        "costa_hip_rccl_version": (i, [C.POINTER(i)]),
         "costa_hip_copy_and_transform": (i, [i, i, i, vp, i, i, vp, i, i, i, i, vp, vp]),
         "costa_hip_execute_tiles": (i, [i, C.POINTER(TileOp), i64, vp, vp, vp, i, i]),
         "costa_hip_plan_export": (i, [i, C.POINTER(vp), C.POINTER(vp), C.c_char_p, vp, vp, i, i,
@@ -517,3 +519,11 @@ def set_planner(mode: int):
 def set_host_staging(mode: int):
     """Host-resident layouts: 1 = pipelined (default), 0 = mirror (costa_hip_set_host_staging)."""
     _check(lib().costa_hip_set_host_staging(int(mode)))
+
+
+def rccl_version() -> int:
+    """ncclGetVersion of the RCCL the exchange runs on in this process (major*10000 + minor*100 +
+    patch): torch's bundled librccl when torch was imported first, else /opt/rocm's."""
+    v = C.c_int(0)
+    _check(lib().costa_hip_rccl_version(C.byref(v)))
+    return v.value

@@ -166,6 +166,13 @@ int costa_hip_device_count(int* count) {
     });
 }
 
+int costa_hip_rccl_version(int* version) {
+    return guarded([&] {
+        if (!version) throw costa::engine::error(COSTA_ERR_ARG, "null argument");
+        *version = costa::engine::rccl_version();
+    });
+}
+
 int costa_hip_block_cyclic_layout(costa_dtype_t dtype, int m, int n, int block_m, int block_n,
                                   int i, int j, int sub_m, int sub_n, int p_m, int p_n,
                                   char rank_grid_ordering, int rsrc, int csrc, void* ptr, int lld,
@@ -221,9 +228,13 @@ int costa_hip_layout_reorder_ranks(costa_layout_t layout, const int* reordering,
         // and maps every owner through it (owner(), grid2D.hpp:183-187)
         if (n > 0 && n < n_base)
             throw costa::engine::error(COSTA_ERR_ARG, "costa: reordering shorter than the ranks");
-        for (int k = 0; k < n; ++k)
+        std::vector<char> seen(size_t(n), 0);
+        for (int k = 0; k < n; ++k) {
             if (reordering[k] < 0 || reordering[k] >= n)
                 throw costa::engine::error(COSTA_ERR_ARG, "costa: reordering out of range");
+            if (seen[size_t(reordering[k])]++)
+                throw costa::engine::error(COSTA_ERR_ARG, "costa: reordering is not a permutation");
+        }
         std::vector<int> owners(base.size());
         for (size_t k = 0; k < base.size(); ++k) owners[k] = n > 0 ? reordering[base[k]] : base[k];
         e.owners = std::move(owners);

@@ -162,6 +162,12 @@ int device_count() {
     return n;
 }
 
+int rccl_version() {
+    int v = 0;
+    NCCL_CHECK(ncclGetVersion(&v));
+    return v;
+}
+
 namespace {
 comm* new_comm(int device) {
     const int n = device_count();
@@ -213,15 +219,18 @@ int loopback_exchange() {
 }
 
 // Largest ncclSend / ncclRecv: 256 MiB by default (override COSTA_MAX_MSG_BYTES), never more
-// than 2^30 bytes.  A single self send/recv above 2^30 bytes delivered only its first half
-// (the failure starts exactly where the byte count crosses 2^30 and the lost part
-// is exactly the second of two halves, i.e. where twice the byte count passes INT32_MAX).
+// than kMaxMessageCap.  A single self send/recv above 2^30 bytes delivered only its first half
+// (the failure starts where twice the byte count passes INT32_MAX, and the lost
+// part is exactly the second of two halves); the last size measured intact was 2^30 - 233472
+// bytes, so the cap stays 1 MiB below 2^30 (exactly 2^30 is already on the failing side of
+// 2 * count > INT32_MAX).  tests/test_gpu_rccl_system.py moves a package in pieces of the cap.
+constexpr size_t kMaxMessageCap = (size_t(1) << 30) - (size_t(1) << 20);
 size_t max_message_bytes() {
     static const size_t v = [] {
         const char* s = std::getenv("COSTA_MAX_MSG_BYTES");  // tuning override
         const long long x = s ? std::atoll(s) : 0;
         const size_t want = x > 0 ? size_t(x) : (size_t(1) << 28);
-        return std::min(want, size_t(1) << 30);
+        return std::min(want, kMaxMessageCap);
     }();
     return v;
 }

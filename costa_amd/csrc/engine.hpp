@@ -128,6 +128,7 @@ uint32_t scale_kind(costa_dtype_t dtype, const scal& s, bool copy_mode, bool con
 
 // ---- executor (engine.cpp / tile_kernels.hip) ----
 int device_count();
+int rccl_version();  // ncclGetVersion of the RCCL this process loaded
 struct comm;
 struct comm* comm_self(int device);
 struct comm* comm_create(const unsigned char* id, int nranks, int rank, int device);

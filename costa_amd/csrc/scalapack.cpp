@@ -78,21 +78,66 @@ grid_info grid_of(int ctxt) {
 }
 
 // The processes of `ctxt`'s grid as one communicator, rank k = grid cell k (row-major); made
-// once per (context, process set) and kept (its RCCL communicator is cached on it).
+// once per process set and kept (its RCCL communicator is cached on it, costa/transform.hpp
+// comm_from_mpi).  BLACS reuses context handles after Cblacs_gridexit, and a reused handle may
+// name a grid of another system communicator with the same process numbers: a cached entry is
+// therefore reused only when its processes are exactly the grid's (MPI_Group_compare, local).
+// The cached communicators (and with them their RCCL communicators) are freed at the start of
+// MPI_Finalize, through an attribute of MPI_COMM_SELF (MPI-3.1 §8.7.1).
+struct comm_cache {
+    std::map<std::pair<int, std::vector<int>>, MPI_Comm> by_key;
+    std::vector<MPI_Comm> all;  // every communicator made, including replaced ones
+};
+
+comm_cache& cached_comms() {
+    static comm_cache c;
+    return c;
+}
+
+int free_cached_comms(MPI_Comm, int, void*, void*) {
+    comm_cache& c = cached_comms();
+    for (MPI_Comm& x : c.all) MPI_Comm_free(&x);
+    c.all.clear();
+    c.by_key.clear();
+    return MPI_SUCCESS;
+}
+
+void free_at_finalize() {
+    static bool done = false;
+    if (done) return;
+    int key = MPI_KEYVAL_INVALID;
+    MPI_Comm_create_keyval(MPI_COMM_NULL_COPY_FN, free_cached_comms, &key, nullptr);
+    MPI_Comm_set_attr(MPI_COMM_SELF, key, nullptr);
+    done = true;
+}
+
 MPI_Comm grid_comm(int ctxt, const grid_info& g) {
-    static std::map<std::pair<int, std::vector<int>>, MPI_Comm> cache;
+    comm_cache& cache = cached_comms();
     auto key = std::make_pair(ctxt, g.pnum);
-    auto it = cache.find(key);
-    if (it != cache.end()) return it->second;
-    MPI_Comm sys = sys_comm(ctxt), out = MPI_COMM_NULL;
+    MPI_Comm sys = sys_comm(ctxt);
     MPI_Group all, grp;
     MPI_Comm_group(sys, &all);
     MPI_Group_incl(all, int(g.pnum.size()), g.pnum.data(), &grp);
+    MPI_Group_free(&all);
+    auto it = cache.by_key.find(key);
+    if (it != cache.by_key.end()) {
+        MPI_Group have;
+        int same = MPI_UNEQUAL;
+        MPI_Comm_group(it->second, &have);
+        MPI_Group_compare(have, grp, &same);
+        MPI_Group_free(&have);
+        if (same == MPI_IDENT) {
+            MPI_Group_free(&grp);
+            return it->second;
+        }
+    }
+    MPI_Comm out = MPI_COMM_NULL;
     MPI_Comm_create_group(sys, grp, 0x6c0d, &out);
     MPI_Group_free(&grp);
-    MPI_Group_free(&all);
     if (out == MPI_COMM_NULL) throw std::runtime_error("could not make the context's communicator");
-    cache.emplace(std::move(key), out);
+    free_at_finalize();
+    cache.by_key[key] = out;
+    cache.all.push_back(out);
     return out;
 }
 
@@ -105,21 +150,26 @@ struct dist {
 };
 
 // Collective over `comm`: the processes inside each matrix's context describe it, the others
-// learn it from them.
+// learn it from them.  A process that finds a bad grid still joins the reduction (its error
+// flag is reduced with the descriptions), so every process of `comm` throws together instead of
+// one aborting while the others wait in the collective.
 std::vector<dist> distributions(MPI_Comm comm, const std::vector<const int*>& descs) {
     int P = 1;
     MPI_Comm_size(comm, &P);
     MPI_Group cg;
     MPI_Comm_group(comm, &cg);
     const size_t W = 8 + size_t(P);
-    std::vector<int> buf(W * descs.size(), -1);
+    std::vector<int> buf(W * descs.size() + 1, -1);  // + the error flag (1: too large, 2: outside)
     std::vector<int> mine(descs.size(), -1);
     for (size_t d = 0; d < descs.size(); ++d) {
         const int* desc = descs[d];
         const grid_info g = grid_of(desc[1]);
         if (!g.member()) continue;
         const int cells = g.pm * g.pn;
-        if (cells > P) throw std::runtime_error("a matrix's grid is larger than the call's context");
+        if (cells > P) {
+            buf.back() = std::max(buf.back(), 1);
+            continue;
+        }
         int* b = &buf[W * d];
         b[0] = g.pm;
         b[1] = g.pn;
@@ -129,12 +179,14 @@ std::vector<dist> distributions(MPI_Comm comm, const std::vector<const int*>& de
         MPI_Group_translate_ranks(sg, cells, g.pnum.data(), cg, b + 8);
         MPI_Group_free(&sg);
         for (int k = 0; k < cells; ++k)
-            if (b[8 + k] == MPI_UNDEFINED || b[8 + k] < 0)
-                throw std::runtime_error("a process of the matrix's grid is outside the call's context");
+            if (b[8 + k] == MPI_UNDEFINED || b[8 + k] < 0) buf.back() = std::max(buf.back(), 2);
         mine[d] = g.myr * g.pn + g.myc;
     }
     MPI_Group_free(&cg);
     MPI_Allreduce(MPI_IN_PLACE, buf.data(), int(buf.size()), MPI_INT, MPI_MAX, comm);
+    if (buf.back() == 1) throw std::runtime_error("a matrix's grid is larger than the call's context");
+    if (buf.back() == 2)
+        throw std::runtime_error("a process of the matrix's grid is outside the call's context");
     std::vector<dist> out(descs.size());
     for (size_t d = 0; d < descs.size(); ++d) {
         const int* b = &buf[W * d];

@@ -120,13 +120,18 @@ class assigned_grid2D {
         return reordered_rank(owners_[size_t(r) * size_t(stored_cols) + size_t(c)]);
     }
     // rank relabelling (reference grid2D.hpp:75-79, 219-233): rank k of the grid becomes
-    // reordering[k] (costa::optimal_reordering proposes one)
+    // reordering[k], a permutation (costa::optimal_reordering proposes one); the process of rank
+    // r then holds the blocks of the rank k with reordering[k] == r (costa_hip.h)
     void reorder_ranks(const std::vector<int>& reordering) {
         if (!reordering.empty() && int(reordering.size()) < n_ranks_)
             throw std::runtime_error("costa::assigned_grid2D: reordering shorter than the ranks");
-        for (int k : reordering)
-            if (k < 0 || k >= std::max(n_ranks_, int(reordering.size())))
+        std::vector<char> seen(reordering.size(), 0);
+        for (int k : reordering) {
+            if (k < 0 || k >= int(reordering.size()))
                 throw std::runtime_error("costa::assigned_grid2D: reordering out of range");
+            if (seen[size_t(k)]++)
+                throw std::runtime_error("costa::assigned_grid2D: reordering is not a permutation");
+        }
         reordering_ = reordering;
     }
     int reordered_rank(int rank) const {

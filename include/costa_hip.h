@@ -110,6 +110,10 @@ typedef struct {
 const char* costa_hip_last_error(void);
 int costa_hip_version(void); /* major*10000 + minor*100 + patch */
 int costa_hip_device_count(int* count); /* visible GPUs (COSTA_ERR_HIP without a GPU) */
+/* the RCCL library the exchange runs on in this process (ncclGetVersion: major*10000 +
+ * minor*100 + patch); which one the loader bound depends on what the process loaded first
+ * (torch ships its own librccl under the same soname) */
+int costa_hip_rccl_version(int* version);
 
 /* ---- layouts (pointers may be host or device memory; never dereferenced
  *      until a transform runs) ---- */
@@ -123,10 +127,13 @@ int costa_hip_custom_layout(costa_dtype_t dtype, int rowblocks, int colblocks, c
 void costa_hip_layout_destroy(costa_layout_t layout);
 /* rank relabelling: owner(i, j) becomes reordering[owner(i, j)] (replaces any earlier one;
  * n = 0 restores the identity).  Replaces grid_layout<T>::reorder_ranks
- * (src/costa/grid2grid/grid_layout.hpp:32-34, grid2D.hpp:183-187, 219-221); the permutation
- * usually comes from costa::optimal_reordering (<costa/grid2grid/ranks_reordering.hpp>).  As in
- * the reference's README (README.md:343-362), rank r's relabelled target layout holds the local
- * blocks of rank reordering[r]. */
+ * (src/costa/grid2grid/grid_layout.hpp:32-34, grid2D.hpp:183-187, 219-221).  `reordering` must
+ * be a permutation of 0..n-1 (COSTA_ERR_ARG otherwise) with n >= the layout's ranks.  A cell of
+ * base owner o then belongs to rank reordering[o], so the process of rank r must hold the local
+ * blocks of base rank o with reordering[o] == r (the inverse permutation at r).  The
+ * permutations costa::optimal_reordering proposes (<costa/grid2grid/ranks_reordering.hpp>) swap
+ * pairs of ranks, i.e. are their own inverse: then rank r holds the blocks of rank
+ * reordering[r], as the reference's README puts it (README.md:343-362). */
 int costa_hip_layout_reorder_ranks(costa_layout_t layout, const int* reordering, int n);
 /* number of local blocks / the i-th block (global intervals, data pointer, ld) */
 int costa_hip_layout_num_blocks(costa_layout_t layout);

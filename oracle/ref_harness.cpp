@@ -158,9 +158,10 @@ int run_case(std::istream& in, const std::string& out, int rank, int P) {
         double ar, ai, br, bi;
         in >> tok >> trans[size_t(p)] >> tok >> ar >> ai >> tok >> br >> bi >> tok >>
             noscale[size_t(p)] >> tok >> seedA[size_t(p)] >> tok >> seedC[size_t(p)];
-        // optional "relabelC k p0 .. p(k-1)": the target layout of rank r holds the local
-        // blocks of rank p[r] and its grid is relabelled by reorder_ranks(p) (README.md:343-362,
-        // grid_layout.hpp:32-34)
+        // optional "relabelC k p0 .. p(k-1)": the target grid is relabelled by reorder_ranks(p)
+        // (grid_layout.hpp:32-34, grid2D.hpp:219-229: a cell of base owner o belongs to rank
+        // p[o]), so the target layout of rank r holds the local blocks of base rank p^-1[r]
+        // (README.md:343-362 states it for the pair swaps optimal_reordering proposes: p^-1 = p)
         in >> std::ws;
         if (in.peek() == 'r') {
             int k;
@@ -187,7 +188,9 @@ int run_case(std::istream& in, const std::string& out, int rank, int P) {
         auto& a = abuf[size_t(p)];
         auto& c = cbuf[size_t(p)];
         auto& rl = relabel[size_t(p)];
-        const int crank = rl.empty() ? rank : rl[size_t(rank)];
+        int crank = rank;
+        for (size_t q = 0; q < rl.size(); ++q)
+            if (rl[q] == rank) crank = int(q);
         a.resize(size_t(buf_size(A[size_t(p)], rank)));
         c.resize(size_t(buf_size(C[size_t(p)], crank)));
         for (size_t k = 0; k < a.size(); ++k) a[k] = gen<T>(seedA[size_t(p)], rank, k);

@@ -187,12 +187,16 @@ class Pair:
     noscale: bool = False  # use the no-scale overload transform(A, C, comm)
     seedA: int = 0xC057A0
     seedC: int = 0xC057C0
-    # rank relabelling of the target layout (README.md:343-362): rank r's C layout holds the
-    # local blocks of rank relabel[r] and is relabelled by reorder_ranks(relabel)
+    # rank relabelling of the target layout (README.md:343-362, grid2D.hpp:219-229): the C
+    # layout is relabelled by reorder_ranks(relabel), so a cell of base owner o belongs to rank
+    # relabel[o] and rank r holds the local blocks of base rank relabel^-1[r] (= relabel[r]
+    # for the pair swaps optimal_reordering proposes)
     relabel: list | None = None
 
     def c_rank(self, rank):
-        return rank if self.relabel is None else int(self.relabel[rank])
+        if self.relabel is None:
+            return rank
+        return int(np.argsort(np.asarray(self.relabel))[rank])
 
 
 @dataclass

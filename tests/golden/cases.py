@@ -165,7 +165,7 @@ def _split(n, b):
 def _relabelled():
     """Targets relabelled by involutions of the kind optimal_reordering proposes (pairs of ranks
     swapped; relabel_readme uses the reference's own proposal for that geometry,
-    tests/golden/relabel.json)."""
+    tests/golden/relabel.json), and one by a 3-cycle."""
     cases = []
     # README.md:461-470 geometry (2x4 'R' -> 4x2 'C' ranks), scaled to 1000^2 / 100^2 blocks
     cases.append(Case("relabel_readme", D, [Pair(
@@ -188,6 +188,11 @@ def _relabelled():
     c_rs, c_cs = _edges(0x73, m, 20, 120), _edges(0x74, n, 20, 120)
     ao = np.random.default_rng(0x75).integers(0, 5, (len(a_rs) - 1, len(a_cs) - 1))
     co = np.random.default_rng(0x76).integers(0, 5, (len(c_rs) - 1, len(c_cs) - 1))
+    # a relabelling that is not its own inverse (a 3-cycle and a fixed point): rank r holds the
+    # blocks of base rank relabel^-1[r]
+    cases.append(Case("relabel_cycle3", D, [Pair(
+        BC(300, 260, 32, 24, pm=2, pn=2, order="R"), BC(260, 300, 20, 28, pm=4, pn=1, order="R"),
+        "T", 0.75, -1.5, seedA=0x79, seedC=0x7A, relabel=[1, 2, 0, 3])], P=4))
     cases.append(Case("relabel_custom_T", CF, [Pair(
         Custom(a_rs, a_cs, ao, ord="R"), Custom(c_rs, c_cs, co, ord="C"), "T",
         0.75 - 0.5j, 1.25 + 0.25j, seedA=0x77, seedC=0x78, relabel=[0, 3, 4, 1, 2])], P=5))

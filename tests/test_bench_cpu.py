@@ -1,0 +1,194 @@
+"""bench.py's host logic on the CPU: the N-rank launch decision, the position-hash data and the
+position-dependent correctness checks of the N > 1 entries (checksums could not see
+misplaced tiles).
+
+The checks run end to end on 2 and 4 gloo ranks with the product planner and the oracle
+executor (as test_multirank_gloo.py): a correct transform passes, one with two tiles swapped
+or one rank's result left out fails.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def test_launch_decision():
+    env = {}
+    assert bench.launch_decision(1, env, ["--gpus", "1"]) == ("self", None)
+    how, cmd = bench.launch_decision(4, env, ["--gpus", "4", "--steps", "5"], port=29555)
+    assert how == "spawn"
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "--nnodes=1" in cmd
+    assert "--master-addr=127.0.0.1" in cmd and "--master-port=29555" in cmd
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "5"]
+    assert cmd[-5] == os.path.join(ROOT, "bench.py")
+    # a rank started by a launcher runs itself; a WORLD_SIZE that disagrees with --gpus is an error
+    assert bench.launch_decision(4, {"WORLD_SIZE": "4"}, []) == ("self", None)
+    with pytest.raises(SystemExit) as e:
+        bench.launch_decision(4, {"WORLD_SIZE": "2"}, [])
+    assert e.value.code == 2
+
+
+def test_run_ranks_relays_json_and_rc():
+    code = "import sys; print('noise'); print('{\"value\": 1}'); sys.exit(3)"
+    r = subprocess.run([sys.executable, "-c",
+                        f"import bench; raise SystemExit(bench.run_ranks([{sys.executable!r}, '-c', {code!r}]))"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 3
+    assert r.stdout.strip() == '{"value": 1}'
+    assert "noise" in r.stderr
+
+
+def test_gpus_n_without_gpus_exits_nonzero():
+    """no GPU here: the parent counts devices (no GPU initialisation) and refuses"""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 2, r.stderr
+    assert "GPU(s) visible" in r.stderr
+
+
+def test_pos_values_exact_and_spread():
+    i = torch.arange(0, 4096, dtype=torch.int64)
+    j = torch.arange(0, 4096, dtype=torch.int64).flip(0)
+    for kind, bits in (("f64", 52), ("f32", 23)):
+        v = bench.pos_values(i, j, bench.SEED_A, kind)
+        a = v.abs().double()
+        assert bool(((a >= 1) & (a < 2)).all())
+        assert len(set(v.tolist())) > 4000  # distinct per position
+        # transposed positions differ (a transpose bug is visible)
+        assert bool((bench.pos_values(j, i, bench.SEED_A, kind) != v).any())
+    z = bench.pos_values(i, j, bench.SEED_C, "c128")
+    assert z.dtype == torch.complex128 and bool((z.real != z.imag).all())
+
+
+def test_bc_global_matches_oracle_geometry():
+    """bc_global(local) agrees with the reference geometry restated by the oracle"""
+    import oracle
+    M, N, b, pm, pn = 100, 70, 8, 3, 2
+    lld = oracle.numroc(M, b, 0, 0, pm)
+    rs, cs, tab = oracle.bc_table(M, N, b, b, 1, 1, M, N, pm, pn, "R", 0, 0, lld, "C")
+    tab = tab.reshape(len(rs) - 1, len(cs) - 1, 3)
+    for bi in range(len(rs) - 1):
+        for bj in range(len(cs) - 1):
+            owner, off, ld = (int(x) for x in tab[bi, bj])
+            pr, pc = owner // pn, owner % pn
+            li, lj = off % ld, off // ld  # local position of the block's first element
+            gi = bench.bc_global(torch.tensor(li), b, pm, pr)
+            gj = bench.bc_global(torch.tensor(lj), b, pn, pc)
+            assert (int(gi), int(gj)) == (rs[bi], cs[bj])
+
+
+def test_arena_global_of():
+    rs, cs = [0, 3, 8], [0, 2, 7]
+    blocks, off = [], 0
+    for i in range(2):
+        for j in range(2):
+            rows, cols = rs[i + 1] - rs[i], cs[j + 1] - cs[j]
+            blocks.append((off, rows, i, j))
+            off += (rows * cols + 3) // 4 * 4
+    ar = bench.Arena(blocks, rs, cs, off, "cpu")
+    ok, gi, gj = ar.global_of(torch.arange(off, dtype=torch.int64))
+    want = {}
+    for o, rows, i, j in blocks:
+        for c in range(cs[j + 1] - cs[j]):
+            for r in range(rows):
+                want[o + r + c * rows] = (rs[i] + r, cs[j] + c)
+    for e in range(off):
+        if e in want:
+            assert bool(ok[e]) and (int(gi[e]), int(gj[e])) == want[e]
+        else:
+            assert not bool(ok[e])
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, kind, corrupt, out_dir):
+    sys.path.insert(0, ROOT)
+    import bench as B
+    import costa_amd as costa
+    import oracle
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n, b = 48, 8
+    pm, pn = B.grid_for(world)
+    pr, pc = rank // pn, rank % pn
+    M, N = n * pm, n * pn
+    if kind == "pxtran":  # C = A^T, fp64 bit copies
+        tdt, code, kk, al, be, op = torch.float64, costa.DOUBLE, "f64", 1.0, 0.0, "T"
+    else:  # cfg4-like: c128 'T' with alpha, beta
+        tdt, code, kk, al, be, op = (torch.complex128, costa.CDOUBLE, "c128", complex(0.75, -0.5),
+                                     complex(1.25, 0.25), "T")
+    lr_c, lc_c = N // pm, M // pn  # C = op(A) is N x M on the same rank grid
+    A = torch.empty(n * n, dtype=tdt)
+    Cm = torch.empty(lr_c * lc_c, dtype=tdt)
+    B.fill_bc(A, n, n, b, pm, pr, pn, pc, B.SEED_A, kk, chunk_elems=500)
+    if be != 0:
+        B.fill_bc(Cm, lr_c, lc_c, b, pm, pr, pn, pc, B.SEED_C, kk)
+    else:
+        Cm.zero_()
+    LA = costa.block_cyclic_layout(M, N, b, b, 1, 1, M, N, pm, pn, "R", 0, 0, A.data_ptr(), n,
+                                   "C", rank, dtype=code)
+    LC = costa.block_cyclic_layout(N, M, b, b, 1, 1, N, M, pm, pn, "R", 0, 0, Cm.data_ptr(),
+                                   lr_c, "C", rank, dtype=code)
+    plan = costa.plan_export([LA], [LC], rank, world, [op], [al], [be])
+    dt = oracle.NP[code]
+    E = np.dtype(dt).itemsize
+    send = np.zeros(max(1, plan.send_elems), dt)
+    recv = np.zeros(max(1, plan.recv_elems), dt)
+    oracle.exec_tile_ops(code, plan.pack_ops, plan.scalars, 0, send.ctypes.data)
+    st, rt = torch.from_numpy(send.view(np.uint8)), torch.from_numpy(recv.view(np.uint8))
+    sc = [int(x) * E for x in plan.send_counts]
+    rc = [int(x) * E for x in plan.recv_counts]
+    dist.all_to_all_single(rt[:sum(rc)], st[:sum(sc)], rc, sc)
+    if not (corrupt == "drop" and rank == 1):  # rank 1 receives on every grid here
+        oracle.exec_tile_ops(code, plan.unpack_ops, plan.scalars, recv.ctypes.data, 0)
+    oracle.exec_tile_ops(code, plan.local_ops, plan.scalars, 0, 0)
+    if corrupt == "swap" and rank == 0:  # two b x b tiles of C swapped
+        c2 = Cm.view(lc_c, lr_c)  # [col][row]
+        t = c2[0:b, 0:b].clone()
+        c2[0:b, 0:b] = c2[b:2 * b, b:2 * b]
+        c2[b:2 * b, b:2 * b] = t
+    g = torch.Generator()
+    g.manual_seed(rank)
+    bad = B.mismatch_bc(Cm, lr_c, lc_c, b, (pm, pr, pn, pc), lambda i, j: (j, i), g, axpby=be != 0,
+                        al=al, be=be, kind=kk, n=4000)
+    t = torch.tensor([bad], dtype=torch.int64)
+    dist.all_reduce(t)
+    with open(os.path.join(out_dir, f"r{rank}.txt"), "w") as f:
+        f.write(str(int(t.item())))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,kind", [(2, "pxtran"), (4, "pxtran"), (4, "cfg4")])
+@pytest.mark.parametrize("corrupt", [None, "swap", "drop"])
+def test_position_check_multirank(tmp_path, world, kind, corrupt):
+    mp.spawn(_worker, args=(world, _free_port(), kind, corrupt, str(tmp_path)), nprocs=world,
+             join=True)
+    total = {int((tmp_path / f"r{r}.txt").read_text()) for r in range(world)}
+    assert len(total) == 1
+    total = total.pop()
+    if corrupt is None:
+        assert total == 0, f"{total} sampled positions differ on a correct transform"
+    else:
+        assert total > 0, f"the position check missed a {corrupt} error"
