@@ -48,14 +48,55 @@ template <typename T> __device__ __forceinline__ T e_add(T a, T b) { return a + 
 template <typename T> __device__ __forceinline__ T e_conj(T a) { return a; }
 template <typename T> __device__ __forceinline__ T e_zero() { return T(0); }
 
-// (a.re + i a.im)(b.re + i b.im) = (a.re b.re - a.im b.im) + i (a.re b.im + a.im b.re):
-// libstdc++/GCC's complex product for finite operands (4 products, 2 sums, no fma)
-template <> __device__ __forceinline__ cpx<float> e_mul(cpx<float> a, cpx<float> b) {
-    return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
+// (a + i b)(c + i d): the reference's std::complex product as GCC compiles it (C99 Annex G):
+// the naive (ac - bd, ad + bc) -- 4 products, 2 sums, no fma -- and, only when BOTH parts come
+// out NaN, libgcc's __muldc3 / __mulsc3 recovery of infinities (GCC 11.4 libgcc2.c; restated in
+// oracle/costa_oracle.c ANNEX_G_MUL and pinned to GCC there): an infinite factor is "boxed" to
+// +-1 / +-0 with the other factor's NaNs zeroed, or, when a partial product overflowed, every
+// NaN is zeroed; then the product is recomputed and scaled by infinity.  The branch is never
+// taken on finite data: (inf + inf i)(1 + 0i) = inf + inf i, not NaN + NaN i.
+// (the partial products are recomputed inside the rare branch rather than kept live: fewer
+// registers on the common path)
+template <typename R>
+__device__ __attribute__((cold)) cpx<R> annex_g_recover(R a, R b, R c, R d) {
+    const R one = R(1), zero = R(0), inf = __builtin_huge_val();
+    const bool ovf = __builtin_isinf(a * c) || __builtin_isinf(b * d) || __builtin_isinf(a * d) ||
+                     __builtin_isinf(b * c);
+    bool recalc = false;
+    if (__builtin_isinf(a) || __builtin_isinf(b)) {
+        a = __builtin_copysign(__builtin_isinf(a) ? one : zero, a);
+        b = __builtin_copysign(__builtin_isinf(b) ? one : zero, b);
+        if (__builtin_isnan(c)) c = __builtin_copysign(zero, c);
+        if (__builtin_isnan(d)) d = __builtin_copysign(zero, d);
+        recalc = true;
+    }
+    if (__builtin_isinf(c) || __builtin_isinf(d)) {
+        c = __builtin_copysign(__builtin_isinf(c) ? one : zero, c);
+        d = __builtin_copysign(__builtin_isinf(d) ? one : zero, d);
+        if (__builtin_isnan(a)) a = __builtin_copysign(zero, a);
+        if (__builtin_isnan(b)) b = __builtin_copysign(zero, b);
+        recalc = true;
+    }
+    if (!recalc && ovf) {
+        if (__builtin_isnan(a)) a = __builtin_copysign(zero, a);
+        if (__builtin_isnan(b)) b = __builtin_copysign(zero, b);
+        if (__builtin_isnan(c)) c = __builtin_copysign(zero, c);
+        if (__builtin_isnan(d)) d = __builtin_copysign(zero, d);
+        recalc = true;
+    }
+    const R p = a * c, q = b * d, r = a * d, t = b * c;
+    if (!recalc) return {p - q, r + t};
+    return {inf * (p - q), inf * (r + t)};
 }
-template <> __device__ __forceinline__ cpx<double> e_mul(cpx<double> a, cpx<double> b) {
-    return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
+template <typename R>
+__device__ __forceinline__ cpx<R> cmul(cpx<R> z, cpx<R> w) {
+    const R x = z.re * w.re - z.im * w.im, y = z.re * w.im + z.im * w.re;
+    if (__builtin_expect(__builtin_isnan(x) && __builtin_isnan(y), 0))
+        return annex_g_recover(z.re, z.im, w.re, w.im);
+    return {x, y};
 }
+template <> __device__ __forceinline__ cpx<float> e_mul(cpx<float> a, cpx<float> b) { return cmul(a, b); }
+template <> __device__ __forceinline__ cpx<double> e_mul(cpx<double> a, cpx<double> b) { return cmul(a, b); }
 template <> __device__ __forceinline__ cpx<float> e_add(cpx<float> a, cpx<float> b) {
     return {a.re + b.re, a.im + b.im};
 }
@@ -74,6 +115,29 @@ __device__ __forceinline__ T scale(T x, T y, uint32_t kind, bool conj, T alpha, 
     if (kind == COSTA_SCALE_ZERO) return e_zero<T>();
     if (kind == COSTA_SCALE_ALPHA) return e_mul(alpha, x);
     if (kind == COSTA_SCALE_AXPBY) return e_add(e_mul(beta, y), e_mul(alpha, x));
+    return x;  // BITCOPY
+}
+
+// The same with the naive complex product only: `bad` is set when a product needs the Annex G
+// recovery (both parts NaN), and the caller then redoes that vector with scale() out of the
+// hot loop (run_tile): the recovery code stays off the register-hungry large shapes' main path
+// (inlined per element it made the 1024-thread c64 shape spill to scratch).
+template <typename T> struct is_cpx { static constexpr bool value = false; };
+template <typename R> struct is_cpx<cpx<R>> { static constexpr bool value = true; };
+template <typename T> __device__ __forceinline__ T e_mul_naive(T a, T b, bool&) { return a * b; }
+template <typename R>
+__device__ __forceinline__ cpx<R> e_mul_naive(cpx<R> z, cpx<R> w, bool& bad) {
+    const R x = z.re * w.re - z.im * w.im, y = z.re * w.im + z.im * w.re;
+    bad = bad || (__builtin_isnan(x) && __builtin_isnan(y));
+    return {x, y};
+}
+template <typename T>
+__device__ __forceinline__ T scale_naive(T x, T y, uint32_t kind, bool conj, T alpha, T beta,
+                                         bool& bad) {
+    if (conj) x = e_conj(x);
+    if (kind == COSTA_SCALE_ZERO) return e_zero<T>();
+    if (kind == COSTA_SCALE_ALPHA) return e_mul_naive(alpha, x, bad);
+    if (kind == COSTA_SCALE_AXPBY) return e_add(e_mul_naive(beta, y, bad), e_mul_naive(alpha, x, bad));
     return x;  // BITCOPY
 }
 
@@ -446,18 +510,43 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
                 if (FULL || (nf_lane > 0 && s < ts)) vload(y[k], dst + s * ldd + lf, nf_lane, vd);
             }
         }
+        uint32_t redo = 0;  // complex vectors left for the Annex G path (bit k: strip k)
 #pragma unroll
         for (int k = 0; k < S::PL; ++k) {
             const int s = c0 + k * S::CPP;
             if (!FULL && (nf_lane <= 0 || s >= ts)) continue;
             T* d = dst + s * ldd + lf;
             if (kind != COSTA_SCALE_BITCOPY) {
+                bool bad = false;
 #pragma unroll
                 for (int e = 0; e < V; ++e)
-                    x[k].e[e] = scale(x[k].e[e], kind == COSTA_SCALE_AXPBY ? y[k].e[e] : e_zero<T>(),
-                                      kind, conj, alpha, beta);
+                    x[k].e[e] = scale_naive(x[k].e[e], kind == COSTA_SCALE_AXPBY ? y[k].e[e] : e_zero<T>(),
+                                            kind, conj, alpha, beta, bad);
+                if (is_cpx<T>::value && bad) {
+                    redo |= 1u << k;
+                    continue;
+                }
             }
             vstore(d, x[k], nf_lane, vd);
+        }
+        if constexpr (is_cpx<T>::value) {
+            static_assert(S::PL <= 32, "redo mask");
+            // strips whose naive products needed the recovery: source and (not yet written)
+            // destination are read again and every element goes through scale()
+            if (__builtin_expect(redo != 0, 0)) {
+#pragma unroll 1
+                for (int k = 0; k < S::PL; ++k) {
+                    if (!((redo >> k) & 1u)) continue;
+                    const int s = c0 + k * S::CPP;
+                    const T* a = src + s * lds + lf;
+                    T* d = dst + s * ldd + lf;
+                    const int n = FULL ? V : min(V, nf_lane);
+#pragma unroll 1
+                    for (int e = 0; e < n; ++e)
+                        d[e] = scale(a[e], kind == COSTA_SCALE_AXPBY ? d[e] : e_zero<T>(), kind, conj,
+                                     alpha, beta);
+                }
+            }
         }
         return;
     }
@@ -509,6 +598,7 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
             __builtin_memcpy(&y[k], &r, 16);
         }
     }
+    uint32_t redo = 0;  // complex store units left for the Annex G path (bit k: unit k)
 #pragma unroll
     for (int k = 0; k < S::PS; ++k) {
         vec<T> o = lane_transpose(y[k], lane);
@@ -516,12 +606,37 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
         if (!unit(k, f, sb, n)) continue;
         T* d = dst + f * ldd + sb;
         if (kind != COSTA_SCALE_BITCOPY) {
+            bool bad = false;
 #pragma unroll
             for (int e = 0; e < V; ++e)
-                o.e[e] = scale(o.e[e], kind == COSTA_SCALE_AXPBY ? old[k].e[e] : e_zero<T>(), kind,
-                               conj, alpha, beta);
+                o.e[e] = scale_naive(o.e[e], kind == COSTA_SCALE_AXPBY ? old[k].e[e] : e_zero<T>(),
+                                     kind, conj, alpha, beta, bad);
+            if (is_cpx<T>::value && bad) {
+                redo |= 1u << k;
+                continue;
+            }
         }
         vstore(d, o, n, vd);
+    }
+    if constexpr (is_cpx<T>::value) {
+        static_assert(S::PS <= 32, "redo mask");
+        // units whose naive products needed the recovery: element e of the unit is source row
+        // sb + e, column f of the staged tile (read straight from LDS: no lane exchange with
+        // part of the wavefront inactive), its old value is still in the destination
+        if (__builtin_expect(redo != 0, 0)) {
+#pragma unroll 1
+            for (int k = 0; k < S::PS; ++k) {
+                if (!((redo >> k) & 1u)) continue;
+                int f, sb, n;
+                unit(k, f, sb, n);
+                T* d = dst + f * ldd + sb;
+                n = FULL ? V : min(V, n);
+#pragma unroll 1
+                for (int e = 0; e < n; ++e)
+                    d[e] = scale(tile[(sb + e) * P + f], kind == COSTA_SCALE_AXPBY ? d[e] : e_zero<T>(),
+                                 kind, conj, alpha, beta);
+            }
+        }
     }
 }
 

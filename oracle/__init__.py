@@ -46,6 +46,8 @@ def lib():
         L.oracle_transform.restype = i
         L.oracle_transform_tiles.argtypes = [i, i, i, vp, vp, vp, vp, vp, ll, i]
         L.oracle_transform_tiles.restype = i
+        L.oracle_cmul.argtypes = [i, vp, vp, vp]
+        L.oracle_cmul.restype = None
         _lib = L
     return _lib
 
@@ -93,6 +95,30 @@ def gen(code: int, seed: int, rank: int, n: int) -> np.ndarray:
         out.imag = im.astype(np.float32)
         return out
     return re + 1j * im
+
+
+_SPECIAL = {np.float64: [np.inf, -np.inf, np.nan, -0.0, 0.0, 1e308, -3.0, 0.5],
+            np.float32: [np.inf, -np.inf, np.nan, -0.0, 0.0, 3e38, -3.0, 0.5]}
+
+
+def add_specials(arr: np.ndarray, code: int, seed: int, rank: int) -> np.ndarray:
+    """about one element in 8 gets non-finite / extreme parts (identical to ref_harness.cpp
+    add_specials: the rule the 'specials' golden cases were generated with)"""
+    if code == INT32:
+        return arr
+    z = _draw(seed ^ 0x5EC1A1, rank, np.arange(arr.size, dtype=np.uint64))
+    hit = (z & np.uint64(7)) == 0
+    rt = np.float32 if code in (FLOAT, CFLOAT) else np.float64
+    table = np.array(_SPECIAL[rt], rt)
+    re = table[((z >> np.uint64(3)) & np.uint64(7)).astype(np.int64)]
+    if code in (FLOAT, DOUBLE):
+        arr[hit] = re[hit]
+    else:
+        im = table[((z >> np.uint64(6)) & np.uint64(7)).astype(np.int64)]
+        v = arr.view(rt).reshape(-1, 2)
+        v[hit, 0] = re[hit]
+        v[hit, 1] = im[hit]
+    return arr
 
 
 # ------------------------------------------------------------------ wrappers

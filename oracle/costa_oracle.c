@@ -24,7 +24,8 @@
  *                               memory_utils.hpp:101-193), used as the timed CPU baseline
  *
  * Arithmetic: products and sums are separate roundings (build with -ffp-contract=off; the
- * reference's x86-64 build has no FMA), complex products as GCC's (ac-bd, ad+bc).
+ * reference's x86-64 build has no FMA), complex products as GCC's: (ac-bd, ad+bc) with the
+ * C99 Annex G recovery of libgcc's __muldc3 / __mulsc3 when both parts are NaN (cmul_f/cmul_d).
  */
 #include <math.h>
 #include <stddef.h>
@@ -98,6 +99,63 @@ static int kind_of(int t, const void* a, const void* b, int copy_mode, int conj)
     return 3;
 }
 
+/* Complex products as the reference's binary computes them.  std::complex<T>::operator* is
+ * GCC's builtin complex multiply (C99 Annex G): the naive (ac - bd, ad + bc), and when BOTH parts
+ * come out NaN a call to libgcc's __muldc3 / __mulsc3, which recovers infinities (third-party
+ * code the reference links: GCC 11.4's libgcc, libgcc2.c; C99 G.5.1).  Restated here;
+ * tests/test_oracle_golden.py pins this restatement to the compiler's own product over a grid of
+ * special values, and tests/golden/specials_*.npz pin the whole path to the reference. */
+#define ANNEX_G_MUL(NAME, R, INF, ISNAN, ISINF, COPYSIGN)                                     \
+    static void NAME(R a, R b, R c, R d, R* re, R* im) {                                     \
+        R ac = a * c, bd = b * d, ad = a * d, bc = b * c;                                    \
+        R x = ac - bd, y = ad + bc;                                                          \
+        if (ISNAN(x) && ISNAN(y)) {                                                          \
+            int recalc = 0;                                                                  \
+            if (ISINF(a) || ISINF(b)) { /* z infinite: box it, NaNs of w to 0 */             \
+                a = COPYSIGN(ISINF(a) ? (R)1 : (R)0, a);                                     \
+                b = COPYSIGN(ISINF(b) ? (R)1 : (R)0, b);                                     \
+                if (ISNAN(c)) c = COPYSIGN((R)0, c);                                         \
+                if (ISNAN(d)) d = COPYSIGN((R)0, d);                                         \
+                recalc = 1;                                                                  \
+            }                                                                                \
+            if (ISINF(c) || ISINF(d)) { /* w infinite */                                     \
+                c = COPYSIGN(ISINF(c) ? (R)1 : (R)0, c);                                     \
+                d = COPYSIGN(ISINF(d) ? (R)1 : (R)0, d);                                     \
+                if (ISNAN(a)) a = COPYSIGN((R)0, a);                                         \
+                if (ISNAN(b)) b = COPYSIGN((R)0, b);                                         \
+                recalc = 1;                                                                  \
+            }                                                                                \
+            if (!recalc && (ISINF(ac) || ISINF(bd) || ISINF(ad) || ISINF(bc))) {             \
+                /* overflow: recover infinities, NaNs to 0 */                                \
+                if (ISNAN(a)) a = COPYSIGN((R)0, a);                                         \
+                if (ISNAN(b)) b = COPYSIGN((R)0, b);                                         \
+                if (ISNAN(c)) c = COPYSIGN((R)0, c);                                         \
+                if (ISNAN(d)) d = COPYSIGN((R)0, d);                                         \
+                recalc = 1;                                                                  \
+            }                                                                                \
+            if (recalc) {                                                                    \
+                R p = a * c, q = b * d, r = a * d, t = b * c;                                \
+                x = INF * (p - q);                                                           \
+                y = INF * (r + t);                                                           \
+            }                                                                                \
+        }                                                                                    \
+        *re = x;                                                                             \
+        *im = y;                                                                             \
+    }
+ANNEX_G_MUL(cmul_f, float, INFINITY, isnan, isinf, copysignf)
+ANNEX_G_MUL(cmul_d, double, (double)INFINITY, isnan, isinf, copysign)
+
+/* exported for tests/test_oracle_golden.py (the restatement against GCC's own product) */
+void oracle_cmul(int t, const void* a, const void* b, void* out) {
+    if (t == OR_CFLOAT) {
+        const float* x = (const float*)a; const float* y = (const float*)b; float* o = (float*)out;
+        cmul_f(x[0], x[1], y[0], y[1], &o[0], &o[1]);
+    } else {
+        const double* x = (const double*)a; const double* y = (const double*)b; double* o = (double*)out;
+        cmul_d(x[0], x[1], y[0], y[1], &o[0], &o[1]);
+    }
+}
+
 /* dst = g(src) for one element; `conj` applies only to complex types (block.hpp:13-25) */
 static void apply1(int t, int kind, int conj, const void* a, const void* b, const void* src,
                    void* dst) {
@@ -135,10 +193,10 @@ static void apply1(int t, int kind, int conj, const void* a, const void* b, cons
         cf_t* d = (cf_t*)dst;
         if (conj) x.im = -x.im;
         if (kind == 1) { d->re = 0.0f; d->im = 0.0f; break; }
-        float pr = al.re * x.re - al.im * x.im, pi = al.re * x.im + al.im * x.re;
+        float pr, pi, qr, qi;
+        cmul_f(al.re, al.im, x.re, x.im, &pr, &pi); /* alpha * el */
         if (kind == 2) { d->re = pr; d->im = pi; break; }
-        float yr = d->re, yi = d->im;
-        float qr = be.re * yr - be.im * yi, qi = be.re * yi + be.im * yr;
+        cmul_f(be.re, be.im, d->re, d->im, &qr, &qi); /* beta * dst */
         d->re = qr + pr;
         d->im = qi + pi;
         break;
@@ -148,10 +206,10 @@ static void apply1(int t, int kind, int conj, const void* a, const void* b, cons
         cd_t* d = (cd_t*)dst;
         if (conj) x.im = -x.im;
         if (kind == 1) { d->re = 0.0; d->im = 0.0; break; }
-        double pr = al.re * x.re - al.im * x.im, pi = al.re * x.im + al.im * x.re;
+        double pr, pi, qr, qi;
+        cmul_d(al.re, al.im, x.re, x.im, &pr, &pi); /* alpha * el */
         if (kind == 2) { d->re = pr; d->im = pi; break; }
-        double yr = d->re, yi = d->im;
-        double qr = be.re * yr - be.im * yi, qi = be.re * yi + be.im * yr;
+        cmul_d(be.re, be.im, d->re, d->im, &qr, &qi); /* beta * dst */
         d->re = qr + pr;
         d->im = qi + pi;
         break;

@@ -37,6 +37,7 @@
 #include <cstdlib>
 #include <fstream>
 #include <iostream>
+#include <limits>
 #include <memory>
 #include <string>
 #include <vector>
@@ -66,6 +67,34 @@ template <> std::complex<double> gen<std::complex<double>>(uint64_t s, int r, ui
 }
 template <> std::complex<float> gen<std::complex<float>>(uint64_t s, int r, uint64_t k) {
     return {float(unif(draw(s, r, 2 * k))), float(unif(draw(s, r, 2 * k + 1)))};
+}
+
+// optional "specials 1" on a pair line: about one element in 8 of A and of C gets non-finite or
+// extreme parts from a fixed table (the same rule as oracle.add_specials in Python)
+template <typename R> R special_part(uint64_t sel);
+template <> double special_part<double>(uint64_t sel) {
+    const double t[8] = {std::numeric_limits<double>::infinity(), -std::numeric_limits<double>::infinity(),
+                         std::numeric_limits<double>::quiet_NaN(), -0.0, 0.0, 1e308, -3.0, 0.5};
+    return t[sel & 7];
+}
+template <> float special_part<float>(uint64_t sel) {
+    const float t[8] = {std::numeric_limits<float>::infinity(), -std::numeric_limits<float>::infinity(),
+                        std::numeric_limits<float>::quiet_NaN(), -0.0f, 0.0f, 3e38f, -3.0f, 0.5f};
+    return t[sel & 7];
+}
+template <typename T> struct part { using type = T; };
+template <typename R> struct part<std::complex<R>> { using type = R; };
+template <typename T>
+void add_specials(std::vector<T>& v, uint64_t seed, int rank) {
+    using R = typename part<T>::type;
+    for (size_t k = 0; k < v.size(); ++k) {
+        const uint64_t z = draw(seed ^ 0x5EC1A1ull, rank, k);
+        if (z & 7) continue;
+        if constexpr (std::is_same<T, R>::value)
+            v[k] = special_part<R>(z >> 3);
+        else
+            v[k] = T(special_part<R>(z >> 3), special_part<R>(z >> 6));
+    }
 }
 
 template <typename T>
@@ -153,6 +182,7 @@ int run_case(std::istream& in, const std::string& out, int rank, int P) {
     std::vector<int> noscale(np);
     std::vector<uint64_t> seedA(np), seedC(np);
     std::vector<std::vector<int>> relabel(np);  // target-layout rank relabelling (may be empty)
+    std::vector<int> specials(np, 0);
     std::vector<lspec> A, C;
     for (int p = 0; p < npairs; ++p) {
         double ar, ai, br, bi;
@@ -169,6 +199,8 @@ int run_case(std::istream& in, const std::string& out, int rank, int P) {
             relabel[size_t(p)].resize(size_t(k));
             for (auto& x : relabel[size_t(p)]) in >> x;
         }
+        in >> std::ws;
+        if (in.peek() == 's') in >> tok >> specials[size_t(p)];
         if constexpr (std::is_same<T, std::complex<double>>::value ||
                       std::is_same<T, std::complex<float>>::value) {
             alpha[size_t(p)] = T(ar, ai);
@@ -195,6 +227,10 @@ int run_case(std::istream& in, const std::string& out, int rank, int P) {
         c.resize(size_t(buf_size(C[size_t(p)], crank)));
         for (size_t k = 0; k < a.size(); ++k) a[k] = gen<T>(seedA[size_t(p)], rank, k);
         for (size_t k = 0; k < c.size(); ++k) c[k] = gen<T>(seedC[size_t(p)], rank, k);
+        if (specials[size_t(p)]) {
+            add_specials(a, seedA[size_t(p)], rank);
+            add_specials(c, seedC[size_t(p)], rank);
+        }
         la.push_back(build<T>(A[size_t(p)], a, rank));
         lc.push_back(build<T>(C[size_t(p)], c, crank));
         if (!rl.empty()) lc.back().reorder_ranks(rl);

@@ -192,6 +192,7 @@ class Pair:
     # relabel[o] and rank r holds the local blocks of base rank relabel^-1[r] (= relabel[r]
     # for the pair swaps optimal_reordering proposes)
     relabel: list | None = None
+    specials: bool = False  # ~1 element in 8 of A and C non-finite or extreme (oracle.add_specials)
 
     def c_rank(self, rank):
         if self.relabel is None:
@@ -219,6 +220,8 @@ class Case:
                     f"noscale {int(p.noscale)} seedA {p.seedA} seedC {p.seedC}")
             if p.relabel is not None:
                 line += f" relabelC {len(p.relabel)} " + " ".join(map(str, p.relabel))
+            if p.specials:
+                line += " specials 1"
             out.append(line)
             out.append(p.A.spec(self.P).rstrip("\n"))
             out.append(p.C.spec(self.P).rstrip("\n"))
@@ -229,6 +232,9 @@ class Case:
         p = self.pairs[pair_idx]
         a = oracle.gen(self.dtype, p.seedA, rank, p.A.buf_elems(rank, self.P))
         c = oracle.gen(self.dtype, p.seedC, rank, p.C.buf_elems(p.c_rank(rank), self.P))
+        if p.specials:
+            oracle.add_specials(a, self.dtype, p.seedA, rank)
+            oracle.add_specials(c, self.dtype, p.seedC, rank)
         return a, c
 
     # ---- the product's layouts of one rank (the C layout relabelled where the pair says so)

@@ -199,6 +199,36 @@ def _relabelled():
     return cases
 
 
+def special_cases():
+    """Non-finite and extreme values (~1 element in 8 of A and C: +-inf, NaN, +-0, 1e308 / 3e38):
+    the reference's complex products go through GCC's C99 Annex G recovery (libgcc __muldc3 /
+    __mulsc3) when both parts of the naive product are NaN.  Kept apart from all_cases(): NaNs
+    GENERATED by arithmetic carry a platform-defined sign (x86: negative, GPU: positive), so the
+    GPU comparison of these treats both-NaN as equal; everything else is bit for bit."""
+    cases = []
+    # 'T' with alpha = 1 (the transposing path multiplies by alpha: (inf+inf i)(1+0i) = inf+inf i)
+    cases.append(Case("specials_z_T", Z, [Pair(BC(50, 60, 16, 12, ord="C"), BC(60, 50, 10, 14, ord="C"),
+                                               "T", 1, 0, seedA=0x51, seedC=0x52, specials=True)]))
+    # 'C' with alpha, beta != 0 over an ordering change (implicit transpose cancels the op's)
+    cases.append(Case("specials_z_C", Z, [Pair(BC(50, 60, 16, 12, ord="R"), BC(60, 50, 10, 14, ord="C"),
+                                               "C", 0.75 - 0.5j, 1.25 + 0.25j, seedA=0x53, seedC=0x54,
+                                               specials=True)]))
+    # complex<float> 'N' copy mode with alpha, beta; and huge alpha: the overflow recovery branch
+    cases.append(Case("specials_c_N", CF, [Pair(BC(70, 40, 9, 11, ord="C"), BC(70, 40, 13, 8, ord="C"),
+                                                "N", 1j, -1, seedA=0x55, seedC=0x56, specials=True)]))
+    cases.append(Case("specials_c_big", CF, [Pair(BC(40, 70, 9, 11, ord="C"), BC(70, 40, 13, 8, ord="R"),
+                                                  "T", 1e30 + 1e30j, 2e25 - 1e25j, seedA=0x57,
+                                                  seedC=0x58, specials=True)]))
+    # real types, and two ranks (the arithmetic in UNPACK)
+    cases.append(Case("specials_d_T", D, [Pair(BC(60, 50, 16, 12, pm=1, pn=2, ord="C"),
+                                               BC(50, 60, 10, 14, pm=2, pn=1, ord="C"), "T", -0.5, 2.0,
+                                               seedA=0x59, seedC=0x5A, specials=True)], P=2))
+    cases.append(Case("specials_z_2r", Z, [Pair(BC(48, 40, 8, 8, pm=2, pn=1, ord="C"),
+                                                BC(40, 48, 8, 8, pm=1, pn=2, ord="C"), "T", 1, 0,
+                                                seedA=0x5B, seedC=0x5C, specials=True)], P=2))
+    return cases
+
+
 def all_cases():
     return _named() + _sweep() + _baseline_geometries() + _relabelled()
 

@@ -28,7 +28,7 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, HERE)
 sys.path.insert(0, os.path.dirname(HERE))
 
-from cases import all_cases  # noqa: E402
+from cases import all_cases, special_cases  # noqa: E402
 
 HARNESS = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
 MPIEXEC = "/opt/conda/bin/mpiexec"
@@ -78,7 +78,7 @@ def main(argv):
     want = set(argv[1:])
     if not want or "kat" in want:
         make_kat()
-    for c in all_cases():
+    for c in all_cases() + special_cases():
         if want and c.name not in want:
             continue
         make_case(c)

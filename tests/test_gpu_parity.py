@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 import oracle
-from cases import BC, Case, Pair, all_cases
+from cases import BC, Case, Pair, all_cases, special_cases
 from golden_io import first_mismatch, load, matches
 
 pytestmark = pytest.mark.gpu
@@ -183,8 +183,20 @@ def assert_bits_equal_or_both_nan(got, expected):
     assert ok.all(), f"{(~ok).sum()} elements differ; first {np.nonzero(~ok)[0][:5]}"
 
 
-SPECIAL = np.array([0.0, -0.0, 1.0, -1.0, 1e-310, -1e-310, 1e308, -1e308, 3.5, -2.25],
-                   np.float64)
+SPECIAL = np.array([0.0, -0.0, 1.0, -1.0, 1e-310, -1e-310, 1e308, -1e308, 3.5, -2.25, np.inf,
+                    -np.inf, np.nan], np.float64)
+
+
+@pytest.mark.parametrize("case", special_cases(), ids=lambda c: c.name)
+def test_special_values_golden(gpu, case):
+    """inf / NaN / signed zeros / huge values against the REFERENCE's own outputs: the complex
+    products recover infinities as GCC's __muldc3 / __mulsc3 do (C99 Annex G), e.g.
+    (inf + inf i)(1 + 0i) = inf + inf i; generated NaNs may differ in sign only"""
+    fx = load(case.name)
+    got = [_run_single_rank(gpu, case)] if case.P == 1 else _run_emulated_ranks(gpu, case)
+    for r in range(case.P):
+        for k in range(len(case.pairs)):
+            assert_bits_equal_or_both_nan(got[r][k], fx[f"C{k}_r{r}"])
 
 
 @pytest.mark.parametrize("dtype", [0, 1, 2, 3])

@@ -4,7 +4,11 @@ tests/golden/make_relabel_fixtures.py from oracle/_ref/ref_harness).
 
 * The communication graph (every rank pair's volume, local pairs included) must equal the
   reference's exactly.
-* The proposed permutation must be a valid involution, and keep at least as much data local as
+* The proposed permutation must equal the reference's on every case with no tie between pair
+  worths (bc_T, bc_remap, custom).  On `permuted` four pairs are worth exactly the same
+  (250000 each): the reference takes them in its unordered_map's iteration order through an
+  unstable std::sort (comm_volume.hpp:36-50, ranks_reordering.cpp:16-39), ours by rank ids, and
+  both keep the same volume local.  On the README geometry ours must keep more data local than
   the reference's.  Known reference bug not copied: optimal_reordering reads
   volume[{a, a}] with operator[] while iterating the same unordered_map
   (ranks_reordering.cpp:18-33), which inserts keys and can invalidate the iteration, so
@@ -50,6 +54,13 @@ def test_relabel_vs_reference(exe, tmp_path, name):
     perm = got["perm"]
     assert sorted(perm) == list(range(P))
     assert all(perm[perm[k]] == k for k in range(P))  # pairs of swapped ranks
-    assert got["new_total"] <= ref["new_total"]
-    if name == "readme":
+    if name == "readme":  # the documented divergence: the published figure, not the bug's
+        assert got["perm"] != ref["perm"] and got["new_total"] < ref["new_total"]
         assert round(100.0 * (got["total"] - got["new_total"]) / got["total"], 4) == 33.3333
+        assert round(100.0 * (ref["total"] - ref["new_total"]) / ref["total"], 4) == 16.6667
+    elif name == "permuted":  # a tie between equal pair worths, broken differently
+        assert (perm, ref["perm"]) == ([1, 0, 3, 2], [2, 3, 0, 1])
+        assert got["new_total"] == ref["new_total"] == got["total"] // 2
+    else:
+        assert perm == ref["perm"], f"permutation differs from the reference's: {perm} vs {ref['perm']}"
+        assert got["new_total"] == ref["new_total"] and got["reordered"] == ref["reordered"]
