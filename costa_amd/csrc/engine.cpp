@@ -391,6 +391,73 @@ void emit_pieces(const costa_tile_op_t& op, int64_t E, const wave_grid& g, costa
     }
 }
 
+// Source neighbours: the tiles one source block is cut into by the target grid continue each
+// other's columns (the op starting at src + nf * E with the same stride holds the rows below),
+// and each pair shares the cache lines where a column of the upper one ends and the same
+// column of the lower one begins.  In destination-address order the two run one target
+// block-row apart (cfg 5: ~5 MB of traffic, far beyond an XCD's L2), so those lines are fetched
+// twice.  This pulls every op's chain of lower neighbours right behind it (keeping the order
+// otherwise): the shared lines then meet in one L2.
+void chain_source_neighbours(const std::vector<const costa_tile_op_t*>& ops, int64_t E,
+                             std::vector<uint32_t>& perm) {
+    const size_t n = ops.size();
+    std::vector<std::pair<uint64_t, uint32_t>> by_src(n);
+    for (size_t i = 0; i < n; ++i) by_src[i] = {ops[i]->src, uint32_t(i)};
+    std::sort(by_src.begin(), by_src.end());
+    auto below = [&](uint32_t i) -> int64_t {
+        const costa_tile_op_t& o = *ops[i];
+        const uint64_t want = o.src + uint64_t(int64_t(o.nf) * E);
+        auto it = std::lower_bound(by_src.begin(), by_src.end(), std::make_pair(want, uint32_t(0)));
+        if (it == by_src.end() || it->first != want) return -1;
+        const costa_tile_op_t& b = *ops[it->second];
+        if (b.lds != o.lds || b.ns != o.ns || (b.flags & COSTA_TILE_TRANSPOSE) != (o.flags & COSTA_TILE_TRANSPOSE))
+            return -1;
+        return int64_t(it->second);
+    };
+    std::vector<char> done(n, 0);
+    std::vector<uint32_t> out;
+    out.reserve(n);
+    for (const uint32_t i : perm) {
+        if (done[i]) continue;
+        for (int64_t j = i; j >= 0 && !done[size_t(j)]; j = below(uint32_t(j))) {
+            done[size_t(j)] = 1;
+            out.push_back(uint32_t(j));
+        }
+    }
+    perm.swap(out);
+}
+
+// Destination rows merged in bands (tuning mode COSTA_TINY_SORT=7): in destination order, a
+// maximal run of ops with one destination stride is taken as one target block-row (custom
+// layouts: every block-row has its own ld); `h` consecutive runs are merged by each op's
+// relative position within its run (~ its target column), so the ops one source block is cut
+// into by a block-row boundary run close together in time.
+void merge_row_bands(const std::vector<const costa_tile_op_t*>& ops, int h, std::vector<uint32_t>& perm) {
+    const size_t n = perm.size();
+    std::vector<uint32_t> run(n);
+    std::vector<std::pair<uint64_t, uint64_t>> span;  // per run: first / last destination
+    for (size_t k = 0; k < n; ++k) {
+        const costa_tile_op_t& o = *ops[perm[k]];
+        if (k == 0 || o.ldd != ops[perm[k - 1]]->ldd) span.push_back({o.dst, o.dst});
+        span.back().second = o.dst;
+        run[k] = uint32_t(span.size() - 1);
+    }
+    struct key_t {
+        uint64_t band, pos, r, k;
+        bool operator<(const key_t& y) const { return std::tie(band, pos, r, k) < std::tie(y.band, y.pos, y.r, y.k); }
+    };
+    std::vector<key_t> key(n);
+    for (size_t k = 0; k < n; ++k) {
+        const auto& sp = span[run[k]];
+        const double f = sp.second > sp.first ? double(ops[perm[k]]->dst - sp.first) / double(sp.second - sp.first) : 0.0;
+        key[k] = {run[k] / uint64_t(h), uint64_t(f * double(1 << 20)), run[k], k};
+    }
+    std::sort(key.begin(), key.end());
+    std::vector<uint32_t> out(n);
+    for (size_t k = 0; k < n; ++k) out[k] = perm[key[k].k];
+    perm.swap(out);
+}
+
 // runs fn(begin, end) over [0, n) on up to 8 host threads (one when n is small)
 template <typename F>
 void host_parallel(size_t n, F fn) {
@@ -438,6 +505,7 @@ struct wave_knobs {  // defaults, overridable for tuning runs
                          // 0.454 with 512^2), else 1 (c128 with 128^2 blocks: 2.87 against 2.27
                          // ms; copy lists untested under 2; tools/order_run.sh,
                          // tools/f32_order_run.sh, profiles/r2/order/)
+    int band_h = 2;  // COSTA_BAND_H: destination rows merged per band (sort mode 7)
     int sort = 5;    // COSTA_TINY_SORT 0: list order, 1: by source, 2: by destination address,
                      // 3: by the planner's locality hint (costa_tile_op_t::order), 4: 3 for
                      // copy-only lists, 2 for lists that transpose (cfg 5 'T' 3.88 against
@@ -456,15 +524,32 @@ const wave_knobs& knobs() {
         if (const char* s = std::getenv("COSTA_WAVE_POLICY")) x.policy = std::atoi(s) == 1 ? 1 : 2;
         if (const char* s = std::getenv("COSTA_TINY_SORT")) x.sort = std::atoi(s);
         if (const char* s = std::getenv("COSTA_LARGE_SORT")) x.large_sort = std::atoi(s);
+        if (const char* s = std::getenv("COSTA_BAND_H")) x.band_h = std::max(1, std::atoi(s));
         return x;
     }();
     return k;
 }
 }  // namespace
 
-work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops,
+work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops_in,
                       std::vector<costa_tile_op_t>& ordered, std::vector<uint64_t>& work,
                       bool pack_list) {
+    // COSTA_MISALIGNED_VEC (tuning only): 1 / 2 / 3 = treat dword-aligned destinations / sources
+    // / both as vector-aligned (16-byte accesses at 4-byte alignment)
+    static const int mis = [] {
+        const char* s = std::getenv("COSTA_MISALIGNED_VEC");
+        return s ? std::atoi(s) : 0;
+    }();
+    std::vector<costa_tile_op_t> ops_mis;
+    if (mis) {
+        ops_mis = ops_in;
+        const uint64_t E = dtype_size(dtype);
+        for (auto& op : ops_mis) {
+            if ((mis & 1) && op.dst % 4 == 0 && (uint64_t(op.ldd) * E) % 4 == 0) op.flags |= COSTA_TILE_VEC_DST;
+            if ((mis & 2) && op.src % 4 == 0 && (uint64_t(op.lds) * E) % 4 == 0) op.flags |= COSTA_TILE_VEC_SRC;
+        }
+    }
+    const std::vector<costa_tile_op_t>& ops = mis ? ops_mis : ops_in;
     const bool tr_shape = any_transpose(ops);
     shape_dims sh;
     tile_shapes(dtype, tr_shape, &sh);
@@ -549,18 +634,41 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
             cls[li] = m ? 1 : 2;
         }
     }
-    std::vector<uint32_t> shaped[2];  // [0] large, [1] medium
+    // transposes whose destination columns are off the 16-byte grid (an odd ScaLAPACK lld) go to
+    // the skew shape (tile_kernels.hip skew_kernel): each sub-tile writes whole 64-byte
+    // granules of every destination column, overlapping its neighbours by identical values,
+    // instead of sharing partial granules with them (measured: a copy whose 128-byte lines are
+    // split between workgroups at 16-byte granularity 0.808 against 0.672 ms, at 64-byte
+    // granularity 0.702; tools/partial_line_probe.hip).  Not for ops that read C (beta != 0:
+    // an overlapping write would apply beta twice).
+    const int64_t k_elems = int64_t(sh.bf_k) * sh.bs_k;
+    static const bool skew_on = [] {  // COSTA_SKEW=0: off (tuning)
+        const char* s = std::getenv("COSTA_SKEW");
+        return !s || std::atoi(s) != 0;
+    }();
+    for (size_t li = 0; skew_on && k_elems > 0 && li < ops.size(); ++li) {
+        const costa_tile_op_t& op = ops[li];
+        if (cls[li] == 3 || !(op.flags & COSTA_TILE_TRANSPOSE) || (op.flags & COSTA_TILE_VEC_DST))
+            continue;
+        const uint32_t kind = (op.flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT;
+        if (kind == COSTA_SCALE_AXPBY || op.dst % uint64_t(E) != 0 || 2 * int64_t(op.nf) * op.ns < k_elems)
+            continue;
+        if (cls[li] == 1) --n_med;
+        cls[li] = 4;
+    }
+    std::vector<uint32_t> shaped[3];  // [0] large, [1] medium, [2] skew
     for (size_t li = 0; li < ops.size(); ++li) {
         const int c = cls[li] == 1 && n_med < kMinMediumOps ? 2 : cls[li];
         if (c < 2) shaped[c].push_back(uint32_t(li));
         else if (c == 2) wave_ops.push_back(&ops[li]);
+        else if (c == 4) shaped[2].push_back(uint32_t(li));
     }
     // each shape's ops in hint order when every one carries a hint; lists whose shaped ops all
     // transpose 8-byte elements then take the sub-tiles in destination-address order (wave_knobs)
-    int64_t n_work[2] = {0, 0};
-    for (int c = 0; c < 2; ++c) {
-        const int bf = c ? (med_sq ? sh.bf_s : sh.bf_m) : sq ? sh.bf_q : sh.bf;
-        const int bs = c ? (med_sq ? sh.bs_s : sh.bs_m) : sq ? sh.bs_q : sh.bs;
+    int64_t n_work[3] = {0, 0, 0};
+    for (int c = 0; c < 3; ++c) {
+        const int bf = c == 2 ? sh.bf_k : c ? (med_sq ? sh.bf_s : sh.bf_m) : sq ? sh.bf_q : sh.bf;
+        const int bs = c == 2 ? sh.bs_k : c ? (med_sq ? sh.bs_s : sh.bs_m) : sq ? sh.bs_q : sh.bs;
         const std::vector<uint32_t>& sel = shaped[c];
         std::vector<uint32_t> sperm(sel.size());
         for (size_t i = 0; i < sel.size(); ++i) sperm[i] = uint32_t(i);
@@ -616,8 +724,10 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         tr = tr || (o->flags & COSTA_TILE_TRANSPOSE);
     }
     const int mode = kn.sort == 5   ? (pack_list ? 1 : 2)
+                     : kn.sort == 6 || kn.sort == 7 ? (pack_list ? 1 : 2)
                      : kn.sort == 4 ? (tr || top == 0 ? 2 : 3)
                      : kn.sort == 3 && top == 0 ? 2 : kn.sort;
+    const bool chain = kn.sort == 6 && !pack_list;
     std::vector<uint32_t> perm(nw);
     if (mode == 3 && size_t(top) <= 4 * nw + 1024) {
         // the planner's hints are ranks within the list: a stable counting sort
@@ -665,6 +775,8 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     } else {
         for (size_t i = 0; i < nw; ++i) perm[i] = uint32_t(i);
     }
+    if (chain && nw > 1) chain_source_neighbours(wave_ops, E, perm);
+    if (kn.sort == 7 && !pack_list && nw > 1) merge_row_bands(wave_ops, kn.band_h, perm);
     // pieces: count per op, scan, fill (host threads for long lists)
     std::vector<wave_grid> grid(nw);
     std::vector<size_t> at_piece(nw + 1, 0);
@@ -687,6 +799,16 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         w.med_full = w.med_full && ops[li].nf % sh.bf_m == 0 && ops[li].ns % sh.bs_m == 0;
     w.n_large = n_work[0];
     w.n_medium = n_work[1];
+    w.n_skew = n_work[2];
+    {
+        static const int mode = [] {  // COSTA_MISDST_MODE (tuning)
+            const char* s = std::getenv("COSTA_MISDST_MODE");
+            return s ? std::atoi(s) & 3 : 0;
+        }();
+        bool mis_dst = false;
+        for (const uint32_t li : shaped[0]) mis_dst = mis_dst || !(ops[li].flags & COSTA_TILE_VEC_DST);
+        w.large_mode = mis_dst ? mode : 0;
+    }
     w.tiny_first = int64_t(ordered.size());
     w.n_tiny = int64_t(at_piece[nw]);
     const size_t base = ordered.size();
@@ -706,6 +828,7 @@ launch_args make_launch(const work_split& w, const void* d_ordered, const void* 
     a.work = static_cast<const uint64_t*>(d_work);
     a.n_large = w.n_large;
     a.n_medium = w.n_medium;
+    a.n_skew = w.n_skew;
     a.tiny_first = w.tiny_first;
     a.n_tiny = w.n_tiny;
     a.src_base = src_base;
@@ -718,6 +841,7 @@ launch_args make_launch(const work_split& w, const void* d_ordered, const void* 
     a.full = w.full;
     a.med_full = w.med_full;
     a.med_sq = w.med_sq;
+    a.large_mode = w.large_mode;
     return a;
 }
 

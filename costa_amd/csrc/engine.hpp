@@ -181,6 +181,7 @@ struct launch_args {
     const uint64_t* work;   // per sub-tile: (op index << 32) | sub-tile index
     int64_t n_large;        // work items using the large sub-tile shape
     int64_t n_medium;       // then work[n_large, n_large + n_medium): the medium shape
+    int64_t n_skew = 0;     // then n_skew items of the skew shape (unaligned destinations)
     int64_t tiny_first;     // ops[tiny_first, tiny_first + n_tiny) run one per wavefront
     int64_t n_tiny;
     const char* src_base;
@@ -193,6 +194,7 @@ struct launch_args {
     bool full;              // work_split::full
     bool med_full;          // work_split::med_full
     bool med_sq;            // work_split::med_sq
+    int large_mode = 0;     // work_split::large_mode
 };
 bool any_transpose(const std::vector<costa_tile_op_t>& ops);
 bool any_axpby(const std::vector<costa_tile_op_t>& ops);
@@ -203,6 +205,7 @@ void launch_tiles(costa_dtype_t dtype, const launch_args& a, void* stream /* hip
 // and the 32 x 32 shape the medium class takes when its ops all fit it (bf_s x bs_s)
 struct shape_dims {
     int bf = 0, bs = 0, bf_m = 0, bs_m = 0, bf_q = 0, bs_q = 0, bf_s = 0, bs_s = 0;
+    int bf_k = 0, bs_k = 0;  // the skew shape (transposes into unaligned destinations; 0: none)
 };
 void tile_shapes(costa_dtype_t dtype, bool transposing_list, shape_dims* out);
 // Execution order of an op list: `ordered` = [sub-tiled ops | tiny ops] (tiny ops sorted by the
@@ -211,13 +214,16 @@ void tile_shapes(costa_dtype_t dtype, bool transposing_list, shape_dims* out);
 // `work` = [large-shape sub-tiles | small-shape sub-tiles], indices into `ordered`.
 struct work_split {
     int64_t n_large = 0, n_medium = 0, tiny_first = 0, n_tiny = 0;
+    int64_t n_skew = 0;     // skew-shape work items, after the medium ones
     bool tr_shape = false;  // sub-tiles cut with tile_shapes(dtype, true, ...)
     bool sq = false;        // ... the large ops with its square variant (bf_q x bs_q)
     bool full = false;      // every large op of a transposing list is aligned and a whole number
                             // of large sub-tiles (the launch may then take fewer threads)
     bool med_full = false;  // the same for the medium ops and the medium sub-tile
     bool med_sq = false;    // the medium class runs on 32 x 32 sub-tiles (bf_s x bs_s)
-    int64_t n_items() const { return n_large + n_medium + n_tiny; }
+    int large_mode = 0;     // large shape, lists with unaligned destinations: bit 0 default-policy
+                            // stores (not nt), bit 1 XCD-contiguous slices of the work list
+    int64_t n_items() const { return n_large + n_medium + n_skew + n_tiny; }
 };
 // pack_list: the ops write the dense send package (their destinations are contiguous whatever
 // their order), which changes the wavefront ops' order (wave_knobs::sort)

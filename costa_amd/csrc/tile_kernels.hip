@@ -183,14 +183,15 @@ __device__ __forceinline__ raw16 ld16(const void* p) {
 #endif
     return r;
 }
+template <bool NT = bool(COSTA_NT_STORES)>
 __device__ __forceinline__ void st16(void* p, const raw16& r) {
-#if COSTA_NT_STORES
-    u32x4a v;
-    __builtin_memcpy(&v, &r, 16);
-    __builtin_nontemporal_store(v, reinterpret_cast<u32x4a*>(p));
-#else
-    *reinterpret_cast<raw16*>(p) = r;
-#endif
+    if constexpr (NT) {
+        u32x4a v;
+        __builtin_memcpy(&v, &r, 16);
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4a*>(p));
+    } else {
+        *reinterpret_cast<raw16*>(p) = r;
+    }
 }
 
 template <typename T>
@@ -206,13 +207,13 @@ __device__ __forceinline__ void vload(vec<T>& out, const T* p, int n, bool vec_o
     }
 }
 
-template <typename T>
+template <typename T, bool NT = bool(COSTA_NT_STORES)>
 __device__ __forceinline__ void vstore(T* p, const vec<T>& in, int n, bool vec_ok) {
     constexpr int V = vec<T>::V;
     if (vec_ok && n >= V) {
         raw16 r;
         __builtin_memcpy(&r, &in, 16);
-        st16(p, r);
+        st16<NT>(p, r);
     } else {
 #pragma unroll
         for (int k = 0; k < V; ++k)
@@ -313,6 +314,60 @@ __device__ __forceinline__ vec<T> lane_transpose(const vec<T>& in, int lane) {
         out.e[3] = sel4(k, g1, g2, g3, g0);
     }
     return out;
+}
+
+// A lane of the transposing store phase holds V consecutive destination elements d[0, V) of one
+// destination column (s values sb .. sb + V - 1); with an odd ld those columns start off the
+// 16-byte grid: d sits eps elements past an aligned address.  Element-wise stores there ran
+// 8-byte fp64 columns at ~4 TB/s against 6.1 aligned (HBM traffic equal: 1.035x), misaligned
+// 16-byte stores no faster.  Instead every aligned chunk [d - eps, d - eps + V) is stored whole,
+// by the lane whose own elements fill its top V - eps slots, the bottom eps taken from the lane V
+// below (which holds d[-V, 0) of the same column: same f, s values sb - V ..).  The lowest lane
+// group of a store unit has no such neighbour in its wavefront and stores its own part element by
+// element; so does a lane whose upper eps elements no lane above will cover (top of the unit or of
+// the tile).  Every lane that is valid here runs the shuffle (the lane V below a valid lane is
+// valid: same column, earlier s).
+template <typename T, int V, int EPS>
+__device__ __forceinline__ vec<T> shifted_chunk(const vec<T>& below, const vec<T>& o) {
+    vec<T> c;
+#pragma unroll
+    for (int e = 0; e < V; ++e)
+        c.e[e] = e < EPS ? below.e[V - EPS + e < V ? V - EPS + e : V - 1] : o.e[e >= EPS ? e - EPS : 0];
+    return c;
+}
+template <typename T, typename S, bool NT>
+__device__ __forceinline__ void store_shifted(T* d, const vec<T>& o, int n, int lane) {
+    constexpr int V = S::V;
+    vec<T> below;
+#pragma unroll
+    for (int e = 0; e < V; ++e) below.e[e] = __shfl_up(o.e[e], unsigned(V), 64);
+    const int eps = int((reinterpret_cast<uintptr_t>(d) / sizeof(T)) & uintptr_t(V - 1));
+    if (eps == 0) {
+        vstore<T, NT>(d, o, n, true);
+        return;
+    }
+    const int ls = lane % S::SW;
+    const int own = V - eps;  // own elements in the chunk that starts eps below d
+    if (ls >= V && n >= own) {
+        // (every register index compile-time: one branch per eps)
+        vec<T> c;
+        if (eps == 1) c = shifted_chunk<T, V, 1>(below, o);
+        if constexpr (V > 2) {
+            if (eps == 2) c = shifted_chunk<T, V, 2>(below, o);
+            if (eps == 3) c = shifted_chunk<T, V, 3>(below, o);
+        }
+        vstore<T, NT>(d - eps, c, V, true);
+    } else {
+#pragma unroll
+        for (int e = 0; e < V; ++e)
+            if (e < own && e < n) d[e] = o.e[e];
+    }
+    // the upper eps elements go with the chunk of the lane V above, unless there is none
+    if (ls + V >= S::SW || n - V < own) {
+#pragma unroll
+        for (int e = 0; e < V; ++e)
+            if (e >= own && e < n) d[e] = o.e[e];
+    }
 }
 
 // sub-tile geometry of one kernel shape
@@ -471,7 +526,7 @@ template <> struct shapes<cpx<double>> {
 // One sub-tile.  FULL: the sub-tile is a whole BF x BS block with 16-byte aligned rows on
 // both sides, so every guard below folds away and each thread issues its loads and stores
 // back to back with no per-lane branches (the common case: block-cyclic tiles).
-template <typename T, typename S, bool FULL>
+template <typename T, typename S, bool FULL, bool NT = bool(COSTA_NT_STORES)>
 __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int s0, int tf_, int ts_,
                                          const char* src_base, char* dst_base, T alpha, T beta,
                                          T* tile) {
@@ -527,7 +582,7 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
                     continue;
                 }
             }
-            vstore(d, x[k], nf_lane, vd);
+            vstore<T, NT>(d, x[k], nf_lane, vd);
         }
         if constexpr (is_cpx<T>::value) {
             static_assert(S::PL <= 32, "redo mask");
@@ -599,6 +654,9 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
         }
     }
     uint32_t redo = 0;  // complex store units left for the Annex G path (bit k: unit k)
+    // destination columns not 16-byte aligned but element aligned (an odd ScaLAPACK lld): the
+    // stores are re-cut into aligned 16-byte chunks across lanes (store_shifted)
+    const bool shift_dst = !vd && op.dst % sizeof(T) == 0;
 #pragma unroll
     for (int k = 0; k < S::PS; ++k) {
         vec<T> o = lane_transpose(y[k], lane);
@@ -616,7 +674,13 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
                 continue;
             }
         }
-        vstore(d, o, n, vd);
+        if constexpr (!FULL && !is_cpx<T>::value && V > 1) {
+            if (shift_dst) {
+                store_shifted<T, S, NT>(d, o, n, lane);
+                continue;
+            }
+        }
+        vstore<T, NT>(d, o, n, vd);
     }
     if constexpr (is_cpx<T>::value) {
         static_assert(S::PS <= 32, "redo mask");
@@ -640,7 +704,9 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
     }
 }
 
-template <typename T, typename S>
+// MODE bit 0: default-policy stores instead of nt; bit 1: XCD-contiguous slices of the work list
+// (lists with unaligned destinations, engine.cpp work_split::large_mode)
+template <typename T, typename S, int MODE = 0>
 __global__ __launch_bounds__(S::NT) void tile_kernel(const costa_tile_op_t* __restrict__ ops,
                                                      const uint64_t* __restrict__ work,
                                                      const char* src_base, char* dst_base,
@@ -648,7 +714,13 @@ __global__ __launch_bounds__(S::NT) void tile_kernel(const costa_tile_op_t* __re
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     T* tile = reinterpret_cast<T*>(smem);
     // which sub-tile of which op (wave-uniform: scalar loads)
-    const uint64_t w = work[blockIdx.x];
+    int64_t wi = blockIdx.x;
+    if constexpr ((MODE & 2) != 0) {  // XCD x of 8 walks one contiguous slice of the list
+        const int64_t nb = gridDim.x, x = int64_t(blockIdx.x) % 8, per = nb / 8, rem = nb % 8;
+        const int64_t i = int64_t(blockIdx.x) / 8;
+        wi = x < rem ? x * (per + 1) + i : rem * (per + 1) + (x - rem) * per + i;
+    }
+    const uint64_t w = work[wi];
     const costa_tile_op_t op = ops[w >> 32];
     const uint32_t sub = uint32_t(w);
     const int nbf = (op.nf + S::BF - 1) / S::BF;
@@ -660,10 +732,111 @@ __global__ __launch_bounds__(S::NT) void tile_kernel(const costa_tile_op_t* __re
     const T alpha = scalars[2 * slot];
     const T beta = scalars[2 * slot + 1];
     const uint32_t vec_both = COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST;
+    constexpr bool NT = bool(COSTA_NT_STORES) && (MODE & 1) == 0;
     if (tf == S::BF && ts == S::BS && (op.flags & vec_both) == vec_both)
-        run_tile<T, S, true>(op, f0, s0, tf, ts, src_base, dst_base, alpha, beta, tile);
+        run_tile<T, S, true, NT>(op, f0, s0, tf, ts, src_base, dst_base, alpha, beta, tile);
     else
-        run_tile<T, S, false>(op, f0, s0, tf, ts, src_base, dst_base, alpha, beta, tile);
+        run_tile<T, S, false, NT>(op, f0, s0, tf, ts, src_base, dst_base, alpha, beta, tile);
+}
+
+// ---------------------------------------------------------------- skew shape
+// Transposing ops whose destination columns are off the 16-byte grid (an odd ScaLAPACK lld;
+// engine.cpp build_work routes them here, real types, never ops that read C).  A partial 64-byte
+// granule written by two workgroups costs the HBM a read-modify-write: a copy with its lines split
+// at 16-byte granularity between neighbouring workgroups ran 0.808 against 0.672 ms
+// (tools/partial_line_probe.hip).  So sub-tile (f0, s0) writes, for each destination column f,
+// the whole granules [s0 - eps_f, s0 + BS - eps_f (+ G if eps_f > 0)) clipped to the op, where
+// eps_f is how far d(f, s0) lies past a granule boundary: the first eps_f and the last G - eps_f
+// elements overlap the neighbouring sub-tiles of the same op, which write the same values (alpha *
+// x, 0 or x: a function of A alone).  The source rows [s0 - G, s0 + BS + G) are staged (odd
+// pitch: the column-wise LDS reads of the store phase are conflict-free); lanes then walk each
+// destination column in element stores, 64 consecutive elements per instruction.
+template <typename T>
+struct skew_shape {
+    static constexpr int NT = 512, BF = 64, BS = 128;
+    static constexpr int E = int(sizeof(T)), G = 64 / E, RS = BS + 2 * G, P = BF + 1;
+    static constexpr int V = 16 / E, LPC = BF / V, CPP = NT / LPC, PL = (RS + CPP - 1) / CPP;
+    static constexpr int NW = NT / 64;
+    static constexpr size_t lds_bytes = size_t(RS) * P * sizeof(T);
+};
+
+template <typename T>
+__global__ __launch_bounds__(512) void skew_kernel(const costa_tile_op_t* __restrict__ ops,
+                                                   const uint64_t* __restrict__ work,
+                                                   const char* src_base, char* dst_base,
+                                                   const T* __restrict__ scalars) {
+    using K = skew_shape<T>;
+    constexpr int V = K::V, BF = K::BF, BS = K::BS, G = K::G, P = K::P;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    T* tile = reinterpret_cast<T*>(smem);
+    const uint64_t w = work[blockIdx.x];
+    const costa_tile_op_t op = ops[w >> 32];
+    const uint32_t sub = uint32_t(w);
+    const int nbf = (op.nf + BF - 1) / BF;
+    const int f0 = int(sub % uint32_t(nbf)) * BF;
+    const int s0 = int(sub / uint32_t(nbf)) * BS;
+    const int tf = min(BF, op.nf - f0), ns = op.ns;
+    const uint32_t kind = (op.flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT;
+    const uint32_t slot = op.flags >> COSTA_SLOT_SHIFT;
+    const T alpha = kind >= COSTA_SCALE_ALPHA ? scalars[2 * slot] : T(0);
+    const bool vs = op.flags & COSTA_TILE_VEC_SRC;
+    const int64_t lds = op.lds, ldd = op.ldd;
+    const T* src = reinterpret_cast<const T*>(src_base + op.src) + f0;
+    // ---- rows s = s0 - G + r, r < RS, inside the op: all loads first
+    const int lf = (int(threadIdx.x) % K::LPC) * V;
+    const int c0 = int(threadIdx.x) / K::LPC;
+    const int nf_lane = tf - lf;
+    vec<T> x[K::PL];
+#pragma unroll
+    for (int k = 0; k < K::PL; ++k) {
+        const int r = c0 + k * K::CPP, s = s0 - G + r;
+        if (r < K::RS && s >= 0 && s < ns && nf_lane > 0) vload(x[k], src + s * lds + lf, nf_lane, vs);
+    }
+#pragma unroll
+    for (int k = 0; k < K::PL; ++k) {
+        const int r = c0 + k * K::CPP, s = s0 - G + r;
+        if (r < K::RS && s >= 0 && s < ns && nf_lane > 0) {
+#pragma unroll
+            for (int e = 0; e < V; ++e)
+                if (e < nf_lane) tile[r * P + lf + e] = x[k].e[e];
+        }
+    }
+    __syncthreads();
+    // ---- destination column f0 + f: whole granules, 64 consecutive elements per store
+    const int lane = int(threadIdx.x) % 64, wave = int(threadIdx.x) / 64;
+    T* dst = reinterpret_cast<T*>(dst_base + op.dst);
+    for (int f = wave; f < tf; f += K::NW) {
+        T* col = dst + int64_t(f0 + f) * ldd;
+        const int eps = int((reinterpret_cast<uintptr_t>(col + s0) / sizeof(T)) & uintptr_t(G - 1));
+        const int lo = max(0, s0 - eps);
+        const int hi = min(ns, s0 + BS - eps + (eps ? G : 0));
+        for (int s = lo + lane; s < hi; s += 64) {
+            T v = tile[(s - s0 + G) * P + f];
+            if (kind == COSTA_SCALE_ZERO) v = T(0);
+            else if (kind == COSTA_SCALE_ALPHA) v = alpha * v;
+#if COSTA_NT_STORES
+            __builtin_nontemporal_store(v, col + s);
+#else
+            col[s] = v;
+#endif
+        }
+    }
+}
+
+template <typename T>
+void launch_skew(const launch_args& a, const uint64_t* work, int64_t n, hipStream_t stream) {
+    if constexpr (std::is_same<T, float>::value || std::is_same<T, double>::value ||
+                  std::is_same<T, int>::value) {
+        const int64_t max_grid = 1LL << 30;
+        for (int64_t off = 0; off < n; off += max_grid) {
+            const int64_t m = std::min(max_grid, n - off);
+            hipLaunchKernelGGL((skew_kernel<T>), dim3(unsigned(m)), dim3(skew_shape<T>::NT),
+                               skew_shape<T>::lds_bytes, stream, a.ops, work + off, a.src_base,
+                               a.dst_base, static_cast<const T*>(a.scalars));
+        }
+    } else if (n > 0) {
+        throw error(COSTA_ERR_INTERNAL, "costa: skew shape for a complex type");
+    }
 }
 
 // ---------------------------------------------------------------- wavefront path
@@ -893,17 +1066,30 @@ void launch_tiny(const launch_args& a, hipStream_t stream) {
                 : launch_tiny_v<T, TINY_WAVES_COPY, false, false>(a, stream);
 }
 
-template <typename T, typename S>
+template <typename T, typename S, int MODE = 0>
 void launch_shape(const launch_args& a, const uint64_t* work, int64_t n, hipStream_t stream) {
     const int64_t max_grid = 1LL << 30;
     for (int64_t off = 0; off < n; off += max_grid) {
         const int64_t m = std::min(max_grid, n - off);
         // copy-only lists need no LDS tile: more workgroups per CU
         const size_t lds = a.any_transpose ? S::lds_bytes : 0;
-        hipLaunchKernelGGL((tile_kernel<T, S>), dim3(unsigned(m)), dim3(S::NT), lds, stream,
+        hipLaunchKernelGGL((tile_kernel<T, S, MODE>), dim3(unsigned(m)), dim3(S::NT), lds, stream,
                            a.ops, work + off, a.src_base, a.dst_base,
                            static_cast<const T*>(a.scalars));
     }
+}
+// the large shapes of real types with the large_mode variants (lists with unaligned destinations)
+template <typename T, typename S>
+void launch_large(const launch_args& a, hipStream_t stream) {
+    if constexpr (std::is_same<T, float>::value || std::is_same<T, double>::value) {
+        switch (a.large_mode) {
+        case 1: return launch_shape<T, S, 1>(a, a.work, a.n_large, stream);
+        case 2: return launch_shape<T, S, 2>(a, a.work, a.n_large, stream);
+        case 3: return launch_shape<T, S, 3>(a, a.work, a.n_large, stream);
+        default: break;
+        }
+    }
+    launch_shape<T, S>(a, a.work, a.n_large, stream);
 }
 
 template <typename T>
@@ -916,9 +1102,9 @@ void launch_t(const launch_args& a, hipStream_t stream) {
     } else if (a.tr_shape && a.full)
         launch_shape<T, typename shapes<T>::large_tr_full>(a, a.work, a.n_large, stream);
     else if (a.tr_shape)
-        launch_shape<T, typename shapes<T>::large_tr>(a, a.work, a.n_large, stream);
+        launch_large<T, typename shapes<T>::large_tr>(a, stream);
     else
-        launch_shape<T, typename shapes<T>::large>(a, a.work, a.n_large, stream);
+        launch_large<T, typename shapes<T>::large>(a, stream);
     if (a.n_medium > 0 && a.med_sq) {  // the medium class on 32 x 32 sub-tiles (nb = 32 blocks)
         if (!a.tr_shape) throw error(COSTA_ERR_INTERNAL, "costa: 32 x 32 shape");
         launch_shape<T, typename shapes<T>::small32_tr>(a, a.work + a.n_large, a.n_medium, stream);
@@ -929,6 +1115,7 @@ void launch_t(const launch_args& a, hipStream_t stream) {
         else
             launch_shape<T, typename shapes<T>::medium_tr>(a, a.work + a.n_large, a.n_medium, stream);
     }
+    if (a.n_skew > 0) launch_skew<T>(a, a.work + a.n_large + a.n_medium, a.n_skew, stream);
     launch_tiny<T>(a, stream);
 }
 
@@ -944,6 +1131,10 @@ void shape_of(bool tr, shape_dims* d) {
     d->bs_q = sq ? shapes<T>::small_tr::BS : 0;
     d->bf_s = tr ? shapes<T>::small32_tr::BF : 0;
     d->bs_s = tr ? shapes<T>::small32_tr::BS : 0;
+    constexpr bool skew = std::is_same<T, float>::value || std::is_same<T, double>::value ||
+                          std::is_same<T, int>::value;
+    d->bf_k = tr && skew ? skew_shape<T>::BF : 0;
+    d->bs_k = tr && skew ? skew_shape<T>::BS : 0;
 }
 
 template <typename T, typename S>
@@ -951,9 +1142,22 @@ void set_lds_limit() {
     // the large shapes need more than the default dynamic-LDS limit
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tile_kernel<T, S>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, int(S::lds_bytes));
+    if constexpr (std::is_same<T, float>::value || std::is_same<T, double>::value) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tile_kernel<T, S, 1>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(S::lds_bytes));
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tile_kernel<T, S, 2>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(S::lds_bytes));
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tile_kernel<T, S, 3>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(S::lds_bytes));
+    }
 }
 template <typename T>
 void set_lds_limits() {
+    if constexpr (std::is_same<T, float>::value || std::is_same<T, double>::value ||
+                  std::is_same<T, int>::value)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&skew_kernel<T>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  int(skew_shape<T>::lds_bytes));
     set_lds_limit<T, typename shapes<T>::large>();
     set_lds_limit<T, typename shapes<T>::large_tr>();
     set_lds_limit<T, typename shapes<T>::medium_tr>();
@@ -978,7 +1182,7 @@ void tile_shapes(costa_dtype_t dtype, bool transposing_list, shape_dims* d) {
 }
 
 void launch_tiles(costa_dtype_t dtype, const launch_args& a, void* stream) {
-    if (a.n_large + a.n_medium + a.n_tiny <= 0) return;
+    if (a.n_large + a.n_medium + a.n_skew + a.n_tiny <= 0) return;
     static bool once = [] {
         set_lds_limits<float>();
         set_lds_limits<double>();

@@ -9,7 +9,9 @@ runs on this library:
   * every single-rank golden case, against the reference's outputs bit for bit;
   * 12288^2 fp64 'T' (a 1.2 GB package: an unchunked self send/recv of it lost its second half
     on torch's RCCL), moved in the default 256 MiB pieces, or in pieces of the
-    largest size the library allows when COSTA_MAX_MSG_BYTES asks for more.
+    largest size the library allows when COSTA_MAX_MSG_BYTES asks for more;
+  * 23168^2 fp64 'N' with 128^2 blocks: a 4.29 GB package, BASELINE cfg 3's per-peer size, in
+    17 pieces over 4 exchange rounds.
 Prints 'COSTA_RCCL <version> <library path>' and a final 'OK <cases>' or 'FAIL ...' lines."""
 import ctypes as C
 import os
@@ -100,12 +102,27 @@ def main():
     if not np.array_equal(got.reshape(m, m), a.reshape(m, m).T):
         half = got.reshape(m, m)[m // 2:]
         bad.append(f"{m}^2 fp64 T (second half zero: {bool((half == 0).all())})")
+    hip.free(pa)
+    hip.free(pc)
+    # a BASELINE cfg 3-sized package: 23168^2 fp64 'N' (128^2 blocks), 4.29 GB to "the peer" =
+    # 17 pieces of <= 256 MiB in 4 exchange rounds (engine.cpp round_range / max_message_bytes)
+    m = 23168
+    a = np.arange(m * m, dtype=np.float64)
+    pa, pc = hip.upload(a), hip.upload(np.zeros(m * m))
+    LA = costa.block_cyclic_layout(m, m, 128, 128, 1, 1, m, m, 1, 1, "R", 0, 0, pa, m, "C", 0)
+    LC = costa.block_cyclic_layout(m, m, 128, 128, 1, 1, m, m, 1, 1, "R", 0, 0, pc, m, "C", 0)
+    costa.transform(LA, LC, comm, "N", 1.0, 0.0)
+    got = hip.download(pc, a)
+    if not np.array_equal(got, a):
+        bad.append(f"{m}^2 fp64 N: {int((got != a).sum())} elements differ")
+    hip.free(pa)
+    hip.free(pc)
     st = costa.get_stats()
     if st["pack_launches"] < n + 1 or st["unpack_launches"] < n + 1 or st["local_launches"]:
         bad.append(f"not every case went through the exchange: {st}")
     for b in bad:
         print("FAIL", b)
-    print("OK" if not bad else "BAD", n + 1)
+    print("OK" if not bad else "BAD", n + 2)
     return 1 if bad else 0
 
 

@@ -298,3 +298,27 @@ def test_plan_cache_reuse(gpu):
     assert r1[0].tobytes() == r2[0].tobytes()
     s = gpu.get_stats()
     assert s["transforms"] == 2
+
+
+@pytest.mark.parametrize("dtype,lda,ldc", [(1, 16385, 16385), (1, 16384, 16387), (0, 16386, 16385),
+                                           (0, 16387, 16386), (4, 16385, 16387)],
+                         ids=["f64-odd", "f64-dst-odd", "f32-2-1", "f32-3-2", "i32-1-3"])
+def test_unaligned_lld_full_size(gpu, dtype, lda, ldc):
+    """a ScaLAPACK-sized 'T' with leading dimensions off the 16-byte grid (lld = LOCr + pad):
+    the large shape re-cuts its stores into aligned chunks across lanes (store_shifted);
+    C == A^T bit for bit, padding rows untouched"""
+    n, b = 16384, 256
+    tdt = {0: torch.float32, 1: torch.float64, 4: torch.int32}[dtype]
+    if tdt == torch.int32:
+        A = torch.randint(-2**31, 2**31 - 1, (n, lda), dtype=torch.int32, device="cuda")
+    else:
+        A = torch.randn(n, lda, dtype=tdt, device="cuda")
+    Cm = torch.full((n, ldc), 7, dtype=tdt, device="cuda")
+    LA = gpu.block_cyclic_layout(n, n, b, b, 1, 1, n, n, 1, 1, "R", 0, 0, A.data_ptr(), lda, "C", 0,
+                                 dtype=dtype)
+    LC = gpu.block_cyclic_layout(n, n, b, b, 1, 1, n, n, 1, 1, "R", 0, 0, Cm.data_ptr(), ldc, "C", 0,
+                                 dtype=dtype)
+    gpu.transform(LA, LC, gpu.Comm.self(0), "T", 1, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(Cm[:, :n], A[:, :n].t())
+    assert bool((Cm[:, n:] == 7).all())

@@ -16,17 +16,18 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import costa_amd as costa  # noqa: E402
 
 
-def run(dtype, n, b, lld, steps, comm):
+def run(dtype, n, b, lld, steps, comm, lldc=None):
+    lldc = lldc or lld
     tdt = {costa.DOUBLE: torch.float64, costa.FLOAT: torch.float32}[dtype]
     es = torch.tensor([], dtype=tdt).element_size()
     A = torch.rand(lld * n, dtype=tdt, device="cuda")
-    C = torch.zeros(lld * n, dtype=tdt, device="cuda")
+    C = torch.zeros(lldc * n, dtype=tdt, device="cuda")
     LA = costa.block_cyclic_layout(n, n, b, b, 1, 1, n, n, 1, 1, "R", 0, 0, A.data_ptr(), lld, "C", 0,
                                    dtype=dtype)
-    LC = costa.block_cyclic_layout(n, n, b, b, 1, 1, n, n, 1, 1, "R", 0, 0, C.data_ptr(), lld, "C", 0,
+    LC = costa.block_cyclic_layout(n, n, b, b, 1, 1, n, n, 1, 1, "R", 0, 0, C.data_ptr(), lldc, "C", 0,
                                    dtype=dtype)
     costa.transform(LA, LC, comm, "T", 1.0, 0.0)
-    ok = torch.equal(C.view(n, lld)[:, :n], A.view(n, lld)[:, :n].t())
+    ok = torch.equal(C.view(n, lldc)[:, :n], A.view(n, lld)[:, :n].t())
     for _ in range(3):
         costa.transform_async(LA, LC, comm, "T", 1.0, 0.0)
     costa.synchronize(comm)
@@ -40,7 +41,7 @@ def run(dtype, n, b, lld, steps, comm):
     ms = st["local_ms"] / steps
     gbps = 2 * n * n * es / (ms * 1e-3) / 1e9
     name = "fp64" if dtype == costa.DOUBLE else "fp32"
-    print(f"{name} {n}^2 blocks {b}^2 lld {lld}: kernel {ms:.4f} ms  {gbps:8.1f} GB/s  "
+    print(f"{name} {n}^2 blocks {b}^2 lld {lld}/{lldc}: kernel {ms:.4f} ms  {gbps:8.1f} GB/s  "
           f"launches/step {st['local_launches'] / steps:.0f}  {'ok' if ok else 'WRONG'}", flush=True)
     del A, C, LA, LC
     costa.release_caches()
@@ -52,6 +53,11 @@ def main():
     costa.lib()
     comm = costa.Comm.self(0)
     n = 16384
+    if len(sys.argv) > 2 and sys.argv[2] == "sides":  # one side misaligned at a time
+        for dtype, odd in ((costa.DOUBLE, 16385), (costa.FLOAT, 16386)):
+            for la, lc in ((16384, 16384), (odd, 16384), (16384, odd), (odd, odd)):
+                run(dtype, n, 256, la, steps, comm, lc)
+        return
     for dtype, llds in ((costa.DOUBLE, (16384, 16385)), (costa.FLOAT, (16384, 16385, 16386))):
         for b in (512, 256, 128):
             for lld in llds:

@@ -11,8 +11,9 @@
 //     * two builds give byte-identical lists (the threaded cut is deterministic).
 //   a sub-list of every 8th cfg 5 op (what one exchange round's pack / unpack list looks like:
 //     hints sparse in the list, so the comparison sort replaces the counting sort): the same.
-//   unaligned large ops (fp32, lld % 4 != 0): ops up to kUnalignedWaveCap large sub-tiles are cut
-//     into wavefront pieces (the same checks), bigger ones stay on the large shape.
+//   unaligned large ops (fp32, lld % 4 != 0): transposes into unaligned destinations take the
+//     skew shape; other ops up to kUnalignedWaveCap large sub-tiles are cut into wavefront
+//     pieces (the same checks), bigger ones stay on the large shape.
 // Prints "ok" and exits 0, or prints the first violation and exits 1.
 #include <cstdio>
 #include <cstring>
@@ -69,16 +70,24 @@ static int64_t expected_shaped(costa_dtype_t dt, const std::vector<costa_tile_op
     tile_shapes(dt, tr, &sh);
     const int64_t E = int64_t(dtype_size(dt)), big = int64_t(sh.bf) * sh.bs, med = int64_t(sh.bf_m) * sh.bs_m;
     const uint32_t both = COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST;
-    int64_t n_large = 0, n_med = 0;
+    int64_t n_large = 0, n_med = 0, n_skew = 0;
+    const int64_t skew_elems = int64_t(sh.bf_k) * sh.bs_k;
     for (const auto& o : ops) {
         const int64_t e = int64_t(o.nf) * o.ns;
         const bool al = (o.flags & both) == both, t = o.flags & COSTA_TILE_TRANSPOSE;
+        const uint32_t kind = (o.flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT;
+        // transposes into unaligned destinations: the skew shape (engine.cpp build_work)
+        if (skew_elems > 0 && e > 0 && t && !(o.flags & COSTA_TILE_VEC_DST) && kind != COSTA_SCALE_AXPBY &&
+            o.dst % uint64_t(E) == 0 && 2 * e >= skew_elems) {
+            ++n_skew;
+            continue;
+        }
         const bool tiny = (t ? int64_t(o.nf | 1) * o.ns * E <= tiny_lds_budget() : e * E <= tiny_copy_budget(E));
         const bool large = 2 * e >= big && (al || e > kUnalignedWaveCap * big) && !tiny;
         n_large += large;
         n_med += !large && med > 0 && al && t && 2 * e >= med;
     }
-    return n_large + (n_med >= 4096 ? n_med : 0);  // engine.cpp kMinMediumOps
+    return n_large + n_skew + (n_med >= 4096 ? n_med : 0);  // engine.cpp kMinMediumOps
 }
 
 // `ops` must carry unique, non-zero hints; expect_large: ops that must go to a sub-tiled shape
@@ -172,8 +181,13 @@ int main() {
         auto p = plan_of(ea, ec, 'T', 1.f, 0.f);
         shape_dims sh;
         tile_shapes(COSTA_FLOAT, true, &sh);  // a transposing list
-        const int64_t elems = int64_t(nb) * nb, sub_elems = int64_t(sh.bf) * sh.bs;
-        const int64_t expect = elems > kUnalignedWaveCap * sub_elems ? int64_t(p->local_ops.size()) : 0;
+        // every op transposes into unaligned destination columns: the skew shape, whatever its size
+        const int64_t expect = expected_shaped(p->dtype, p->local_ops);
+        if (expect != int64_t(p->local_ops.size())) {
+            std::printf("FAIL unaligned %d^2 blocks: %lld of %zu ops expected on the skew shape\n", nb,
+                        (long long)expect, p->local_ops.size());
+            return 1;
+        }
         if (!check_list("unaligned " + std::to_string(nb) + "^2 blocks", p->dtype, p->local_ops, expect))
             return 1;
     }
