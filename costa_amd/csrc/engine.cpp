@@ -458,6 +458,49 @@ void merge_row_bands(const std::vector<const costa_tile_op_t*>& ops, int h, std:
     perm.swap(out);
 }
 
+// Merges ops that continue each other: the op whose source starts where op a's source ends along
+// s (a.src + a.ns * lds) and whose destination continues a's the same way (one destination
+// stride further for copies, ns elements further for transposes), with the same extent along f,
+// strides and flags, joins a (then the same along f).  Same elements, same transform: only the
+// op boundaries move.  Order hint: the smaller one.
+void merge_adjacent(std::vector<costa_tile_op_t>& v, int64_t E) {
+    if (v.size() < 2) return;
+    for (int pass = 0; pass < 2; ++pass) {  // 0: along s, 1: along f
+        std::unordered_map<uint64_t, uint32_t> by_src;
+        by_src.reserve(v.size() * 2);
+        for (size_t i = 0; i < v.size(); ++i) by_src.emplace(v[i].src, uint32_t(i));
+        std::vector<char> gone(v.size(), 0);
+        std::vector<uint32_t> idx(v.size());
+        for (size_t i = 0; i < v.size(); ++i) idx[i] = uint32_t(i);
+        std::sort(idx.begin(), idx.end(), [&](uint32_t x, uint32_t y) { return v[x].src < v[y].src; });
+        for (const uint32_t i : idx) {
+            if (gone[i]) continue;
+            costa_tile_op_t& a = v[i];
+            const bool tr = a.flags & COSTA_TILE_TRANSPOSE;
+            for (;;) {
+                const int64_t n = pass == 0 ? a.ns : a.nf;
+                const uint64_t next_src = a.src + uint64_t(pass == 0 ? n * a.lds * E : n * E);
+                const uint64_t next_dst =
+                    a.dst + uint64_t(pass == 0 ? (tr ? n : n * a.ldd) * E : (tr ? n * a.ldd : n) * E);
+                const auto it = by_src.find(next_src);
+                if (it == by_src.end() || gone[it->second] || it->second == i) break;
+                const costa_tile_op_t& b = v[it->second];
+                const bool same = b.dst == next_dst && b.flags == a.flags && b.lds == a.lds &&
+                                  b.ldd == a.ldd && (pass == 0 ? b.nf == a.nf : b.ns == a.ns);
+                const int64_t total = n + (pass == 0 ? b.ns : b.nf);
+                if (!same || total > (int64_t(1) << 30)) break;
+                (pass == 0 ? a.ns : a.nf) = int32_t(total);
+                a.order = std::min(a.order ? a.order : b.order, b.order ? b.order : a.order);
+                gone[it->second] = 1;
+            }
+        }
+        size_t o = 0;
+        for (size_t i = 0; i < v.size(); ++i)
+            if (!gone[i]) v[o++] = v[i];
+        v.resize(o);
+    }
+}
+
 // runs fn(begin, end) over [0, n) on up to 8 host threads (one when n is small)
 template <typename F>
 void host_parallel(size_t n, F fn) {
@@ -534,17 +577,26 @@ const wave_knobs& knobs() {
 work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops_in,
                       std::vector<costa_tile_op_t>& ordered, std::vector<uint64_t>& work,
                       bool pack_list) {
-    // COSTA_MISALIGNED_VEC (tuning only): 1 / 2 / 3 = treat dword-aligned destinations / sources
-    // / both as vector-aligned (16-byte accesses at 4-byte alignment)
-    static const int mis = [] {
+    // Sources off the 16-byte grid: 4-byte elements are read as 16-byte vectors anyway (dword
+    // alignment suffices for global_load_dwordx4): fp32 16384^2 'T' with lld 16386 0.405 against
+    // 0.499 ms element by element; 8-byte elements stay element-wise (0.794 against 0.755 ms);
+    // misaligned 16-byte stores lost for both (tools/unaligned_mis.sh, profiles/r3/).
+    // COSTA_MISALIGNED_VEC (tuning): bit 0 destinations, bit 1 sources, for every element size.
+    static const int mis_env = [] {
         const char* s = std::getenv("COSTA_MISALIGNED_VEC");
-        return s ? std::atoi(s) : 0;
+        return s ? std::atoi(s) : -1;
     }();
+    // (by default only for ops of at least one large sub-tile: smaller ones keep their class)
+    const int mis = mis_env >= 0 ? mis_env : dtype_size(dtype) == 4 ? 2 : 0;
     std::vector<costa_tile_op_t> ops_mis;
     if (mis) {
         ops_mis = ops_in;
         const uint64_t E = dtype_size(dtype);
+        shape_dims shm;
+        tile_shapes(dtype, any_transpose(ops_in), &shm);
+        const int64_t min_elems = mis_env >= 0 ? 0 : int64_t(shm.bf) * shm.bs;
         for (auto& op : ops_mis) {
+            if (int64_t(op.nf) * op.ns < min_elems) continue;
             if ((mis & 1) && op.dst % 4 == 0 && (uint64_t(op.ldd) * E) % 4 == 0) op.flags |= COSTA_TILE_VEC_DST;
             if ((mis & 2) && op.src % 4 == 0 && (uint64_t(op.lds) * E) % 4 == 0) op.flags |= COSTA_TILE_VEC_SRC;
         }
@@ -657,12 +709,18 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         cls[li] = 4;
     }
     std::vector<uint32_t> shaped[3];  // [0] large, [1] medium, [2] skew
+    std::vector<costa_tile_op_t> skew_ops;
     for (size_t li = 0; li < ops.size(); ++li) {
         const int c = cls[li] == 1 && n_med < kMinMediumOps ? 2 : cls[li];
         if (c < 2) shaped[c].push_back(uint32_t(li));
         else if (c == 2) wave_ops.push_back(&ops[li]);
-        else if (c == 4) shaped[2].push_back(uint32_t(li));
+        else if (c == 4) skew_ops.push_back(ops[li]);
     }
+    // skew ops that continue each other in source and destination (the tiles of one local
+    // matrix) become one op: a tile edge inside a destination column would otherwise be a
+    // partial granule shared by two workgroups again
+    merge_adjacent(skew_ops, E);
+    for (size_t i = 0; i < skew_ops.size(); ++i) shaped[2].push_back(uint32_t(i));
     // each shape's ops in hint order when every one carries a hint; lists whose shaped ops all
     // transpose 8-byte elements then take the sub-tiles in destination-address order (wave_knobs)
     int64_t n_work[3] = {0, 0, 0};
@@ -670,19 +728,20 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         const int bf = c == 2 ? sh.bf_k : c ? (med_sq ? sh.bf_s : sh.bf_m) : sq ? sh.bf_q : sh.bf;
         const int bs = c == 2 ? sh.bs_k : c ? (med_sq ? sh.bs_s : sh.bs_m) : sq ? sh.bs_q : sh.bs;
         const std::vector<uint32_t>& sel = shaped[c];
+        const std::vector<costa_tile_op_t>& src_ops = c == 2 ? skew_ops : ops;
         std::vector<uint32_t> sperm(sel.size());
         for (size_t i = 0; i < sel.size(); ++i) sperm[i] = uint32_t(i);
         if (kn.large_sort >= 1 && !sel.empty()) {
             bool hints = true;
-            for (uint32_t li : sel) hints = hints && ops[li].order != 0;
+            for (uint32_t li : sel) hints = hints && src_ops[li].order != 0;
             if (hints)
                 std::stable_sort(sperm.begin(), sperm.end(), [&](uint32_t x, uint32_t y) {
-                    return ops[sel[x]].order < ops[sel[y]].order;
+                    return src_ops[sel[x]].order < src_ops[sel[y]].order;
                 });
         }
         const size_t op0 = ordered.size(), w0 = work.size();
         for (const uint32_t k : sperm) {
-            const costa_tile_op_t& op = ops[sel[k]];
+            const costa_tile_op_t& op = src_ops[sel[k]];
             const uint64_t i = ordered.size();
             if (i > 0xFFFFFFFFull) throw error(COSTA_ERR_ARG, "costa: too many tiles in one list");
             ordered.push_back(op);

@@ -31,13 +31,19 @@ constexpr long SEG = 1024;     // segment bytes
 constexpr int S = 16;          // columns per workgroup
 
 // W = 16: 16-byte stores, W = 8: 8-byte stores (two per loaded vector)
-template <int W, bool NT, bool XCD = false>
+// XCD: 0 = blocks in order (round-robin over the 8 XCDs), -1 = each XCD a contiguous slice of
+// the grid, R > 0 = runs of R consecutive segments per XCD inside every group of 8 R (the
+// in-flight window stays one contiguous range; neighbours inside a run meet in one L2)
+template <int W, bool NT, int XCD = 0>
 __global__ __launch_bounds__(256) void k_copy(const char* a, char* c) {
     constexpr long SPC = COLB / SEG;
     long w = blockIdx.x;
-    if (XCD) {  // XCD x of 8 walks one contiguous slice: neighbouring segments meet in one L2
+    if (XCD < 0) {
         const long nb = gridDim.x, x = w % 8, per = nb / 8, i = w / 8;
         w = x * per + i;
+    } else if (XCD > 0) {
+        const long grp = w / (8 * XCD), in = w % (8 * XCD), x = in % 8, slot = in / 8;
+        w = grp * (8 * XCD) + x * XCD + slot;
     }
     const long g = w / SPC, q = w % SPC;
     const long base = g * S * COLB + q * SEG;
@@ -92,11 +98,19 @@ int main(int argc, char** argv) {
     std::vector<variant> vs = {
         {"16B nt  off 0", 0, r16nt},   {"16B nt  off 128", 128, r16nt}, {"16B nt  off 16", 16, r16nt},
         {"16B nt  off 64", 64, r16nt}, {"16B def off 0", 0, r16},       {"16B def off 16", 16, r16},
+        {"16B nt  off 32", 32, r16nt}, {"16B nt  off 48", 48, r16nt},   {"16B nt  off 96", 96, r16nt},
         {"8B  nt  off 0", 0, r8nt},    {"8B  nt  off 8", 8, r8nt},      {"8B  def off 8", 8, r8},
-        {"16B xcd nt off 0", 0, [](const char* a, char* c, unsigned b) { hipLaunchKernelGGL((k_copy<16, true, true>), dim3(b), dim3(256), 0, 0, a, c); }},
-        {"16B xcd nt off 16", 16, [](const char* a, char* c, unsigned b) { hipLaunchKernelGGL((k_copy<16, true, true>), dim3(b), dim3(256), 0, 0, a, c); }},
-        {"16B xcd def off 16", 16, [](const char* a, char* c, unsigned b) { hipLaunchKernelGGL((k_copy<16, false, true>), dim3(b), dim3(256), 0, 0, a, c); }},
-        {"8B xcd def off 8", 8, [](const char* a, char* c, unsigned b) { hipLaunchKernelGGL((k_copy<8, false, true>), dim3(b), dim3(256), 0, 0, a, c); }},
+        {"16B xcd nt off 0", 0, [](const char* a, char* c, unsigned b) { hipLaunchKernelGGL((k_copy<16, true, -1>), dim3(b), dim3(256), 0, 0, a, c); }},
+        {"16B xcd def off 16", 16, [](const char* a, char* c, unsigned b) { hipLaunchKernelGGL((k_copy<16, false, -1>), dim3(b), dim3(256), 0, 0, a, c); }},
+        {"16B r2 nt off 0", 0, [](const char* a, char* c, unsigned b) { hipLaunchKernelGGL((k_copy<16, true, 2>), dim3(b), dim3(256), 0, 0, a, c); }},
+        {"16B r2 def off 16", 16, [](const char* a, char* c, unsigned b) { hipLaunchKernelGGL((k_copy<16, false, 2>), dim3(b), dim3(256), 0, 0, a, c); }},
+        {"16B r4 nt off 0", 0, [](const char* a, char* c, unsigned b) { hipLaunchKernelGGL((k_copy<16, true, 4>), dim3(b), dim3(256), 0, 0, a, c); }},
+        {"16B r4 def off 0", 0, [](const char* a, char* c, unsigned b) { hipLaunchKernelGGL((k_copy<16, false, 4>), dim3(b), dim3(256), 0, 0, a, c); }},
+        {"16B r4 def off 16", 16, [](const char* a, char* c, unsigned b) { hipLaunchKernelGGL((k_copy<16, false, 4>), dim3(b), dim3(256), 0, 0, a, c); }},
+        {"16B r4 nt off 16", 16, [](const char* a, char* c, unsigned b) { hipLaunchKernelGGL((k_copy<16, true, 4>), dim3(b), dim3(256), 0, 0, a, c); }},
+        {"16B r8 def off 16", 16, [](const char* a, char* c, unsigned b) { hipLaunchKernelGGL((k_copy<16, false, 8>), dim3(b), dim3(256), 0, 0, a, c); }},
+        {"16B r16 def off 16", 16, [](const char* a, char* c, unsigned b) { hipLaunchKernelGGL((k_copy<16, false, 16>), dim3(b), dim3(256), 0, 0, a, c); }},
+        {"8B r4 def off 8", 8, [](const char* a, char* c, unsigned b) { hipLaunchKernelGGL((k_copy<8, false, 4>), dim3(b), dim3(256), 0, 0, a, c); }},
     };
     std::vector<std::vector<float>> t(vs.size());
     for (int r = 0; r < reps; ++r)

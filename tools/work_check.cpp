@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <set>
 #include <random>
 #include <string>
 #include <vector>
@@ -60,46 +61,60 @@ static grid_layout<float> layout(const std::vector<int>& rs, const std::vector<i
         }                                              \
     } while (0)
 
-// the shaped ops (large or medium sub-tiles) the classification rules give: aligned ops of at
-// least half a large sub-tile, unaligned ones above kUnalignedWaveCap sub-tiles, and in lists
-// that transpose, aligned transposing ops of at least half a medium sub-tile
-static int64_t expected_shaped(costa_dtype_t dt, const std::vector<costa_tile_op_t>& ops) {
+// hints of the ops the classification rules put on a sub-tiled shape: aligned ops of at least
+// half a large sub-tile, unaligned ones above kUnalignedWaveCap sub-tiles, transposes into
+// unaligned destinations (the skew shape, engine.cpp build_work), and in lists that transpose,
+// aligned transposing ops of at least half a medium sub-tile
+static std::set<uint32_t> expected_shaped(costa_dtype_t dt, const std::vector<costa_tile_op_t>& ops) {
     bool tr = false;
     for (const auto& o : ops) tr = tr || (o.flags & COSTA_TILE_TRANSPOSE);
     shape_dims sh;
     tile_shapes(dt, tr, &sh);
     const int64_t E = int64_t(dtype_size(dt)), big = int64_t(sh.bf) * sh.bs, med = int64_t(sh.bf_m) * sh.bs_m;
     const uint32_t both = COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST;
-    int64_t n_large = 0, n_med = 0, n_skew = 0;
     const int64_t skew_elems = int64_t(sh.bf_k) * sh.bs_k;
-    for (const auto& o : ops) {
+    std::set<uint32_t> large, medium;
+    for (const auto& o0 : ops) {
+        costa_tile_op_t o = o0;
         const int64_t e = int64_t(o.nf) * o.ns;
+        // 4-byte sources off the grid read as 16-byte vectors (engine.cpp build_work), ops of at
+        // least one large sub-tile
+        if (E == 4 && e >= big && o.src % 4 == 0) o.flags |= COSTA_TILE_VEC_SRC;
         const bool al = (o.flags & both) == both, t = o.flags & COSTA_TILE_TRANSPOSE;
         const uint32_t kind = (o.flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT;
-        // transposes into unaligned destinations: the skew shape (engine.cpp build_work)
         if (skew_elems > 0 && e > 0 && t && !(o.flags & COSTA_TILE_VEC_DST) && kind != COSTA_SCALE_AXPBY &&
             o.dst % uint64_t(E) == 0 && 2 * e >= skew_elems) {
-            ++n_skew;
+            large.insert(o.order);
             continue;
         }
         const bool tiny = (t ? int64_t(o.nf | 1) * o.ns * E <= tiny_lds_budget() : e * E <= tiny_copy_budget(E));
-        const bool large = 2 * e >= big && (al || e > kUnalignedWaveCap * big) && !tiny;
-        n_large += large;
-        n_med += !large && med > 0 && al && t && 2 * e >= med;
+        const bool lg = 2 * e >= big && (al || e > kUnalignedWaveCap * big) && !tiny;
+        if (lg) large.insert(o.order);
+        else if (med > 0 && al && t && 2 * e >= med) medium.insert(o.order);
     }
-    return n_large + n_skew + (n_med >= 4096 ? n_med : 0);  // engine.cpp kMinMediumOps
+    if (medium.size() >= 4096) large.insert(medium.begin(), medium.end());  // engine.cpp kMinMediumOps
+    return large;
+}
+
+static int64_t big_elems(costa_dtype_t dt, const std::vector<costa_tile_op_t>& ops) {
+    bool tr = false;
+    for (const auto& o : ops) tr = tr || (o.flags & COSTA_TILE_TRANSPOSE);
+    shape_dims sh;
+    tile_shapes(dt, tr, &sh);
+    return int64_t(sh.bf) * sh.bs;
 }
 
 // `ops` must carry unique, non-zero hints; expect_large: ops that must go to a sub-tiled shape
 static bool check_list(const std::string& name, costa_dtype_t dt, const std::vector<costa_tile_op_t>& ops,
-                       int64_t expect_large_ops, bool pack = false) {
+                       const std::set<uint32_t>& shaped, bool pack = false) {
     const int64_t E = int64_t(dtype_size(dt));
     std::vector<costa_tile_op_t> ord, ord2;
     std::vector<uint64_t> work, work2;
     const work_split w = build_work(dt, ops, ord, work, pack);
     build_work(dt, ops, ord2, work2, pack);
-    CHECK(w.tiny_first == expect_large_ops, "%lld ops on the large shape, expected %lld",
-          (long long)w.tiny_first, (long long)expect_large_ops);
+    // (skew ops that continue each other are merged: fewer shaped ops than parents)
+    CHECK(w.tiny_first <= int64_t(shaped.size()) && (w.tiny_first == 0) == shaped.empty(),
+          "%lld ops on the sub-tiled shapes, expected %zu", (long long)w.tiny_first, shaped.size());
     CHECK(ord.size() == ord2.size() && work == work2 &&
               std::memcmp(ord.data(), ord2.data(), ord.size() * sizeof(costa_tile_op_t)) == 0,
           "two builds differ");
@@ -107,13 +122,23 @@ static bool check_list(const std::string& name, costa_dtype_t dt, const std::vec
     for (const auto& o : ops) CHECK(o.order > 0 && parent.emplace(o.order, &o).second, "hint %u not unique", o.order);
     std::map<uint32_t, int64_t> area;
     int restarts = 0;  // the large ops, then the medium ones: each run whole, in hint order
+    int64_t shaped_area = 0, want_area = 0;
+    for (const auto& o : ops)
+        if (shaped.count(o.order)) want_area += int64_t(o.nf) * o.ns;
     for (int64_t i = 0; i < w.tiny_first; ++i) {
         const costa_tile_op_t& s = ord[size_t(i)];
-        CHECK(parent.count(s.order) && std::memcmp(&s, parent[s.order], sizeof(s)) == 0, "shaped op %lld", (long long)i);
+        CHECK(parent.count(s.order) && shaped.count(s.order), "shaped op %lld has no shaped parent", (long long)i);
+        costa_tile_op_t q = *parent[s.order];
+        if (E == 4 && int64_t(q.nf) * q.ns >= big_elems(dt, ops) && q.src % 4 == 0) q.flags |= COSTA_TILE_VEC_SRC;
+        const bool merged = s.src == q.src && s.dst == q.dst && s.flags == q.flags && s.lds == q.lds &&
+                            s.ldd == q.ldd && s.nf >= q.nf && s.ns >= q.ns && (s.flags & COSTA_TILE_TRANSPOSE);
+        CHECK(std::memcmp(&s, &q, sizeof(s)) == 0 || merged, "shaped op %lld", (long long)i);
         restarts += i > 0 && ord[size_t(i) - 1].order > s.order;
-        CHECK(restarts <= 1, "shaped op %lld out of hint order", (long long)i);
-        area[s.order] += int64_t(s.nf) * s.ns;
+        CHECK(restarts <= 2, "shaped op %lld out of hint order", (long long)i);
+        shaped_area += int64_t(s.nf) * s.ns;
     }
+    CHECK(shaped_area == want_area, "shaped ops cover %lld of %lld elements", (long long)shaped_area,
+          (long long)want_area);
     uint64_t last_key = 0;
     for (int64_t i = w.tiny_first; i < w.tiny_first + w.n_tiny; ++i) {
         const costa_tile_op_t& s = ord[size_t(i)];
@@ -135,8 +160,8 @@ static bool check_list(const std::string& name, costa_dtype_t dt, const std::vec
         last_key = key;
     }
     for (const auto& o : ops)
-        CHECK(area[o.order] == int64_t(o.nf) * o.ns, "op %u: pieces cover %lld of %lld", o.order,
-              (long long)area[o.order], (long long)(int64_t(o.nf) * o.ns));
+        CHECK(shaped.count(o.order) || area[o.order] == int64_t(o.nf) * o.ns, "op %u: pieces cover %lld of %lld",
+              o.order, (long long)area[o.order], (long long)(int64_t(o.nf) * o.ns));
     std::printf("%s: %zu ops -> %lld large, %lld pieces\n", name.c_str(), ops.size(),
                 (long long)w.tiny_first, (long long)w.n_tiny);
     return true;
@@ -159,7 +184,7 @@ int main() {
     elayout a = erase(LA), c = erase(LC);
     for (char op : {'N', 'T'}) {
         auto p = plan_of(a, c, op, op == 'N' ? 1.f : -0.5f, op == 'N' ? 0.f : 2.f);
-        const int64_t shaped = expected_shaped(p->dtype, p->local_ops);
+        const std::set<uint32_t> shaped = expected_shaped(p->dtype, p->local_ops);
         if (!check_list(std::string("cfg5 ") + op, p->dtype, p->local_ops, shaped)) return 1;
         // one exchange round's share of a list: every 8th op (hints sparse)
         std::vector<costa_tile_op_t> sub;
@@ -182,10 +207,10 @@ int main() {
         shape_dims sh;
         tile_shapes(COSTA_FLOAT, true, &sh);  // a transposing list
         // every op transposes into unaligned destination columns: the skew shape, whatever its size
-        const int64_t expect = expected_shaped(p->dtype, p->local_ops);
-        if (expect != int64_t(p->local_ops.size())) {
-            std::printf("FAIL unaligned %d^2 blocks: %lld of %zu ops expected on the skew shape\n", nb,
-                        (long long)expect, p->local_ops.size());
+        const std::set<uint32_t> expect = expected_shaped(p->dtype, p->local_ops);
+        if (expect.size() != p->local_ops.size()) {
+            std::printf("FAIL unaligned %d^2 blocks: %zu of %zu ops expected on the skew shape\n", nb,
+                        expect.size(), p->local_ops.size());
             return 1;
         }
         if (!check_list("unaligned " + std::to_string(nb) + "^2 blocks", p->dtype, p->local_ops, expect))
