@@ -859,15 +859,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     w.n_large = n_work[0];
     w.n_medium = n_work[1];
     w.n_skew = n_work[2];
-    {
-        static const int mode = [] {  // COSTA_MISDST_MODE (tuning)
-            const char* s = std::getenv("COSTA_MISDST_MODE");
-            return s ? std::atoi(s) & 3 : 0;
-        }();
-        bool mis_dst = false;
-        for (const uint32_t li : shaped[0]) mis_dst = mis_dst || !(ops[li].flags & COSTA_TILE_VEC_DST);
-        w.large_mode = mis_dst ? mode : 0;
-    }
+
     w.tiny_first = int64_t(ordered.size());
     w.n_tiny = int64_t(at_piece[nw]);
     const size_t base = ordered.size();
@@ -900,7 +892,6 @@ launch_args make_launch(const work_split& w, const void* d_ordered, const void* 
     a.full = w.full;
     a.med_full = w.med_full;
     a.med_sq = w.med_sq;
-    a.large_mode = w.large_mode;
     return a;
 }
 

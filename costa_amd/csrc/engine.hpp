@@ -194,7 +194,6 @@ struct launch_args {
     bool full;              // work_split::full
     bool med_full;          // work_split::med_full
     bool med_sq;            // work_split::med_sq
-    int large_mode = 0;     // work_split::large_mode
 };
 bool any_transpose(const std::vector<costa_tile_op_t>& ops);
 bool any_axpby(const std::vector<costa_tile_op_t>& ops);
@@ -221,8 +220,6 @@ struct work_split {
                             // of large sub-tiles (the launch may then take fewer threads)
     bool med_full = false;  // the same for the medium ops and the medium sub-tile
     bool med_sq = false;    // the medium class runs on 32 x 32 sub-tiles (bf_s x bs_s)
-    int large_mode = 0;     // large shape, lists with unaligned destinations: bit 0 default-policy
-                            // stores (not nt), bit 1 XCD-contiguous slices of the work list
     int64_t n_items() const { return n_large + n_medium + n_skew + n_tiny; }
 };
 // pack_list: the ops write the dense send package (their destinations are contiguous whatever

@@ -704,9 +704,7 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
     }
 }
 
-// MODE bit 0: default-policy stores instead of nt; bit 1: XCD-contiguous slices of the work list
-// (lists with unaligned destinations, engine.cpp work_split::large_mode)
-template <typename T, typename S, int MODE = 0>
+template <typename T, typename S>
 __global__ __launch_bounds__(S::NT) void tile_kernel(const costa_tile_op_t* __restrict__ ops,
                                                      const uint64_t* __restrict__ work,
                                                      const char* src_base, char* dst_base,
@@ -714,13 +712,7 @@ __global__ __launch_bounds__(S::NT) void tile_kernel(const costa_tile_op_t* __re
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     T* tile = reinterpret_cast<T*>(smem);
     // which sub-tile of which op (wave-uniform: scalar loads)
-    int64_t wi = blockIdx.x;
-    if constexpr ((MODE & 2) != 0) {  // XCD x of 8 walks one contiguous slice of the list
-        const int64_t nb = gridDim.x, x = int64_t(blockIdx.x) % 8, per = nb / 8, rem = nb % 8;
-        const int64_t i = int64_t(blockIdx.x) / 8;
-        wi = x < rem ? x * (per + 1) + i : rem * (per + 1) + (x - rem) * per + i;
-    }
-    const uint64_t w = work[wi];
+    const uint64_t w = work[blockIdx.x];
     const costa_tile_op_t op = ops[w >> 32];
     const uint32_t sub = uint32_t(w);
     const int nbf = (op.nf + S::BF - 1) / S::BF;
@@ -732,7 +724,7 @@ __global__ __launch_bounds__(S::NT) void tile_kernel(const costa_tile_op_t* __re
     const T alpha = scalars[2 * slot];
     const T beta = scalars[2 * slot + 1];
     const uint32_t vec_both = COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST;
-    constexpr bool NT = bool(COSTA_NT_STORES) && (MODE & 1) == 0;
+    constexpr bool NT = bool(COSTA_NT_STORES);
     if (tf == S::BF && ts == S::BS && (op.flags & vec_both) == vec_both)
         run_tile<T, S, true, NT>(op, f0, s0, tf, ts, src_base, dst_base, alpha, beta, tile);
     else
@@ -1079,32 +1071,18 @@ void launch_tiny(const launch_args& a, hipStream_t stream) {
                 : launch_tiny_v<T, TINY_WAVES_COPY, false, false>(a, stream);
 }
 
-template <typename T, typename S, int MODE = 0>
+template <typename T, typename S>
 void launch_shape(const launch_args& a, const uint64_t* work, int64_t n, hipStream_t stream) {
     const int64_t max_grid = 1LL << 30;
     for (int64_t off = 0; off < n; off += max_grid) {
         const int64_t m = std::min(max_grid, n - off);
         // copy-only lists need no LDS tile: more workgroups per CU
         const size_t lds = a.any_transpose ? S::lds_bytes : 0;
-        hipLaunchKernelGGL((tile_kernel<T, S, MODE>), dim3(unsigned(m)), dim3(S::NT), lds, stream,
+        hipLaunchKernelGGL((tile_kernel<T, S>), dim3(unsigned(m)), dim3(S::NT), lds, stream,
                            a.ops, work + off, a.src_base, a.dst_base,
                            static_cast<const T*>(a.scalars));
     }
 }
-// the large shapes of real types with the large_mode variants (lists with unaligned destinations)
-template <typename T, typename S>
-void launch_large(const launch_args& a, hipStream_t stream) {
-    if constexpr (std::is_same<T, float>::value || std::is_same<T, double>::value) {
-        switch (a.large_mode) {
-        case 1: return launch_shape<T, S, 1>(a, a.work, a.n_large, stream);
-        case 2: return launch_shape<T, S, 2>(a, a.work, a.n_large, stream);
-        case 3: return launch_shape<T, S, 3>(a, a.work, a.n_large, stream);
-        default: break;
-        }
-    }
-    launch_shape<T, S>(a, a.work, a.n_large, stream);
-}
-
 template <typename T>
 void launch_t(const launch_args& a, hipStream_t stream) {
     // work list: the large shape's sub-tiles (the list's shape: build_work cut them with
@@ -1115,9 +1093,9 @@ void launch_t(const launch_args& a, hipStream_t stream) {
     } else if (a.tr_shape && a.full)
         launch_shape<T, typename shapes<T>::large_tr_full>(a, a.work, a.n_large, stream);
     else if (a.tr_shape)
-        launch_large<T, typename shapes<T>::large_tr>(a, stream);
+        launch_shape<T, typename shapes<T>::large_tr>(a, a.work, a.n_large, stream);
     else
-        launch_large<T, typename shapes<T>::large>(a, stream);
+        launch_shape<T, typename shapes<T>::large>(a, a.work, a.n_large, stream);
     if (a.n_medium > 0 && a.med_sq) {  // the medium class on 32 x 32 sub-tiles (nb = 32 blocks)
         if (!a.tr_shape) throw error(COSTA_ERR_INTERNAL, "costa: 32 x 32 shape");
         launch_shape<T, typename shapes<T>::small32_tr>(a, a.work + a.n_large, a.n_medium, stream);
@@ -1155,14 +1133,6 @@ void set_lds_limit() {
     // the large shapes need more than the default dynamic-LDS limit
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tile_kernel<T, S>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, int(S::lds_bytes));
-    if constexpr (std::is_same<T, float>::value || std::is_same<T, double>::value) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tile_kernel<T, S, 1>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(S::lds_bytes));
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tile_kernel<T, S, 2>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(S::lds_bytes));
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tile_kernel<T, S, 3>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(S::lds_bytes));
-    }
 }
 template <typename T>
 void set_lds_limits() {
