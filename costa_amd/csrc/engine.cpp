@@ -749,7 +749,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
             if (n > 0xFFFFFFFFull) throw error(COSTA_ERR_ARG, "costa: tile too large");
             for (uint64_t q = 0; q < n; ++q) work.push_back((i << 32) | q);
         }
-        bool by_address = kn.large_sort == 2;
+        bool by_address = kn.large_sort == 2 || kn.large_sort >= 4;
         if (kn.large_sort == 3) {
             by_address = (E == 4 || E == 8) && ordered.size() > op0;
             for (size_t i = op0; i < ordered.size(); ++i)
@@ -764,6 +764,15 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
                 const uint64_t q = wx & 0xFFFFFFFFull, nbf = uint64_t((op.nf + bf - 1) / bf);
                 const int64_t f0 = int64_t(q % nbf) * bf, s0 = int64_t(q / nbf) * bs;
                 const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
+                if (kn.large_sort >= 4 && tr) {
+                    // tuning: COSTA_LARGE_SORT=4+k pairs 2^k f-neighbours (sub-tiles continuing
+                    // each other's source columns) at each destination position
+                    const int64_t span = int64_t(bf) << (kn.large_sort - 3);
+                    const int64_t fp = f0 / span * span;
+                    const uint64_t a = op.dst + uint64_t((fp * op.ldd + s0) * E);
+                    key[x] = {(a << 4) | uint64_t((f0 - fp) / bf), wx};
+                    continue;
+                }
                 key[x] = {op.dst + uint64_t((tr ? f0 * op.ldd + s0 : s0 * op.ldd + f0) * E), wx};
             }
             std::sort(key.begin(), key.end());

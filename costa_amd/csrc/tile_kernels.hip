@@ -88,10 +88,13 @@ __device__ __attribute__((cold)) cpx<R> annex_g_recover(R a, R b, R c, R d) {
     if (!recalc) return {p - q, r + t};
     return {inf * (p - q), inf * (r + t)};
 }
+#ifndef COSTA_ANNEX_G  // 0: naive complex products only (tuning builds: the recovery's cost)
+#define COSTA_ANNEX_G 1
+#endif
 template <typename R>
 __device__ __forceinline__ cpx<R> cmul(cpx<R> z, cpx<R> w) {
     const R x = z.re * w.re - z.im * w.im, y = z.re * w.im + z.im * w.re;
-    if (__builtin_expect(__builtin_isnan(x) && __builtin_isnan(y), 0))
+    if (COSTA_ANNEX_G && __builtin_expect(__builtin_isnan(x) && __builtin_isnan(y), 0))
         return annex_g_recover(z.re, z.im, w.re, w.im);
     return {x, y};
 }
@@ -124,21 +127,30 @@ __device__ __forceinline__ T scale(T x, T y, uint32_t kind, bool conj, T alpha, 
 // (inlined per element it made the 1024-thread c64 shape spill to scratch).
 template <typename T> struct is_cpx { static constexpr bool value = false; };
 template <typename R> struct is_cpx<cpx<R>> { static constexpr bool value = true; };
-template <typename T> __device__ __forceinline__ T e_mul_naive(T a, T b, bool&) { return a * b; }
+// (a product whose parts are both NaN leaves both parts of the result NaN, beta * y + alpha * x
+// included, so checking the result suffices; a NaN result for another reason is redone too,
+// with the same outcome).  Costs cfg 4 (c128 'T', alpha, beta) ~3 %: 2.234 against 2.170 ms
+// with naive products only (COSTA_ANNEX_G=0, profiles/r3/annex_ab.txt); storing unconditionally
+// and fixing up afterwards would keep the old values live and spill.
+template <typename T> __device__ __forceinline__ T e_mul_naive(T a, T b) { return a * b; }
 template <typename R>
-__device__ __forceinline__ cpx<R> e_mul_naive(cpx<R> z, cpx<R> w, bool& bad) {
-    const R x = z.re * w.re - z.im * w.im, y = z.re * w.im + z.im * w.re;
-    bad = bad || (__builtin_isnan(x) && __builtin_isnan(y));
-    return {x, y};
+__device__ __forceinline__ cpx<R> e_mul_naive(cpx<R> z, cpx<R> w) {
+    return {z.re * w.re - z.im * w.im, z.re * w.im + z.im * w.re};
+}
+template <typename T> __device__ __forceinline__ bool both_nan(const T&) { return false; }
+template <typename R> __device__ __forceinline__ bool both_nan(const cpx<R>& v) {
+    return COSTA_ANNEX_G && (v.re != v.re) & (v.im != v.im);
 }
 template <typename T>
 __device__ __forceinline__ T scale_naive(T x, T y, uint32_t kind, bool conj, T alpha, T beta,
                                          bool& bad) {
     if (conj) x = e_conj(x);
-    if (kind == COSTA_SCALE_ZERO) return e_zero<T>();
-    if (kind == COSTA_SCALE_ALPHA) return e_mul_naive(alpha, x, bad);
-    if (kind == COSTA_SCALE_AXPBY) return e_add(e_mul_naive(beta, y, bad), e_mul_naive(alpha, x, bad));
-    return x;  // BITCOPY
+    T r = x;  // BITCOPY
+    if (kind == COSTA_SCALE_ZERO) r = e_zero<T>();
+    else if (kind == COSTA_SCALE_ALPHA) r = e_mul_naive(alpha, x);
+    else if (kind == COSTA_SCALE_AXPBY) r = e_add(e_mul_naive(beta, y), e_mul_naive(alpha, x));
+    bad = bad | both_nan(r);
+    return r;
 }
 
 // ---- cross-lane moves ----
