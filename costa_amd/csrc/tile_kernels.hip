@@ -755,11 +755,21 @@ __global__ __launch_bounds__(S::NT) void tile_kernel(const costa_tile_op_t* __re
 // x, 0 or x: a function of A alone).  The source rows [s0 - G, s0 + BS + G) are staged (odd
 // pitch: the column-wise LDS reads of the store phase are conflict-free); lanes then walk each
 // destination column in element stores, 64 consecutive elements per instruction.
+#ifndef COSTA_SKEW_BF4  // tuning builds: the skew sub-tile of 4- / 8-byte types
+#define COSTA_SKEW_BF4 64
+#define COSTA_SKEW_BS4 256
+#endif
+#ifndef COSTA_SKEW_BF8
+#define COSTA_SKEW_BF8 64
+#define COSTA_SKEW_BS8 128
+#endif
 template <typename T>
 struct skew_shape {
     // BS: 4-byte types 256 (G = 16: the overlap rows stay 1/8 of the sub-tile), 8-byte 128;
     // ~75 KB of LDS either way (two workgroups per CU)
-    static constexpr int NT = 512, BF = 64, BS = sizeof(T) == 4 ? 256 : 128;
+    static constexpr int NT = 512;
+    static constexpr int BF = sizeof(T) == 4 ? COSTA_SKEW_BF4 : COSTA_SKEW_BF8;
+    static constexpr int BS = sizeof(T) == 4 ? COSTA_SKEW_BS4 : COSTA_SKEW_BS8;
     static constexpr int E = int(sizeof(T)), G = 64 / E, RS = BS + 2 * G, P = BF + 1;
     static constexpr int V = 16 / E, LPC = BF / V, CPP = NT / LPC, PL = (RS + CPP - 1) / CPP;
     static constexpr int NW = NT / 64;

@@ -57,6 +57,7 @@ def main():
         for dtype, odd in ((costa.DOUBLE, 16385), (costa.FLOAT, 16386)):
             for la, lc in ((16384, 16384), (odd, 16384), (16384, odd), (odd, odd)):
                 run(dtype, n, 256, la, steps, comm, lc)
+        run(costa.FLOAT, n, 256, 16385, steps, comm, 16385)
         return
     for dtype, llds in ((costa.DOUBLE, (16384, 16385)), (costa.FLOAT, (16384, 16385, 16386))):
         for b in (512, 256, 128):
