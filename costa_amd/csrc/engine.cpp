@@ -532,6 +532,8 @@ struct wave_knobs {  // defaults, overridable for tuning runs
                      // unchanged; profiles/r11/c5_align_policy*.log).  Bigger unaligned ops stay
                      // on the large shape (its guarded path): cut into wavefront pieces, a
                      // 16384^2 fp32 op would become ~350 k pieces of host and device list.
+    int skew_xcd = 0;    // COSTA_SKEW_XCD=F (tuning): F skew sub-tiles continuing each other's
+                         // source rows on one XCD (one L2) at the same time
     int large_sort = 3;  // COSTA_LARGE_SORT 1: large ops in the order of the planner's locality
                          // hint (column-major target order: consecutive ops continue down the
                          // same target columns, so the write stream is sequential in aggregate);
@@ -567,6 +569,7 @@ const wave_knobs& knobs() {
         if (const char* s = std::getenv("COSTA_WAVE_POLICY")) x.policy = std::atoi(s) == 1 ? 1 : 2;
         if (const char* s = std::getenv("COSTA_TINY_SORT")) x.sort = std::atoi(s);
         if (const char* s = std::getenv("COSTA_LARGE_SORT")) x.large_sort = std::atoi(s);
+        if (const char* s = std::getenv("COSTA_SKEW_XCD")) x.skew_xcd = std::max(0, std::atoi(s));
         if (const char* s = std::getenv("COSTA_BAND_H")) x.band_h = std::max(1, std::atoi(s));
         return x;
     }();
@@ -687,12 +690,11 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         }
     }
     // transposes whose destination columns are off the 16-byte grid (an odd ScaLAPACK lld) go to
-    // the skew shape (tile_kernels.hip skew_kernel): each sub-tile writes whole 64-byte
-    // granules of every destination column, overlapping its neighbours by identical values,
-    // instead of sharing partial granules with them (measured: a copy whose 128-byte lines are
-    // split between workgroups at 16-byte granularity 0.808 against 0.672 ms, at 64-byte
-    // granularity 0.702; tools/partial_line_probe.hip).  Not for ops that read C (beta != 0:
-    // an overlapping write would apply beta twice).
+    // the skew shape (tile_kernels.hip skew_kernel): the cut between its sub-tiles follows the
+    // 64-byte granules of each destination column, so no granule is shared by two workgroups
+    // (measured: a copy whose 128-byte lines are split between workgroups at 16-byte granularity
+    // 0.808 against 0.672 ms, at 64-byte granularity 0.702; tools/partial_line_probe.hip).  Every
+    // element is written once: ops that read C (beta != 0) go there too.
     const int64_t k_elems = int64_t(sh.bf_k) * sh.bs_k;
     static const bool skew_on = [] {  // COSTA_SKEW=0: off (tuning)
         const char* s = std::getenv("COSTA_SKEW");
@@ -702,8 +704,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         const costa_tile_op_t& op = ops[li];
         if (cls[li] == 3 || !(op.flags & COSTA_TILE_TRANSPOSE) || (op.flags & COSTA_TILE_VEC_DST))
             continue;
-        const uint32_t kind = (op.flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT;
-        if (kind == COSTA_SCALE_AXPBY || op.dst % uint64_t(E) != 0 || 2 * int64_t(op.nf) * op.ns < k_elems)
+        if (op.dst % uint64_t(E) != 0 || 2 * int64_t(op.nf) * op.ns < k_elems)
             continue;
         if (cls[li] == 1) --n_med;
         cls[li] = 4;
@@ -777,6 +778,30 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
             }
             std::sort(key.begin(), key.end());
             for (size_t x = 0; x < key.size(); ++x) work[w0 + x] = key[x].second;
+        }
+        if (c == 2 && kn.skew_xcd > 1 && work.size() - w0 > 1) {
+            // runs of F f-neighbours at one destination position, then run r of every 8 runs
+            // spread to positions r, r + 8, ...: dispatch goes round-robin over the 8 XCDs
+            const int64_t F = kn.skew_xcd;
+            std::vector<std::pair<uint64_t, uint64_t>> key(work.size() - w0);
+            for (size_t x = 0; x < key.size(); ++x) {
+                const uint64_t wx = work[w0 + x];
+                const costa_tile_op_t& op = ordered[size_t(wx >> 32)];
+                const uint64_t q = wx & 0xFFFFFFFFull, nbf = uint64_t((op.nf + bf - 1) / bf);
+                const int64_t f0 = int64_t(q % nbf) * bf, s0 = int64_t(q / nbf) * bs;
+                const int64_t fp = f0 / (bf * F) * (bf * F);
+                key[x] = {((op.dst + uint64_t((fp * op.ldd + s0) * E)) << 6) | uint64_t((f0 - fp) / bf), wx};
+            }
+            std::sort(key.begin(), key.end());
+            const size_t n = key.size(), blk = size_t(8 * F);
+            for (size_t b = 0; b < n; b += blk) {
+                const size_t m = std::min(blk, n - b);
+                for (size_t x = 0; x < m; ++x) {
+                    const size_t run = x / size_t(F), in = x % size_t(F);
+                    const size_t to = m == blk ? in * 8 + run : x;
+                    work[w0 + b + to] = key[b + x].second;
+                }
+            }
         }
         n_work[c] = int64_t(work.size() - w0);
     }

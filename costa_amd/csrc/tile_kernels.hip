@@ -745,19 +745,20 @@ __global__ __launch_bounds__(S::NT) void tile_kernel(const costa_tile_op_t* __re
 
 // ---------------------------------------------------------------- skew shape
 // Transposing ops whose destination columns are off the 16-byte grid (an odd ScaLAPACK lld;
-// engine.cpp build_work routes them here, real types, never ops that read C).  A partial 64-byte
-// granule written by two workgroups costs the HBM a read-modify-write: a copy with its lines split
-// at 16-byte granularity between neighbouring workgroups ran 0.808 against 0.672 ms
-// (tools/partial_line_probe.hip).  So sub-tile (f0, s0) writes, for each destination column f,
-// the whole granules [s0 - eps_f, s0 + BS - eps_f (+ G if eps_f > 0)) clipped to the op, where
-// eps_f is how far d(f, s0) lies past a granule boundary: the first eps_f and the last G - eps_f
-// elements overlap the neighbouring sub-tiles of the same op, which write the same values (alpha *
-// x, 0 or x: a function of A alone).  The source rows [s0 - G, s0 + BS + G) are staged (odd
-// pitch: the column-wise LDS reads of the store phase are conflict-free); lanes then walk each
-// destination column in element stores, 64 consecutive elements per instruction.
+// engine.cpp build_work routes them here, real types).  A partial 64-byte granule written by two
+// workgroups costs the HBM a read-modify-write: a copy with its lines split at 16-byte granularity
+// between neighbouring workgroups ran 0.808 against 0.672 ms (tools/partial_line_probe.hip).  So
+// the cut between sub-tiles follows the granules of each destination column instead of the source
+// rows: in column f, sub-tile (f0, s0) writes [s0 - eps_f, s0 + BS - eps_f), eps_f being how far
+// d(f, s0) lies past a granule boundary (the same for every s0 of the column: BS * sizeof(T) is a
+// multiple of 64), the first sub-tile of the op from 0, the last one up to ns.  Every element is
+// written by exactly one workgroup, every granule inside the op by one: no duplicated bytes, and
+// ops that read C (beta != 0) are as safe here as anywhere.  The source rows [s0 - G, s0 + BS)
+// are staged (odd pitch: the column-wise LDS reads of the store phase are conflict-free); lanes
+// then walk each destination column in 16-byte chunks, 64 consecutive chunks per instruction.
 #ifndef COSTA_SKEW_BF4  // tuning builds: the skew sub-tile of 4- / 8-byte types
-#define COSTA_SKEW_BF4 64
-#define COSTA_SKEW_BS4 256
+#define COSTA_SKEW_BF4 32
+#define COSTA_SKEW_BS4 512
 #endif
 #ifndef COSTA_SKEW_BF8
 #define COSTA_SKEW_BF8 64
@@ -765,15 +766,14 @@ __global__ __launch_bounds__(S::NT) void tile_kernel(const costa_tile_op_t* __re
 #endif
 template <typename T>
 struct skew_shape {
-    // BS: 4-byte types 256 (G = 16: the overlap rows stay 1/8 of the sub-tile), 8-byte 128;
-    // ~75 KB of LDS either way (two workgroups per CU)
     static constexpr int NT = 512;
     static constexpr int BF = sizeof(T) == 4 ? COSTA_SKEW_BF4 : COSTA_SKEW_BF8;
     static constexpr int BS = sizeof(T) == 4 ? COSTA_SKEW_BS4 : COSTA_SKEW_BS8;
-    static constexpr int E = int(sizeof(T)), G = 64 / E, RS = BS + 2 * G, P = BF + 1;
+    static constexpr int E = int(sizeof(T)), G = 64 / E, RS = BS + G, P = BF + 1;
     static constexpr int V = 16 / E, LPC = BF / V, CPP = NT / LPC, PL = (RS + CPP - 1) / CPP;
     static constexpr int NW = NT / 64;
     static constexpr size_t lds_bytes = size_t(RS) * P * sizeof(T);
+    static_assert(BS * E % 64 == 0, "sub-tile rows: whole granules");
 };
 
 template <typename T>
@@ -795,56 +795,63 @@ __global__ __launch_bounds__(512) void skew_kernel(const costa_tile_op_t* __rest
     const uint32_t kind = (op.flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT;
     const uint32_t slot = op.flags >> COSTA_SLOT_SHIFT;
     const T alpha = kind >= COSTA_SCALE_ALPHA ? scalars[2 * slot] : T(0);
+    const T beta = kind == COSTA_SCALE_AXPBY ? scalars[2 * slot + 1] : T(0);
     const bool vs = op.flags & COSTA_TILE_VEC_SRC;
     const int64_t lds = op.lds, ldd = op.ldd;
     const T* src = reinterpret_cast<const T*>(src_base + op.src) + f0;
     // ---- rows s = s0 - G + r, r < RS, inside the op: all loads first (16-byte vectors when the
-    // source is aligned, else element loads: shifted aligned chunks measured slower here,
-    // 0.954 against 0.843 ms with both sides off the grid)
+    // source allows, else element loads: shifted aligned chunks measured slower here, 0.954
+    // against 0.843 ms with both sides off the grid)
     const int lf = (int(threadIdx.x) % K::LPC) * V;
     const int c0 = int(threadIdx.x) / K::LPC;
     const int nf_lane = tf - lf;
+    const int s_lo = s0 > 0 ? s0 - G : 0, s_hi = min(ns, s0 + BS);
     vec<T> x[K::PL];
 #pragma unroll
     for (int k = 0; k < K::PL; ++k) {
         const int r = c0 + k * K::CPP, s = s0 - G + r;
-        if (r < K::RS && s >= 0 && s < ns && nf_lane > 0) vload(x[k], src + s * lds + lf, nf_lane, vs);
+        if (r < K::RS && s >= s_lo && s < s_hi && nf_lane > 0) vload(x[k], src + s * lds + lf, nf_lane, vs);
     }
 #pragma unroll
     for (int k = 0; k < K::PL; ++k) {
         const int r = c0 + k * K::CPP, s = s0 - G + r;
-        if (r < K::RS && s >= 0 && s < ns && nf_lane > 0) {
+        if (r < K::RS && s >= s_lo && s < s_hi && nf_lane > 0) {
 #pragma unroll
             for (int e = 0; e < V; ++e)
                 if (e < nf_lane) tile[r * P + lf + e] = x[k].e[e];
         }
     }
     __syncthreads();
-    // ---- destination column f0 + f: whole granules, 64 consecutive elements per store
+    // ---- destination column f0 + f, 16-byte chunks between granule boundaries
     const int lane = int(threadIdx.x) % 64, wave = int(threadIdx.x) / 64;
     T* dst = reinterpret_cast<T*>(dst_base + op.dst);
-    auto g = [&](T v) {
-        if (kind == COSTA_SCALE_ZERO) return T(0);
-        if (kind == COSTA_SCALE_ALPHA) return alpha * v;
-        return v;
-    };
+    const bool last = s0 + BS >= ns;
     for (int f = wave; f < tf; f += K::NW) {
         T* col = dst + int64_t(f0 + f) * ldd;
         const int eps = int((reinterpret_cast<uintptr_t>(col + s0) / sizeof(T)) & uintptr_t(G - 1));
-        const int lo = max(0, s0 - eps);
-        const int hi = min(ns, s0 + BS - eps + (eps ? G : 0));
+        const int lo = s0 > 0 ? s0 - eps : 0;
+        const int hi = last ? ns : s0 + BS - eps;
         // [lo, hi) is whole granules except where it meets the op's edges: 16-byte chunks from the
         // first aligned element a to b, single elements before and after
         const int mis = int((reinterpret_cast<uintptr_t>(col + lo) / sizeof(T)) & uintptr_t(V - 1));
         const int a = min(hi, lo + ((V - mis) & (V - 1)));
         const int b = a + (hi - a) / V * V;
         const T* tcol = tile + (G - s0) * P + f;  // element s of the column at tcol[s * P]
-        if (lo + lane < a) col[lo + lane] = g(tcol[(lo + lane) * P]);
-        if (b + lane < hi) col[b + lane] = g(tcol[(b + lane) * P]);
+        if (lo + lane < a) {
+            T* d = col + lo + lane;
+            *d = scale(tcol[(lo + lane) * P], kind == COSTA_SCALE_AXPBY ? *d : T(0), kind, false, alpha, beta);
+        }
+        if (b + lane < hi) {
+            T* d = col + b + lane;
+            *d = scale(tcol[(b + lane) * P], kind == COSTA_SCALE_AXPBY ? *d : T(0), kind, false, alpha, beta);
+        }
         for (int c = a + V * lane; c < b; c += 64 * V) {
-            vec<T> o;
+            vec<T> y, o;
+            if (kind == COSTA_SCALE_AXPBY) vload(y, col + c, V, true);
 #pragma unroll
-            for (int e = 0; e < V; ++e) o.e[e] = g(tcol[(c + e) * P]);
+            for (int e = 0; e < V; ++e)
+                o.e[e] = scale(tcol[(c + e) * P], kind == COSTA_SCALE_AXPBY ? y.e[e] : T(0), kind, false,
+                               alpha, beta);
             vstore<T, bool(COSTA_NT_STORES)>(col + c, o, V, true);
         }
     }

@@ -82,7 +82,7 @@ static std::set<uint32_t> expected_shaped(costa_dtype_t dt, const std::vector<co
         if (E == 4 && e >= big && o.src % 4 == 0) o.flags |= COSTA_TILE_VEC_SRC;
         const bool al = (o.flags & both) == both, t = o.flags & COSTA_TILE_TRANSPOSE;
         const uint32_t kind = (o.flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT;
-        if (skew_elems > 0 && e > 0 && t && !(o.flags & COSTA_TILE_VEC_DST) && kind != COSTA_SCALE_AXPBY &&
+        if (skew_elems > 0 && e > 0 && t && !(o.flags & COSTA_TILE_VEC_DST) &&
             o.dst % uint64_t(E) == 0 && 2 * e >= skew_elems) {
             large.insert(o.order);
             continue;
