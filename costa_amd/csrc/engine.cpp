@@ -532,8 +532,9 @@ struct wave_knobs {  // defaults, overridable for tuning runs
                      // unchanged; profiles/r11/c5_align_policy*.log).  Bigger unaligned ops stay
                      // on the large shape (its guarded path): cut into wavefront pieces, a
                      // 16384^2 fp32 op would become ~350 k pieces of host and device list.
-    int skew_xcd = 0;    // COSTA_SKEW_XCD=F (tuning): F skew sub-tiles continuing each other's
-                         // source rows on one XCD (one L2) at the same time
+    int skew_xcd = -1;   // COSTA_SKEW_XCD=F (tuning): F skew sub-tiles continuing each other's
+                         // source rows on one XCD (one L2) at the same time; -1 (default):
+                         // kSkewWideGroup for lists on the wide skew variant, else none
     int large_sort = 3;  // COSTA_LARGE_SORT 1: large ops in the order of the planner's locality
                          // hint (column-major target order: consecutive ops continue down the
                          // same target columns, so the write stream is sequential in aggregate);
@@ -563,13 +564,16 @@ struct wave_knobs {  // defaults, overridable for tuning runs
                      // / 0.596-0.600, unpack 0.556-0.558 / 0.606-0.610, 'T' pack 0.725-0.729 /
                      // 0.751-0.761, unpack equal
 };
+// f-neighbour skew sub-tiles grouped per XCD on the wide variant (fp32 16384^2 'T', both sides
+// lld 16385: 0.453 / 0.440 / 0.428 / 0.419-0.424 ms with groups of 1 / 2 / 4 / 8; profiles/r3b/skew/)
+constexpr int64_t kSkewWideGroup = 8;
 const wave_knobs& knobs() {
     static wave_knobs k = [] {
         wave_knobs x;
         if (const char* s = std::getenv("COSTA_WAVE_POLICY")) x.policy = std::atoi(s) == 1 ? 1 : 2;
         if (const char* s = std::getenv("COSTA_TINY_SORT")) x.sort = std::atoi(s);
         if (const char* s = std::getenv("COSTA_LARGE_SORT")) x.large_sort = std::atoi(s);
-        if (const char* s = std::getenv("COSTA_SKEW_XCD")) x.skew_xcd = std::max(0, std::atoi(s));
+        if (const char* s = std::getenv("COSTA_SKEW_XCD")) x.skew_xcd = std::max(-1, std::atoi(s));
         if (const char* s = std::getenv("COSTA_BAND_H")) x.band_h = std::max(1, std::atoi(s));
         return x;
     }();
@@ -722,12 +726,18 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     // partial granule shared by two workgroups again
     merge_adjacent(skew_ops, E);
     for (size_t i = 0; i < skew_ops.size(); ++i) shaped[2].push_back(uint32_t(i));
+    // 4-byte types reading sources off the 16-byte grid too: the wide skew variant, its
+    // f-neighbours (which share the misaligned source runs' partial lines) grouped on one XCD
+    bool skew_wide = false;
+    for (const auto& op : skew_ops)
+        skew_wide = skew_wide || (E == 4 && (op.src % 16 != 0 || (uint64_t(op.lds) * uint64_t(E)) % 16 != 0));
+    const int64_t skew_group = kn.skew_xcd >= 0 ? kn.skew_xcd : skew_wide ? kSkewWideGroup : 0;
     // each shape's ops in hint order when every one carries a hint; lists whose shaped ops all
     // transpose 8-byte elements then take the sub-tiles in destination-address order (wave_knobs)
     int64_t n_work[3] = {0, 0, 0};
     for (int c = 0; c < 3; ++c) {
-        const int bf = c == 2 ? sh.bf_k : c ? (med_sq ? sh.bf_s : sh.bf_m) : sq ? sh.bf_q : sh.bf;
-        const int bs = c == 2 ? sh.bs_k : c ? (med_sq ? sh.bs_s : sh.bs_m) : sq ? sh.bs_q : sh.bs;
+        const int bf = c == 2 ? (skew_wide ? sh.bf_kw : sh.bf_k) : c ? (med_sq ? sh.bf_s : sh.bf_m) : sq ? sh.bf_q : sh.bf;
+        const int bs = c == 2 ? (skew_wide ? sh.bs_kw : sh.bs_k) : c ? (med_sq ? sh.bs_s : sh.bs_m) : sq ? sh.bs_q : sh.bs;
         const std::vector<uint32_t>& sel = shaped[c];
         const std::vector<costa_tile_op_t>& src_ops = c == 2 ? skew_ops : ops;
         std::vector<uint32_t> sperm(sel.size());
@@ -779,10 +789,10 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
             std::sort(key.begin(), key.end());
             for (size_t x = 0; x < key.size(); ++x) work[w0 + x] = key[x].second;
         }
-        if (c == 2 && kn.skew_xcd > 1 && work.size() - w0 > 1) {
+        if (c == 2 && skew_group > 1 && work.size() - w0 > 1) {
             // runs of F f-neighbours at one destination position, then run r of every 8 runs
             // spread to positions r, r + 8, ...: dispatch goes round-robin over the 8 XCDs
-            const int64_t F = kn.skew_xcd;
+            const int64_t F = skew_group;
             std::vector<std::pair<uint64_t, uint64_t>> key(work.size() - w0);
             for (size_t x = 0; x < key.size(); ++x) {
                 const uint64_t wx = work[w0 + x];
@@ -893,6 +903,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     w.n_large = n_work[0];
     w.n_medium = n_work[1];
     w.n_skew = n_work[2];
+    w.skew_wide = skew_wide && n_work[2] > 0;
 
     w.tiny_first = int64_t(ordered.size());
     w.n_tiny = int64_t(at_piece[nw]);
@@ -926,6 +937,7 @@ launch_args make_launch(const work_split& w, const void* d_ordered, const void* 
     a.full = w.full;
     a.med_full = w.med_full;
     a.med_sq = w.med_sq;
+    a.skew_wide = w.skew_wide;
     return a;
 }
 

@@ -194,6 +194,7 @@ struct launch_args {
     bool full;              // work_split::full
     bool med_full;          // work_split::med_full
     bool med_sq;            // work_split::med_sq
+    bool skew_wide = false; // work_split::skew_wide
 };
 bool any_transpose(const std::vector<costa_tile_op_t>& ops);
 bool any_axpby(const std::vector<costa_tile_op_t>& ops);
@@ -205,6 +206,7 @@ void launch_tiles(costa_dtype_t dtype, const launch_args& a, void* stream /* hip
 struct shape_dims {
     int bf = 0, bs = 0, bf_m = 0, bs_m = 0, bf_q = 0, bs_q = 0, bf_s = 0, bs_s = 0;
     int bf_k = 0, bs_k = 0;  // the skew shape (transposes into unaligned destinations; 0: none)
+    int bf_kw = 0, bs_kw = 0;  // its wide variant (sources off the 16-byte grid too; 4-byte types)
 };
 void tile_shapes(costa_dtype_t dtype, bool transposing_list, shape_dims* out);
 // Execution order of an op list: `ordered` = [sub-tiled ops | tiny ops] (tiny ops sorted by the
@@ -220,6 +222,7 @@ struct work_split {
                             // of large sub-tiles (the launch may then take fewer threads)
     bool med_full = false;  // the same for the medium ops and the medium sub-tile
     bool med_sq = false;    // the medium class runs on 32 x 32 sub-tiles (bf_s x bs_s)
+    bool skew_wide = false; // the skew items are sub-tiles of its wide variant (bf_kw x bs_kw)
     int64_t n_items() const { return n_large + n_medium + n_skew + n_tiny; }
 };
 // pack_list: the ops write the dense send package (their destinations are contiguous whatever

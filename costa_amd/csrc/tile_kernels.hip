@@ -760,15 +760,25 @@ __global__ __launch_bounds__(S::NT) void tile_kernel(const costa_tile_op_t* __re
 #define COSTA_SKEW_BF4 32
 #define COSTA_SKEW_BS4 512
 #endif
+#ifndef COSTA_SKEW_BF4W  // 4-byte types whose source columns are off the 16-byte grid too
+#define COSTA_SKEW_BF4W 64
+#define COSTA_SKEW_BS4W 256
+#endif
 #ifndef COSTA_SKEW_BF8
 #define COSTA_SKEW_BF8 64
 #define COSTA_SKEW_BS8 128
 #endif
-template <typename T>
+// WIDE (4-byte types, lists whose skew ops also read sources off the 16-byte grid): 64 x 256
+// instead of 32 x 512, so every misaligned source run is 256 bytes, not 128 (its two partial
+// lines shared with the f-neighbour sub-tiles, which engine.cpp build_work then puts on one XCD);
+// fp32 16384^2 'T' lld 16385 both sides 0.456 -> 0.419-0.424 ms with that grouping, while
+// destination-only lists lost with it (0.384 -> 0.430: they keep 32 x 512, no grouping;
+// profiles/r3b/skew/)
+template <typename T, bool WIDE = false>
 struct skew_shape {
     static constexpr int NT = 512;
-    static constexpr int BF = sizeof(T) == 4 ? COSTA_SKEW_BF4 : COSTA_SKEW_BF8;
-    static constexpr int BS = sizeof(T) == 4 ? COSTA_SKEW_BS4 : COSTA_SKEW_BS8;
+    static constexpr int BF = sizeof(T) == 4 ? (WIDE ? COSTA_SKEW_BF4W : COSTA_SKEW_BF4) : COSTA_SKEW_BF8;
+    static constexpr int BS = sizeof(T) == 4 ? (WIDE ? COSTA_SKEW_BS4W : COSTA_SKEW_BS4) : COSTA_SKEW_BS8;
     static constexpr int E = int(sizeof(T)), G = 64 / E, RS = BS + G, P = BF + 1;
     static constexpr int V = 16 / E, LPC = BF / V, CPP = NT / LPC, PL = (RS + CPP - 1) / CPP;
     static constexpr int NW = NT / 64;
@@ -776,12 +786,12 @@ struct skew_shape {
     static_assert(BS * E % 64 == 0, "sub-tile rows: whole granules");
 };
 
-template <typename T>
+template <typename T, bool WIDE>
 __global__ __launch_bounds__(512) void skew_kernel(const costa_tile_op_t* __restrict__ ops,
                                                    const uint64_t* __restrict__ work,
                                                    const char* src_base, char* dst_base,
                                                    const T* __restrict__ scalars) {
-    using K = skew_shape<T>;
+    using K = skew_shape<T, WIDE>;
     constexpr int V = K::V, BF = K::BF, BS = K::BS, G = K::G, P = K::P;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     T* tile = reinterpret_cast<T*>(smem);
@@ -857,17 +867,24 @@ __global__ __launch_bounds__(512) void skew_kernel(const costa_tile_op_t* __rest
     }
 }
 
+template <typename T, bool WIDE>
+void launch_skew_w(const launch_args& a, const uint64_t* work, int64_t n, hipStream_t stream) {
+    using K = skew_shape<T, WIDE>;
+    const int64_t max_grid = 1LL << 30;
+    for (int64_t off = 0; off < n; off += max_grid) {
+        const int64_t m = std::min(max_grid, n - off);
+        hipLaunchKernelGGL((skew_kernel<T, WIDE>), dim3(unsigned(m)), dim3(K::NT), K::lds_bytes, stream,
+                           a.ops, work + off, a.src_base, a.dst_base, static_cast<const T*>(a.scalars));
+    }
+}
 template <typename T>
 void launch_skew(const launch_args& a, const uint64_t* work, int64_t n, hipStream_t stream) {
     if constexpr (std::is_same<T, float>::value || std::is_same<T, double>::value ||
                   std::is_same<T, int>::value) {
-        const int64_t max_grid = 1LL << 30;
-        for (int64_t off = 0; off < n; off += max_grid) {
-            const int64_t m = std::min(max_grid, n - off);
-            hipLaunchKernelGGL((skew_kernel<T>), dim3(unsigned(m)), dim3(skew_shape<T>::NT),
-                               skew_shape<T>::lds_bytes, stream, a.ops, work + off, a.src_base,
-                               a.dst_base, static_cast<const T*>(a.scalars));
-        }
+        if (a.skew_wide && sizeof(T) == 4)
+            launch_skew_w<T, true>(a, work, n, stream);
+        else
+            launch_skew_w<T, false>(a, work, n, stream);
     } else if (n > 0) {
         throw error(COSTA_ERR_INTERNAL, "costa: skew shape for a complex type");
     }
@@ -1155,6 +1172,8 @@ void shape_of(bool tr, shape_dims* d) {
                           std::is_same<T, int>::value;
     d->bf_k = tr && skew ? skew_shape<T>::BF : 0;
     d->bs_k = tr && skew ? skew_shape<T>::BS : 0;
+    d->bf_kw = tr && skew ? skew_shape<T, true>::BF : 0;
+    d->bs_kw = tr && skew ? skew_shape<T, true>::BS : 0;
 }
 
 template <typename T, typename S>
@@ -1167,9 +1186,14 @@ template <typename T>
 void set_lds_limits() {
     if constexpr (std::is_same<T, float>::value || std::is_same<T, double>::value ||
                   std::is_same<T, int>::value)
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&skew_kernel<T>),
+    {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&skew_kernel<T, false>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  int(skew_shape<T>::lds_bytes));
+                                  int(skew_shape<T, false>::lds_bytes));
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&skew_kernel<T, true>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  int(skew_shape<T, true>::lds_bytes));
+    }
     set_lds_limit<T, typename shapes<T>::large>();
     set_lds_limit<T, typename shapes<T>::large_tr>();
     set_lds_limit<T, typename shapes<T>::medium_tr>();
