@@ -331,7 +331,15 @@ bool any_axpby(const std::vector<costa_tile_op_t>& ops) {
 int64_t tiny_copy_budget(int64_t E) { return 48 * int64_t(tiny_copy_lane_bytes(size_t(E))); }
 
 // Transpose mode: the staged tile, kTinyLdsDefault bytes of LDS per wavefront
-int64_t tiny_lds_budget() { return int64_t(kTinyLdsDefault); }
+// (COSTA_TINY_LDS: another budget up to kTinyLdsBytes, tuning runs only)
+int64_t tiny_lds_budget() {
+    static const int64_t b = [] {
+        const char* s = std::getenv("COSTA_TINY_LDS");
+        const int64_t v = s ? std::atoll(s) : 0;
+        return v >= 256 && v <= kTinyLdsBytes ? v : int64_t(kTinyLdsDefault);
+    }();
+    return b;
+}
 
 static bool is_tiny(const costa_tile_op_t& op, int64_t E) {
     if (op.flags & COSTA_TILE_TRANSPOSE) return int64_t(op.nf | 1) * op.ns * E <= tiny_lds_budget();

@@ -905,11 +905,15 @@ void launch_skew(const launch_args& a, const uint64_t* work, int64_t n, hipStrea
 // ragged edges.  Variants measured slower and removed: 16-byte copy accesses,
 // several ops per wavefront (strided, chunked, moved together), a persistent pipelined kernel
 // (next op's loads in flight while this op stores: 2.9 against 4.4 TB/s), nt cache policy here.
-// Wavefronts per workgroup: 4 for lists that transpose (4 KiB of LDS per wavefront), 8 for
-// copy-only lists (no LDS) (profiles/r06/c5_knobs.log).
+// r3: transposing ops stage through LDS-DMA and request their old destination values before
+// the one wait (tiny_transpose_glds): cfg 5 'T' 0.781 -> 0.743 ms on one lease (4 waves per
+// workgroup), 0.722 with 8; without the early old-value loads 0.948 (profiles/r3b/glds/).
+// Wavefronts per workgroup: 8 (4 KiB of LDS each for lists that transpose; copy-only lists
+// without LDS: profiles/r06/c5_knobs.log).
 #ifndef COSTA_TINY_WAVES_TR  // build-time overrides for tuning builds (tools/tiny_variants.sh)
-#define COSTA_TINY_WAVES_TR 4  // r2: cfg 5 'T' 0.7733 -> 0.7629 ms against 2 (1: 0.7637, 8: 0.800;
-#endif                         // profiles/r2d/c5T_waves/)
+#define COSTA_TINY_WAVES_TR 8  // r3 (LDS-DMA staging): cfg 5 'T' 0.736-0.738 ms with 4, 0.721-0.723
+#endif                         // with 8, 0.728-0.729 with 16, 0.759-0.761 with 2
+                               // (profiles/r3b/glds/); r2 (register staging) had 4 best
 #ifndef COSTA_TINY_WAVES_COPY
 #define COSTA_TINY_WAVES_COPY 8
 #endif
@@ -943,6 +947,78 @@ struct lin {  // (f, s) of linear element index e = f + s*n, stepped by 64
         }
     }
 };
+
+// Transpose mode with the staging loads going straight to LDS (global_load_lds_dword: no VGPR
+// destination), so a wavefront has its whole staged tile and, for ops that read C, every old
+// destination value (16 VGPRs at most: the tile is at most tiny_lds_budget() bytes) in flight at
+// once, and waits once: one memory round trip per op instead of one per 64 x U elements of each
+// phase (register staging holds U elements per lane and pass).  The LDS image is the same
+// (element (f, s) at s * pitch + f, pitch odd): an LDS-DMA instruction writes its 64 dwords
+// lane-linearly from a wave-uniform base, so lane j of instruction k takes dword 64 k + j of the
+// padded image and loads whatever source word belongs there (pad words: lane inactive).
+#ifndef COSTA_TINY_GLDS  // 0: register staging (tuning builds only)
+#define COSTA_TINY_GLDS 1
+#endif
+#ifndef COSTA_TINY_Y_BYTES  // old destination values requested before the wait: a whole staged op
+#define COSTA_TINY_Y_BYTES kTinyLdsDefault
+#endif
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void glob_void;
+template <typename T, bool AX>
+__device__ __forceinline__ void tiny_transpose_glds(const T* src, T* dst, int nf, int ns, int64_t lds,
+                                                    int64_t ldd, uint32_t kind, bool conj, T alpha, T beta,
+                                                    int lane, T* t) {
+    constexpr int W = int(sizeof(T)) / 4;         // dwords per element
+    constexpr int DP = 64 / W;                    // image positions per instruction
+    constexpr int NY = COSTA_TINY_Y_BYTES / (64 * int(sizeof(T)));  // passes with old values held
+    constexpr int NP = kTinyLdsBytes / (64 * int(sizeof(T)));         // destination passes at most
+    const int pitch = nf | 1, total = nf * ns, nd = pitch * ns * W;
+    {
+        const int w = lane % W;
+        int f = (lane / W) % pitch, s = (lane / W) / pitch;
+        const int df = DP % pitch, ds = DP / pitch;
+        const char* sb = reinterpret_cast<const char*>(src) + 4 * w;
+        char* tb = reinterpret_cast<char*>(t);
+        for (int d0 = 0; d0 < nd; d0 += 64) {
+            if (f < nf && d0 + lane < nd)
+                __builtin_amdgcn_global_load_lds((glob_void*)(sb + (int64_t(s) * lds + f) * int64_t(sizeof(T))),
+                                                 (lds_void*)(tb + 4 * d0), 4, 0, 0);
+            f += df;
+            s += ds;
+            if (f >= pitch) {
+                f -= pitch;
+                ++s;
+            }
+        }
+    }
+    // the old destination values of the whole op, requested before the wait
+    T y[AX && NY > 0 ? NY : 1];
+    if constexpr (AX) {
+        if (kind == COSTA_SCALE_AXPBY) {
+            lin<T> q(lane, ns);  // destination order: q.f walks s, q.s walks f
+#pragma unroll
+            for (int u = 0; u < NY; ++u) {
+                if (u * 64 >= total) break;
+                if (u * 64 + lane < total) y[u] = dst[int64_t(q.s) * ldd + q.f];
+                q.step();
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA writes (and y) have landed
+    lin<T> q(lane, ns);
+#pragma unroll
+    for (int u = 0; u < NP; ++u) {
+        if (u * 64 >= total) break;
+        if (u * 64 + lane < total) {
+            const T v = t[q.f * pitch + q.s];
+            T* d = dst + int64_t(q.s) * ldd + q.f;
+            T old = e_zero<T>();
+            if (AX && kind == COSTA_SCALE_AXPBY) old = u < NY ? y[AX && u < NY ? u : 0] : *d;
+            *d = scale(v, old, kind, conj, alpha, beta);
+        }
+        q.step();
+    }
+}
 
 // TR = false: the list has no transposing op (the transpose path and its registers are
 // compiled out, so copy-only lists keep a high occupancy).  AX = false: no op of the list reads
@@ -1012,6 +1088,12 @@ __device__ __forceinline__ void tiny_op(const costa_tile_op_t& op, int lane, T* 
     }
     // transpose mode: stage in LDS (pitch odd), then write in destination order
     const int pitch = nf | 1;
+#if COSTA_TINY_GLDS
+    if constexpr (sizeof(T) % 4 == 0) {
+        tiny_transpose_glds<T, AX>(src, dst, nf, ns, lds, ldd, kind, conj, alpha, beta, lane, t);
+        return;
+    }
+#endif
     // (requesting the first pass's old values before the staging loads was measured slower on
     // cfg 5 'T': 2.92 against 3.13 TB/s; the 16 extra VGPRs cost a wavefront per SIMD)
     {
