@@ -466,6 +466,36 @@ void merge_row_bands(const std::vector<const costa_tile_op_t*>& ops, int h, std:
     perm.swap(out);
 }
 
+// XCD column bands (wave_knobs::xcd_bands): the tiny kernel gives XCD x the x-th eighth of
+// the list; destination order alone makes that eighth a run of whole target block-rows, so an A
+// cache line shared by the tiles above and below a block-row boundary is fetched again one
+// block-row of the XCD's traffic later (~11 MB for cfg 5: past its 4 MB L2).  Here the list is
+// first split into eight bands of target columns (by the planner's column-major hint, equal piece
+// counts), each band in destination order: every XCD walks all block-rows of its own columns, and
+// the two tiles sharing the line run ~1/8 of a block-row apart on the same XCD.
+void xcd_bands(const std::vector<const costa_tile_op_t*>& ops, int64_t E, int k, std::vector<uint32_t>& perm) {
+    const uint64_t nb = 8 * uint64_t(k);  // bands: XCD x walks bands k x .. k x + k - 1 in turn
+    const size_t n = perm.size();
+    std::vector<uint64_t> pieces(n);
+    uint64_t total = 0;
+    for (size_t i = 0; i < n; ++i) {
+        const wave_grid g = wave_pieces(*ops[i], E);
+        pieces[i] = uint64_t(g.nfc * g.nsc);
+        total += pieces[i];
+    }
+    std::vector<uint32_t> by_hint(n);
+    for (size_t i = 0; i < n; ++i) by_hint[i] = uint32_t(i);
+    std::stable_sort(by_hint.begin(), by_hint.end(),
+                     [&](uint32_t x, uint32_t y) { return ops[x]->order < ops[y]->order; });
+    std::vector<uint32_t> band(n);
+    uint64_t cum = 0;
+    for (const uint32_t i : by_hint) {
+        band[i] = uint32_t(std::min<uint64_t>(nb - 1, cum * nb / std::max<uint64_t>(total, 1)));
+        cum += pieces[i];
+    }
+    std::stable_sort(perm.begin(), perm.end(), [&](uint32_t x, uint32_t y) { return band[x] < band[y]; });
+}
+
 // Merges ops that continue each other: the op whose source starts where op a's source ends along
 // s (a.src + a.ns * lds) and whose destination continues a's the same way (one destination
 // stride further for copies, ns elements further for transposes), with the same extent along f,
@@ -560,6 +590,11 @@ struct wave_knobs {  // defaults, overridable for tuning runs
                          // ms; copy lists untested under 2; tools/order_run.sh,
                          // tools/f32_order_run.sh, profiles/r2/order/)
     int band_h = 2;  // COSTA_BAND_H: destination rows merged per band (sort mode 7)
+    int xcd_bands = 1;  // COSTA_XCD_BANDS=k: destination-ordered wavefront lists in 8 k column
+                        // bands, k per XCD (xcd_bands); 0: off.  cfg 5 'N' 0.476 -> 0.446 ms with
+                        // k = 1 (2 / 4 / 16: 0.464 / 0.475 / 0.490), 'T' equal; through the
+                        // loopback exchange unpack 'N' 0.609 -> 0.592, 'T' 1.016 -> 0.960
+                        // (profiles/r3b/bands/)
     int sort = 5;    // COSTA_TINY_SORT 0: list order, 1: by source, 2: by destination address,
                      // 3: by the planner's locality hint (costa_tile_op_t::order), 4: 3 for
                      // copy-only lists, 2 for lists that transpose (cfg 5 'T' 3.88 against
@@ -583,6 +618,7 @@ const wave_knobs& knobs() {
         if (const char* s = std::getenv("COSTA_LARGE_SORT")) x.large_sort = std::atoi(s);
         if (const char* s = std::getenv("COSTA_SKEW_XCD")) x.skew_xcd = std::max(-1, std::atoi(s));
         if (const char* s = std::getenv("COSTA_BAND_H")) x.band_h = std::max(1, std::atoi(s));
+        if (const char* s = std::getenv("COSTA_XCD_BANDS")) x.xcd_bands = std::atoi(s);
         return x;
     }();
     return k;
@@ -887,6 +923,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         for (size_t i = 0; i < nw; ++i) perm[i] = uint32_t(i);
     }
     if (chain && nw > 1) chain_source_neighbours(wave_ops, E, perm);
+    if (kn.xcd_bands && mode == 2 && top > 0 && nw > 1) xcd_bands(wave_ops, E, kn.xcd_bands, perm);
     if (kn.sort == 7 && !pack_list && nw > 1) merge_row_bands(wave_ops, kn.band_h, perm);
     // pieces: count per op, scan, fill (host threads for long lists)
     std::vector<wave_grid> grid(nw);

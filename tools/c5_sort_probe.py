@@ -19,7 +19,7 @@ def main():
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
     costa.lib()
     comm = costa.Comm.self(0)
-    LA, LC, A, C, op, al, be, wl, masks = bench.cfg5_workload(costa, torch, 0, 1, op)
+    LA, LC, A, C, op, al, be, wl, masks, _ca = bench.cfg5_workload(costa, torch, 0, 1, op)
     for _ in range(3):
         costa.transform_async(LA, LC, comm, op, al, be)
     costa.synchronize(comm)
