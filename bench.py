@@ -220,14 +220,16 @@ def measured_traffic(alg_bytes: int):
     bytes per launch).  PMC counters cannot be read from inside this process, so they come
     from that separate pass."""
     import glob
-    best = None
+    best, best_key = None, None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_*.json"))):
         try:
             d = json.load(open(p))
         except Exception:
             continue
         if d.get("bytes_per_launch_alg") == alg_bytes and d.get("hbm_bytes_per_launch_corrected"):
-            best = (d["hbm_bytes_per_launch_corrected"], os.path.relpath(p, ROOT))
+            key = d.get("collected", "")  # ISO date of the pass (r3 on); older files by name order
+            if best_key is None or key >= best_key:
+                best, best_key = (d["hbm_bytes_per_launch_corrected"], os.path.relpath(p, ROOT)), key
     return best if best else (None, None)
 
 

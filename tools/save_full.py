@@ -13,6 +13,7 @@ import os
 import shutil
 import statistics
 import sys
+import time
 
 tag = sys.argv[1]
 src = os.path.join("gpurun_out", tag)
@@ -55,13 +56,13 @@ if os.path.exists(tr):
     json.dump(out, open(os.path.join(dst, "kernel_dispatches.json"), "w"), indent=1)
 
 
-def counter(kind):
-    """median per dispatch of the largest-grid tile_kernel<double> (the cfg 2 launch), KiB"""
-    files = glob.glob(os.path.join(src, f"pmc_{kind}", "**", "*counter_collection.csv"), recursive=True)
+def counter(base, kind, kern):
+    """median per dispatch of the largest-grid `kern` launch in one --pmc pass, KiB"""
+    files = glob.glob(os.path.join(base, "**", "*counter_collection.csv"), recursive=True)
     vals = {}
     for f in files:
         for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] != kind or "tile_kernel<double" not in r["Kernel_Name"]:
+            if r["Counter_Name"] != kind or kern not in r["Kernel_Name"]:
                 continue
             g = int(r["Grid_Size"])
             vals.setdefault(g, []).append(float(r["Counter_Value"]))
@@ -71,18 +72,37 @@ def counter(kind):
     return statistics.median(vals[g]), {"grid": g, "dispatches": len(vals[g])}
 
 
-fk, fi = counter("FETCH_SIZE")
-wk, wi = counter("WRITE_SIZE")
-d = line(os.path.join(src, "pmc_FETCH_SIZE.log"))
-if fk is not None and wk is not None and d:
-    out = {"FETCH_SIZE_KiB": fk, "WRITE_SIZE_KiB": wk, "fetch": fi, "write": wi,
+def save_pmc(fetch_dir, write_dir, log, kern, name, read_share):
+    """one workload's HBM traffic per launch from its FETCH_SIZE and WRITE_SIZE passes;
+    read_share: the algorithmic reads' share of the algorithmic bytes"""
+    fk, fi = counter(fetch_dir, "FETCH_SIZE", kern)
+    wk, wi = counter(write_dir, "WRITE_SIZE", kern)
+    d = line(log) if os.path.exists(log) else None
+    if fk is None or wk is None or not d:
+        return
+    alg = d["roofline"]["bytes_per_launch"]
+    out = {"FETCH_SIZE_KiB": fk, "WRITE_SIZE_KiB": wk, "fetch": fi, "write": wi, "kernel": kern,
            "hbm_bytes_per_launch_corrected": int((2 * fk + wk) * 1024),
            "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halving)",
-           "bytes_per_launch_alg": d["roofline"]["bytes_per_launch"],
-           "workload": d["config"]["workload"]}
-    out["ratio_to_algorithmic"] = round(out["hbm_bytes_per_launch_corrected"] / out["bytes_per_launch_alg"], 4)
-    json.dump(out, open(os.path.join(dst, "pmc_tile_kernel.json"), "w"), indent=1)
-    print("pmc", {k: v for k, v in out.items() if k not in ("fetch", "write")})
+           "bytes_per_launch_alg": alg, "workload": d["config"]["workload"],
+           "collected": time.strftime("%Y-%m-%dT%H:%M:%S", time.gmtime(os.path.getmtime(log)))}
+    out["ratio_to_algorithmic"] = round(out["hbm_bytes_per_launch_corrected"] / alg, 4)
+    out["reads_to_algorithmic"] = round(2 * fk * 1024 / (alg * read_share), 4)
+    out["writes_to_algorithmic"] = round(wk * 1024 / (alg * (1 - read_share)), 4)
+    json.dump(out, open(os.path.join(dst, name), "w"), indent=1)
+    print(name, {k: v for k, v in out.items() if k not in ("fetch", "write", "correction", "workload")})
+
+
+# the cfg 2 launch (tools/gpu_full.sh); cfg 5 'N' / 'T' when tools/c5_pmc.sh ran as <tag>_c5pmc
+save_pmc(os.path.join(src, "pmc_FETCH_SIZE"), os.path.join(src, "pmc_WRITE_SIZE"),
+         os.path.join(src, "pmc_FETCH_SIZE.log"), "tile_kernel<double", "pmc_tile_kernel.json", 0.5)
+c5 = src + "_c5pmc"
+for op, share in (("N", 0.5), ("T", 2 / 3)):
+    save_pmc(os.path.join(c5, f"pmc_{op}_FETCH_SIZE"), os.path.join(c5, f"pmc_{op}_WRITE_SIZE"),
+             os.path.join(c5, f"pmc_{op}_FETCH_SIZE.log"), "tiny_kernel<float", f"pmc_cfg5_{op}.json", share)
+    st = os.path.join(c5, f"prof_{op}", "trace_kernel_stats.csv")
+    if os.path.exists(st):
+        shutil.copy(st, os.path.join(dst, f"c5{op}_trace_kernel_stats.csv"))
 for name in ("bench.json", "c5N.json", "c5T.json", "extra.json"):
     d = line(os.path.join(dst, name))
     if d:
