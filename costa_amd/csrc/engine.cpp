@@ -323,12 +323,23 @@ bool any_axpby(const std::vector<costa_tile_op_t>& ops) {
 // rectangular sub-ops within it (a sub-rectangle of a tile op is a tile op).  Budgets: copy
 // mode one wavefront pass of data (tiny_copy_budget), transpose mode tiny_lds_budget() of staged
 // tile (row pitch nf | 1).
-// Copy mode: three quarters of one wavefront pass (64 lanes x tiny_copy_lane_bytes), an op the
-// wavefront moves in one round trip, cut a little finer for more wavefronts in flight; cfg 5 'N'
-// 4.26 TB/s at 3 KiB against 4.15 at 4 KiB and 4.25 at 2 KiB with 64-byte lanes and the XCD
-// remap (profiles/r11/c5_budget_uc64.log; r09, 128-byte lanes without the remap: 8 KiB best,
-// profiles/r09/c5b.log).
-int64_t tiny_copy_budget(int64_t E) { return 48 * int64_t(tiny_copy_lane_bytes(size_t(E))); }
+// Copy mode: a part of one wavefront pass (64 lanes x tiny_copy_lane_bytes), an op the wavefront
+// moves in one round trip, cut finer for more wavefronts in flight.  Local lists: half (2 KiB);
+// r3 with the XCD column bands, cfg 5 'N' 0.434-0.436 ms at 2 KiB against 0.446-0.447 at 3 KiB,
+// 0.438 at 2.5, 0.449-0.451 at 1.5, 0.466 at 4, 0.517 at 1 (profiles/r3b/copy_budget/).  Pack
+// and unpack lists (one side the dense package): three quarters (3 KiB); through the loopback
+// exchange pack 'N' 0.587-0.590 ms against 0.607-0.608 at 2 KiB, unpack 0.592-0.597 against
+// 0.607-0.608 (profiles/r3b/copy_budget/lb2_loopback.txt; r11: 3 KiB best for every list,
+// profiles/r11/c5_budget_uc64.log).
+// (COSTA_TINY_COPY: another budget in bytes up to kTinyCopyBytes, tuning runs only)
+int64_t tiny_copy_budget(int64_t E, bool local) {
+    static const int64_t env = [] {
+        const char* s = std::getenv("COSTA_TINY_COPY");
+        const int64_t v = s ? std::atoll(s) : 0;
+        return v >= 256 && v <= kTinyCopyBytes ? v : int64_t(0);
+    }();
+    return env ? env : (local ? 32 : 48) * int64_t(tiny_copy_lane_bytes(size_t(E)));
+}
 
 // Transpose mode: the staged tile, kTinyLdsDefault bytes of LDS per wavefront
 // (COSTA_TINY_LDS: another budget up to kTinyLdsBytes, tuning runs only)
@@ -341,9 +352,9 @@ int64_t tiny_lds_budget() {
     return b;
 }
 
-static bool is_tiny(const costa_tile_op_t& op, int64_t E) {
+static bool is_tiny(const costa_tile_op_t& op, int64_t E, bool local) {
     if (op.flags & COSTA_TILE_TRANSPOSE) return int64_t(op.nf | 1) * op.ns * E <= tiny_lds_budget();
-    return int64_t(op.nf) * op.ns * E <= tiny_copy_budget(E);
+    return int64_t(op.nf) * op.ns * E <= tiny_copy_budget(E, local);
 }
 
 static uint32_t vec_flags(uint64_t src, int64_t lds, uint64_t dst, int64_t ldd, int64_t E) {
@@ -359,11 +370,11 @@ namespace {
 struct wave_grid {
     int64_t nfc = 1, nsc = 1;
 };
-wave_grid wave_pieces(const costa_tile_op_t& op, int64_t E) {
+wave_grid wave_pieces(const costa_tile_op_t& op, int64_t E, bool local) {
     wave_grid g;
-    if (is_tiny(op, E)) return g;
+    if (is_tiny(op, E, local)) return g;
     const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
-    const int64_t budget = (tr ? tiny_lds_budget() : tiny_copy_budget(E)) / E;  // elements
+    const int64_t budget = (tr ? tiny_lds_budget() : tiny_copy_budget(E, local)) / E;  // elements
     const int64_t nf = op.nf, ns = op.ns;
     // transpose: near-square pieces (both the source columns and the destination rows stay
     // long); copy: whole columns when one fits, else tall pieces
@@ -375,7 +386,7 @@ wave_grid wave_pieces(const costa_tile_op_t& op, int64_t E) {
     return g;
 }
 // writes the g.nfc * g.nsc pieces of `op` at `out`
-void emit_pieces(const costa_tile_op_t& op, int64_t E, const wave_grid& g, costa_tile_op_t* out) {
+void emit_pieces(const costa_tile_op_t& op, int64_t E, const wave_grid& g, bool local, costa_tile_op_t* out) {
     if (g.nfc == 1 && g.nsc == 1) {
         *out = op;
         return;
@@ -393,7 +404,7 @@ void emit_pieces(const costa_tile_op_t& op, int64_t E, const wave_grid& g, costa
             sub.nf = int32_t(f1 - f0);
             sub.ns = int32_t(s1 - s0);
             sub.flags = keep | vec_flags(sub.src, op.lds, sub.dst, op.ldd, E);
-            if (!is_tiny(sub, E)) throw error(COSTA_ERR_INTERNAL, "costa: wave split over budget");
+            if (!is_tiny(sub, E, local)) throw error(COSTA_ERR_INTERNAL, "costa: wave split over budget");
             *out++ = sub;
         }
     }
@@ -473,13 +484,14 @@ void merge_row_bands(const std::vector<const costa_tile_op_t*>& ops, int h, std:
 // first split into eight bands of target columns (by the planner's column-major hint, equal piece
 // counts), each band in destination order: every XCD walks all block-rows of its own columns, and
 // the two tiles sharing the line run ~1/8 of a block-row apart on the same XCD.
-void xcd_bands(const std::vector<const costa_tile_op_t*>& ops, int64_t E, int k, std::vector<uint32_t>& perm) {
+void xcd_bands(const std::vector<const costa_tile_op_t*>& ops, int64_t E, int k, bool local,
+               std::vector<uint32_t>& perm) {
     const uint64_t nb = 8 * uint64_t(k);  // bands: XCD x walks bands k x .. k x + k - 1 in turn
     const size_t n = perm.size();
     std::vector<uint64_t> pieces(n);
     uint64_t total = 0;
     for (size_t i = 0; i < n; ++i) {
-        const wave_grid g = wave_pieces(*ops[i], E);
+        const wave_grid g = wave_pieces(*ops[i], E, local);
         pieces[i] = uint64_t(g.nfc * g.nsc);
         total += pieces[i];
     }
@@ -627,7 +639,8 @@ const wave_knobs& knobs() {
 
 work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops_in,
                       std::vector<costa_tile_op_t>& ordered, std::vector<uint64_t>& work,
-                      bool pack_list) {
+                      list_kind kind) {
+    const bool pack_list = kind == list_pack, local = kind == list_local;
     // Sources off the 16-byte grid: 4-byte elements are read as 16-byte vectors anyway (dword
     // alignment suffices for global_load_dwordx4): fp32 16384^2 'T' with lld 16386 0.405 against
     // 0.499 ms element by element; 8-byte elements stay element-wise (0.794 against 0.755 ms);
@@ -677,7 +690,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         const bool aligned = (op.flags & vec_both) == vec_both;
         bool large = 2 * elems >= lo;
         if (kn.policy == 2 && !aligned && elems <= kUnalignedWaveCap * sub_elems) large = false;
-        return large && !is_tiny(op, E);
+        return large && !is_tiny(op, E, local);
     };
     // A transposing list whose large ops all fit the square variant of the large shape (bf_q x
     // bs_q) runs them on it: one sub-tile per op instead of a half-filled large one (fp64 / c64 /
@@ -923,13 +936,13 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         for (size_t i = 0; i < nw; ++i) perm[i] = uint32_t(i);
     }
     if (chain && nw > 1) chain_source_neighbours(wave_ops, E, perm);
-    if (kn.xcd_bands && mode == 2 && top > 0 && nw > 1) xcd_bands(wave_ops, E, kn.xcd_bands, perm);
+    if (kn.xcd_bands && mode == 2 && top > 0 && nw > 1) xcd_bands(wave_ops, E, kn.xcd_bands, local, perm);
     if (kn.sort == 7 && !pack_list && nw > 1) merge_row_bands(wave_ops, kn.band_h, perm);
     // pieces: count per op, scan, fill (host threads for long lists)
     std::vector<wave_grid> grid(nw);
     std::vector<size_t> at_piece(nw + 1, 0);
     host_parallel(nw, [&](size_t b, size_t e) {
-        for (size_t i = b; i < e; ++i) grid[i] = wave_pieces(*wave_ops[perm[i]], E);
+        for (size_t i = b; i < e; ++i) grid[i] = wave_pieces(*wave_ops[perm[i]], E, local);
     });
     for (size_t i = 0; i < nw; ++i)
         at_piece[i + 1] = at_piece[i] + size_t(grid[i].nfc * grid[i].nsc);
@@ -956,7 +969,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     ordered.resize(base + at_piece[nw]);
     host_parallel(nw, [&](size_t b, size_t e) {
         for (size_t i = b; i < e; ++i)
-            emit_pieces(*wave_ops[perm[i]], E, grid[i], &ordered[base + at_piece[i]]);
+            emit_pieces(*wave_ops[perm[i]], E, grid[i], local, &ordered[base + at_piece[i]]);
     });
     return w;
 }
@@ -1436,8 +1449,8 @@ cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
         auto x = std::make_unique<cached_plan::xround>();
         x->tr_unpack = any_transpose(up[size_t(r)]);
         x->ax_unpack = any_axpby(up[size_t(r)]);
-        x->l_pack = build_work(p.dtype, pk[size_t(r)], ord_p[size_t(r)], w_p[size_t(r)], true);
-        x->l_unpack = build_work(p.dtype, up[size_t(r)], ord_u[size_t(r)], w_u[size_t(r)]);
+        x->l_pack = build_work(p.dtype, pk[size_t(r)], ord_p[size_t(r)], w_p[size_t(r)], list_pack);
+        x->l_unpack = build_work(p.dtype, up[size_t(r)], ord_u[size_t(r)], w_u[size_t(r)], list_unpack);
         cp->rounds.push_back(std::move(x));
     }
     t_work = now() - t0 - t_resid - t_plan;

@@ -170,7 +170,7 @@ int64_t tiny_lds_budget();
 constexpr int tiny_copy_lane_bytes(size_t) { return 64; }
 // bytes of one copy-mode wavefront op / of one transposing wavefront op's staged tile (the
 // budgets the host split cuts to)
-int64_t tiny_copy_budget(int64_t elem_size);
+int64_t tiny_copy_budget(int64_t elem_size, bool local_list = true);
 // a large op that is not 16-byte aligned on both sides takes the wavefront path up to this many
 // large sub-tiles of data (engine.cpp wave_knobs::policy)
 constexpr int64_t kUnalignedWaveCap = 4;
@@ -225,11 +225,13 @@ struct work_split {
     bool skew_wide = false; // the skew items are sub-tiles of its wide variant (bf_kw x bs_kw)
     int64_t n_items() const { return n_large + n_medium + n_skew + n_tiny; }
 };
-// pack_list: the ops write the dense send package (their destinations are contiguous whatever
-// their order), which changes the wavefront ops' order (wave_knobs::sort)
+// list_pack: the ops write the dense send package (their destinations are contiguous whatever
+// their order), which changes the wavefront ops' order (wave_knobs::sort); local lists (both
+// sides user matrices) cut copy ops finer than pack / unpack lists (tiny_copy_budget)
+enum list_kind { list_local, list_pack, list_unpack };
 work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops,
                       std::vector<costa_tile_op_t>& ordered, std::vector<uint64_t>& work,
-                      bool pack_list = false);
+                      list_kind kind = list_local);
 // launch arguments of one ordered op list
 launch_args make_launch(const work_split& w, const void* d_ordered, const void* d_work,
                         const char* src_base, char* dst_base, const void* d_scalars, bool transpose,

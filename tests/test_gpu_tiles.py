@@ -20,9 +20,10 @@ torch = pytest.importorskip("torch")
 TINY_LDS = 4096  # engine.hpp kTinyLdsDefault
 
 
-def tiny_copy(E):
-    """engine.cpp tiny_copy_budget: 3/4 of a wavefront pass, 48 lanes x tiny_copy_lane_bytes"""
-    return 48 * 64
+def tiny_copy(E, local=True):
+    """engine.cpp tiny_copy_budget: half a wavefront pass for local lists (32 lanes x
+    tiny_copy_lane_bytes), 3/4 for pack / unpack lists (48 lanes)"""
+    return (32 if local else 48) * 64
 
 
 @pytest.fixture(scope="module")
@@ -47,7 +48,7 @@ def _shape(rng, E, transpose):
     if pick == 0:  # tiny, ragged
         return int(rng.integers(1, 70)), int(rng.integers(1, 70))
     if pick == 1:  # at the tiny boundary
-        limit = (TINY_LDS if transpose else tiny_copy(E)) // E
+        limit = (TINY_LDS if transpose else tiny_copy(E, bool(rng.integers(0, 2)))) // E
         nf = int(rng.integers(1, 129))
         ns = max(1, limit // ((nf | 1) if transpose else nf) + int(rng.integers(-1, 2)))
         return nf, ns

@@ -65,7 +65,8 @@ static grid_layout<float> layout(const std::vector<int>& rs, const std::vector<i
 // half a large sub-tile, unaligned ones above kUnalignedWaveCap sub-tiles, transposes into
 // unaligned destinations (the skew shape, engine.cpp build_work), and in lists that transpose,
 // aligned transposing ops of at least half a medium sub-tile
-static std::set<uint32_t> expected_shaped(costa_dtype_t dt, const std::vector<costa_tile_op_t>& ops) {
+static std::set<uint32_t> expected_shaped(costa_dtype_t dt, const std::vector<costa_tile_op_t>& ops,
+                                          bool pack = false) {
     bool tr = false;
     for (const auto& o : ops) tr = tr || (o.flags & COSTA_TILE_TRANSPOSE);
     shape_dims sh;
@@ -87,7 +88,7 @@ static std::set<uint32_t> expected_shaped(costa_dtype_t dt, const std::vector<co
             large.insert(o.order);
             continue;
         }
-        const bool tiny = (t ? int64_t(o.nf | 1) * o.ns * E <= tiny_lds_budget() : e * E <= tiny_copy_budget(E));
+        const bool tiny = (t ? int64_t(o.nf | 1) * o.ns * E <= tiny_lds_budget() : e * E <= tiny_copy_budget(E, !pack));
         const bool lg = 2 * e >= big && (al || e > kUnalignedWaveCap * big) && !tiny;
         if (lg) large.insert(o.order);
         else if (med > 0 && al && t && 2 * e >= med) medium.insert(o.order);
@@ -110,8 +111,9 @@ static bool check_list(const std::string& name, costa_dtype_t dt, const std::vec
     const int64_t E = int64_t(dtype_size(dt));
     std::vector<costa_tile_op_t> ord, ord2;
     std::vector<uint64_t> work, work2;
-    const work_split w = build_work(dt, ops, ord, work, pack);
-    build_work(dt, ops, ord2, work2, pack);
+    const list_kind kind = pack ? list_pack : list_local;
+    const work_split w = build_work(dt, ops, ord, work, kind);
+    build_work(dt, ops, ord2, work2, kind);
     // (skew ops that continue each other are merged: fewer shaped ops than parents)
     CHECK(w.tiny_first <= int64_t(shaped.size()) && (w.tiny_first == 0) == shaped.empty(),
           "%lld ops on the sub-tiled shapes, expected %zu", (long long)w.tiny_first, shaped.size());
@@ -145,7 +147,7 @@ static bool check_list(const std::string& name, costa_dtype_t dt, const std::vec
         const costa_tile_op_t& s = ord[size_t(i)];
         const bool tr = s.flags & COSTA_TILE_TRANSPOSE;
         const int64_t bytes = tr ? int64_t(s.nf | 1) * s.ns * E : int64_t(s.nf) * s.ns * E;
-        CHECK(bytes <= (tr ? tiny_lds_budget() : tiny_copy_budget(E)), "piece %lld over budget (%lld B)",
+        CHECK(bytes <= (tr ? tiny_lds_budget() : tiny_copy_budget(E, !pack)), "piece %lld over budget (%lld B)",
               (long long)i, (long long)bytes);
         auto it = parent.find(s.order);
         CHECK(it != parent.end(), "piece %lld has no parent", (long long)i);
@@ -196,7 +198,7 @@ int main() {
         if (!check_list(std::string("cfg5 sub-list ") + op, p->dtype, sub, expected_shaped(p->dtype, sub)))
             return 1;
         // the same as a pack list (wavefront ops by source address)
-        if (!check_list(std::string("cfg5 pack sub-list ") + op, p->dtype, sub, expected_shaped(p->dtype, sub), true))
+        if (!check_list(std::string("cfg5 pack sub-list ") + op, p->dtype, sub, expected_shaped(p->dtype, sub, true), true))
             return 1;
     }
     // unaligned large ops: fp32 4096^2 'T' with lld = 4097 (columns 4-byte aligned only)
