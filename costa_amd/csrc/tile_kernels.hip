@@ -959,6 +959,9 @@ struct lin {  // (f, s) of linear element index e = f + s*n, stepped by 64
 #ifndef COSTA_TINY_GLDS  // 0: register staging (tuning builds only)
 #define COSTA_TINY_GLDS 1
 #endif
+#ifndef COSTA_TINY_GLDS_AUX  // cache policy bits of the LDS-DMA loads (tuning builds: 2 = nt)
+#define COSTA_TINY_GLDS_AUX 0
+#endif
 #ifndef COSTA_TINY_Y_BYTES  // old destination values requested before the wait: a whole staged op
 #define COSTA_TINY_Y_BYTES kTinyLdsDefault
 #endif
@@ -982,7 +985,7 @@ __device__ __forceinline__ void tiny_transpose_glds(const T* src, T* dst, int nf
         for (int d0 = 0; d0 < nd; d0 += 64) {
             if (f < nf && d0 + lane < nd)
                 __builtin_amdgcn_global_load_lds((glob_void*)(sb + (int64_t(s) * lds + f) * int64_t(sizeof(T))),
-                                                 (lds_void*)(tb + 4 * d0), 4, 0, 0);
+                                                 (lds_void*)(tb + 4 * d0), 4, 0, COSTA_TINY_GLDS_AUX);
             f += df;
             s += ds;
             if (f >= pitch) {
