@@ -511,7 +511,8 @@ void xcd_bands(const std::vector<const costa_tile_op_t*>& ops, int64_t E, int k,
 // Merges ops that continue each other: the op whose source starts where op a's source ends along
 // s (a.src + a.ns * lds) and whose destination continues a's the same way (one destination
 // stride further for copies, ns elements further for transposes), with the same extent along f,
-// strides and flags, joins a (then the same along f).  Same elements, same transform: only the
+// strides and flags (16-byte alignment flags aside: the merged op keeps a's, which describe its
+// start and strides), joins a (then the same along f).  Same elements, same transform: only the
 // op boundaries move.  Order hint: the smaller one.
 void merge_adjacent(std::vector<costa_tile_op_t>& v, int64_t E) {
     if (v.size() < 2) return;
@@ -535,7 +536,8 @@ void merge_adjacent(std::vector<costa_tile_op_t>& v, int64_t E) {
                 const auto it = by_src.find(next_src);
                 if (it == by_src.end() || gone[it->second] || it->second == i) break;
                 const costa_tile_op_t& b = v[it->second];
-                const bool same = b.dst == next_dst && b.flags == a.flags && b.lds == a.lds &&
+                const uint32_t vec = COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST;
+                const bool same = b.dst == next_dst && (b.flags & ~vec) == (a.flags & ~vec) && b.lds == a.lds &&
                                   b.ldd == a.ldd && (pass == 0 ? b.nf == a.nf : b.ns == a.ns);
                 const int64_t total = n + (pass == 0 ? b.ns : b.nf);
                 if (!same || total > (int64_t(1) << 30)) break;
@@ -549,6 +551,23 @@ void merge_adjacent(std::vector<costa_tile_op_t>& v, int64_t E) {
             if (!gone[i]) v[o++] = v[i];
         v.resize(o);
     }
+}
+
+// Only ops with equal strides can continue each other: block-cyclic layouts have one stride per
+// local matrix, while a custom layout whose blocks are separate buffers has one per block (cfg 5:
+// hundreds), whose tiles practically never continue across blocks.  Lists with more than 16
+// distinct source strides skip the merge (cfg 5's 245 k ops: the merge pass cost 2x build_work).
+bool few_strides(const std::vector<costa_tile_op_t>& ops) {
+    int32_t seen[16];
+    int k = 0;
+    for (const auto& o : ops) {
+        bool found = false;
+        for (int i = 0; i < k && !found; ++i) found = seen[i] == o.lds;
+        if (found) continue;
+        if (k == 16) return false;
+        seen[k++] = o.lds;
+    }
+    return true;
 }
 
 // runs fn(begin, end) over [0, n) on up to 8 host threads (one when n is small)
@@ -602,6 +621,8 @@ struct wave_knobs {  // defaults, overridable for tuning runs
                          // ms; copy lists untested under 2; tools/order_run.sh,
                          // tools/f32_order_run.sh, profiles/r2/order/)
     int band_h = 2;  // COSTA_BAND_H: destination rows merged per band (sort mode 7)
+    int merge = 1;      // COSTA_MERGE=0: ops that continue each other are not merged (tuning; the
+                        // skew list always merges)
     int xcd_bands = 1;  // COSTA_XCD_BANDS=k: destination-ordered wavefront lists in 8 k column
                         // bands, k per XCD (xcd_bands); 0: off.  cfg 5 'N' 0.476 -> 0.446 ms with
                         // k = 1 (2 / 4 / 16: 0.464 / 0.475 / 0.490), 'T' equal; through the
@@ -631,6 +652,7 @@ const wave_knobs& knobs() {
         if (const char* s = std::getenv("COSTA_SKEW_XCD")) x.skew_xcd = std::max(-1, std::atoi(s));
         if (const char* s = std::getenv("COSTA_BAND_H")) x.band_h = std::max(1, std::atoi(s));
         if (const char* s = std::getenv("COSTA_XCD_BANDS")) x.xcd_bands = std::atoi(s);
+        if (const char* s = std::getenv("COSTA_MERGE")) x.merge = std::atoi(s);
         return x;
     }();
     return k;
@@ -652,9 +674,30 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     }();
     // (by default only for ops of at least one large sub-tile: smaller ones keep their class)
     const int mis = mis_env >= 0 ? mis_env : dtype_size(dtype) == 4 ? 2 : 0;
+    // small tiles (below half a large sub-tile) of one local matrix that continue each other in
+    // source and destination become one op (a 16384^2 'T' with 24^2 blocks on one rank: one op on
+    // the large shape instead of 466 k wavefront tiles); ops already on the large shape stay as
+    // the planner cut them
+    const wave_knobs& kn0 = knobs();
+    std::vector<costa_tile_op_t> ops_merged;
+    const std::vector<costa_tile_op_t>* ops_src = &ops_in;
+    if (kn0.merge && ops_in.size() > 1 && few_strides(ops_in)) {
+        shape_dims sh0;
+        tile_shapes(dtype, any_transpose(ops_in), &sh0);
+        const int64_t half_large = int64_t(sh0.bf) * sh0.bs / 2;
+        std::vector<costa_tile_op_t> small;
+        for (const auto& op : ops_in)
+            (int64_t(op.nf) * op.ns < half_large ? small : ops_merged).push_back(op);
+        const size_t n_small = small.size();
+        merge_adjacent(small, int64_t(dtype_size(dtype)));
+        if (small.size() < n_small) {
+            ops_merged.insert(ops_merged.end(), small.begin(), small.end());
+            ops_src = &ops_merged;
+        }
+    }
     std::vector<costa_tile_op_t> ops_mis;
     if (mis) {
-        ops_mis = ops_in;
+        ops_mis = *ops_src;
         const uint64_t E = dtype_size(dtype);
         shape_dims shm;
         tile_shapes(dtype, any_transpose(ops_in), &shm);
@@ -665,7 +708,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
             if ((mis & 2) && op.src % 4 == 0 && (uint64_t(op.lds) * E) % 4 == 0) op.flags |= COSTA_TILE_VEC_SRC;
         }
     }
-    const std::vector<costa_tile_op_t>& ops = mis ? ops_mis : ops_in;
+    const std::vector<costa_tile_op_t>& ops = mis ? ops_mis : *ops_src;
     const bool tr_shape = any_transpose(ops);
     shape_dims sh;
     tile_shapes(dtype, tr_shape, &sh);

@@ -38,9 +38,14 @@ def main():
     costa.synchronize(comm)
     st = costa.get_stats(reset=True)
     ms = st["local_ms"] / steps
-    gbps = (3 if beta != 0 else 2) * n * n * es / (ms * 1e-3) / 1e9
+    gbps = (3 if beta != 0 else 2) * n * n * es / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    extra = ""
+    if st["pack_launches"]:  # COSTA_LOOPBACK=1: every tile through the exchange
+        extra = "".join(f"  {k} {st[k + '_ms'] / steps:.4f} ms "
+                        f"{st[k + '_bytes'] / steps / (st[k + '_ms'] / steps * 1e-3) / 1e9:7.1f} GB/s"
+                        for k in ("pack", "unpack"))
     print(f"{dt} {n}^2 block {b} beta {beta} sort {os.environ.get('COSTA_LARGE_SORT', '1')}: "
-          f"kernel {ms:.4f} ms {gbps:8.1f} GB/s", flush=True)
+          f"kernel {ms:.4f} ms {gbps:8.1f} GB/s{extra}", flush=True)
 
 
 if __name__ == "__main__":

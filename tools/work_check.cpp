@@ -14,7 +14,10 @@
 //   unaligned large ops (fp32, lld % 4 != 0): transposes into unaligned destinations take the
 //     skew shape; other ops up to kUnalignedWaveCap large sub-tiles are cut into wavefront
 //     pieces (the same checks), bigger ones stay on the large shape.
+//   run with COSTA_MERGE=0 (ops that continue each other stay apart: every op has one parent);
+//   `work_check merge` checks the merging itself.
 // Prints "ok" and exits 0, or prints the first violation and exits 1.
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -183,7 +186,58 @@ static std::unique_ptr<plan> plan_of(const elayout& a, const elayout& c, char op
     return make_plan({j}, 0, 1);
 }
 
-int main() {
+// merging (engine.cpp merge_adjacent, run with COSTA_MERGE unset): a 4096^2 matrix on one rank
+// with 24^2 blocks, 'T' and 'N', fp32 and fp64: every tile continues its neighbours in source and
+// destination, so the list becomes one op on the large shape; with a ragged last block row
+// (4100^2: blocks of 24 and 20 rows) the ops still cover every element once
+static bool check_merge() {
+    const std::string name = "merge";
+    for (int m : {4096, 4100})
+        for (char op : {'T', 'N'}) {
+            auto A = block_cyclic_layout<float>(m, m, 24, 24, 1, 1, m, m, 1, 1, 'R', 0, 0,
+                                                reinterpret_cast<float*>(uint64_t(1) << 40), m, 'C', 0);
+            auto C = block_cyclic_layout<float>(m, m, 24, 24, 1, 1, m, m, 1, 1, 'R', 0, 0,
+                                                reinterpret_cast<float*>(uint64_t(1) << 41), m, 'C', 0);
+            elayout ea = erase(A), ec = erase(C);
+            auto p = plan_of(ea, ec, op, 1.f, 0.f);
+            std::vector<costa_tile_op_t> ord;
+            std::vector<uint64_t> work;
+            const work_split w = build_work(p->dtype, p->local_ops, ord, work, list_local);
+            int64_t area = 0;
+            for (const auto& o : ord) area += int64_t(o.nf) * o.ns;
+            // (pieces of wavefront ops are in `ord` after tiny_first; shaped ops before)
+            CHECK(area == int64_t(m) * m, "%c %d: ops cover %lld of %lld elements", op, m, (long long)area,
+                  (long long)int64_t(m) * m);
+            CHECK(p->local_ops.size() > 1000 && w.tiny_first <= 2 && w.n_tiny == 0 && w.n_large > 0,
+                  "%c %d: %zu tiles -> %lld shaped ops, %lld pieces", op, m, p->local_ops.size(),
+                  (long long)w.tiny_first, (long long)w.n_tiny);
+            std::printf("merge %c %d: %zu tiles -> %lld op(s), %lld large sub-tiles\n", op, m,
+                        p->local_ops.size(), (long long)w.tiny_first, (long long)w.n_large);
+        }
+    return true;
+}
+
+int main(int argc, char** argv) {
+    if (argc > 1 && std::string(argv[1]) == "time") {  // build_work on cfg 5's 'N' list (host cost)
+        const int n = 16384;
+        auto LA = layout(splits(0xC5A1, 8, 96, n), splits(0xC5A2, 8, 96, n), uint64_t(1) << 40);
+        auto LC = layout(splits(0xC5A3, 16, 160, n), splits(0xC5A4, 16, 160, n), uint64_t(1) << 41);
+        elayout a = erase(LA), c = erase(LC);
+        auto p = plan_of(a, c, 'N', 1.f, 0.f);
+        std::vector<costa_tile_op_t> ord;
+        std::vector<uint64_t> work;
+        build_work(p->dtype, p->local_ops, ord, work, list_local);
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int k = 0; k < 5; ++k) build_work(p->dtype, p->local_ops, ord, work, list_local);
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / 5;
+        std::printf("build_work cfg 5 'N' (%zu ops): %.2f ms\n", p->local_ops.size(), ms);
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "merge") {
+        if (!check_merge()) return 1;
+        std::printf("ok\n");
+        return 0;
+    }
     const int n = 16384;
     auto LA = layout(splits(0xC5A1, 8, 96, n), splits(0xC5A2, 8, 96, n), uint64_t(1) << 40);
     auto LC = layout(splits(0xC5A3, 16, 160, n), splits(0xC5A4, 16, 160, n), uint64_t(1) << 41);
