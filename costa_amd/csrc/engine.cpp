@@ -513,8 +513,15 @@ void xcd_bands(const std::vector<const costa_tile_op_t*>& ops, int64_t E, int k,
 // stride further for copies, ns elements further for transposes), with the same extent along f,
 // strides and flags (16-byte alignment flags aside: the merged op keeps a's, which describe its
 // start and strides), joins a (then the same along f).  Same elements, same transform: only the
-// op boundaries move.  Order hint: the smaller one.
-void merge_adjacent(std::vector<costa_tile_op_t>& v, int64_t E) {
+// op boundaries move.  Order hint: the smaller one.  `root` (optional): for every input op, the
+// input op it ended up merged into (itself when it survives).
+void merge_adjacent(std::vector<costa_tile_op_t>& v, int64_t E, std::vector<uint32_t>* root = nullptr) {
+    std::vector<uint32_t> id(v.size());  // input index of each op of v
+    for (size_t i = 0; i < v.size(); ++i) id[i] = uint32_t(i);
+    if (root) {
+        root->resize(v.size());
+        for (size_t i = 0; i < v.size(); ++i) (*root)[i] = uint32_t(i);
+    }
     if (v.size() < 2) return;
     for (int pass = 0; pass < 2; ++pass) {  // 0: along s, 1: along f
         std::unordered_map<uint64_t, uint32_t> by_src;
@@ -544,13 +551,52 @@ void merge_adjacent(std::vector<costa_tile_op_t>& v, int64_t E) {
                 (pass == 0 ? a.ns : a.nf) = int32_t(total);
                 a.order = std::min(a.order ? a.order : b.order, b.order ? b.order : a.order);
                 gone[it->second] = 1;
+                if (root) (*root)[id[it->second]] = id[i];
             }
         }
         size_t o = 0;
         for (size_t i = 0; i < v.size(); ++i)
-            if (!gone[i]) v[o++] = v[i];
+            if (!gone[i]) {
+                id[o] = id[i];
+                v[o++] = v[i];
+            }
         v.resize(o);
+        id.resize(o);
     }
+    if (root)  // path compression: pass 1 merged pass-0 survivors
+        for (size_t i = 0; i < root->size(); ++i) {
+            uint32_t r = (*root)[i];
+            while ((*root)[r] != r) r = (*root)[r];
+            (*root)[i] = r;
+        }
+}
+
+// Small ops of a list merged (merge_adjacent), keeping a merged op only when it fills the large
+// shape's sub-tiles at least half along each dimension (bf x bs): a strip of one block's width
+// (nf = 24 of a 64-wide sub-tile, say, a package's tiles continuing along s) would run the large
+// shape a third full, slower than its tiles on the wavefront path (loopback unpack fp64 24^2
+// beta != 0: 1.571 against 1.412 ms); its tiles stay apart instead.
+std::vector<costa_tile_op_t> merge_small(const std::vector<costa_tile_op_t>& small, int64_t E, int bf, int bs) {
+    std::vector<costa_tile_op_t> v = small;
+    std::vector<uint32_t> root;
+    merge_adjacent(v, E, &root);
+    if (v.size() == small.size()) return v;
+    std::vector<costa_tile_op_t> out;
+    out.reserve(small.size());
+    std::vector<char> keep(small.size(), 0);  // per root: the merged op is kept
+    std::vector<uint32_t> count(small.size(), 0);
+    for (size_t i = 0; i < small.size(); ++i) ++count[root[i]];
+    // v holds the surviving ops in input order, i.e. in the order of their roots
+    size_t k = 0;
+    for (size_t i = 0; i < small.size(); ++i) {
+        if (root[i] != i) continue;
+        const costa_tile_op_t& m = v[k++];
+        keep[i] = count[i] == 1 || (2 * int64_t(m.nf) >= bf && 2 * int64_t(m.ns) >= bs);
+        if (keep[i]) out.push_back(m);
+    }
+    for (size_t i = 0; i < small.size(); ++i)
+        if (!keep[root[i]]) out.push_back(small[i]);
+    return out;
 }
 
 // Only ops with equal strides can continue each other: block-cyclic layouts have one stride per
@@ -689,7 +735,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         for (const auto& op : ops_in)
             (int64_t(op.nf) * op.ns < half_large ? small : ops_merged).push_back(op);
         const size_t n_small = small.size();
-        merge_adjacent(small, int64_t(dtype_size(dtype)));
+        small = merge_small(small, int64_t(dtype_size(dtype)), sh0.bf, sh0.bs);
         if (small.size() < n_small) {
             ops_merged.insert(ops_merged.end(), small.begin(), small.end());
             ops_src = &ops_merged;

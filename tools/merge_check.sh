@@ -9,3 +9,4 @@ for m in 1 0; do
   done
 done
 timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-e2e --no-extra > $O/bench.json 2> $O/bench.err || exit 1
+bash tools/merge_loopback.sh $(basename $O)_lb || exit 1

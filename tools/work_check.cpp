@@ -214,6 +214,28 @@ static bool check_merge() {
             std::printf("merge %c %d: %zu tiles -> %lld op(s), %lld large sub-tiles\n", op, m,
                         p->local_ops.size(), (long long)w.tiny_first, (long long)w.n_large);
         }
+    // tiles that continue each other along s only (each strip's destination elsewhere): merged
+    // they would be 24-wide strips, a third of the fp64 sub-tile, so they stay apart
+    std::vector<costa_tile_op_t> strips;
+    const int64_t lda = 4096;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 170; ++j) {
+            costa_tile_op_t o{};
+            o.src = (uint64_t(1) << 40) + uint64_t((j * 24 * lda + i * 24) * 8);
+            o.dst = (uint64_t(1) << 41) + (uint64_t(i) << 32) + uint64_t(j * 24 * 8);
+            o.nf = o.ns = 24;
+            o.lds = int32_t(lda);
+            o.ldd = 8192;
+            o.flags = COSTA_TILE_TRANSPOSE | COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST;
+            o.order = uint32_t(strips.size() + 1);
+            strips.push_back(o);
+        }
+    std::vector<costa_tile_op_t> ord;
+    std::vector<uint64_t> work;
+    const work_split w = build_work(COSTA_DOUBLE, strips, ord, work, list_unpack);
+    CHECK(w.tiny_first == 0 && w.n_large == 0, "thin strips: %lld shaped ops", (long long)w.tiny_first);
+    std::printf("merge: %zu tiles continuing along s only -> %lld shaped ops, %lld pieces\n", strips.size(),
+                (long long)w.tiny_first, (long long)w.n_tiny);
     return true;
 }
 
