@@ -357,3 +357,44 @@ def test_unaligned_skew_vs_oracle(gpu, dtype, pad, ab, geo):
     gpu.transform(A, Cl, gpu.Comm.self(0), "T", alpha, beta)
     got = host(dc, npd)
     assert got.tobytes() == expected.tobytes()
+
+
+@pytest.mark.parametrize("dtype", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("trans", ["N", "T", "C"])
+@pytest.mark.parametrize("geo", [(1000, 1100, 24, 24, 1, 1, 0), (1037, 997, 24, 20, 3, 5, 2),
+                                 (2048, 700, 16, 16, 1, 1, 1)],
+                         ids=["b24", "ragged-sub-pad", "b16-pad"])
+def test_merged_small_blocks_vs_oracle(gpu, dtype, trans, geo):
+    """small blocks on one rank: the tiles of the local matrix continue each other on both sides
+    and merge into large-shape ops (engine.cpp merge_small); ragged last blocks, sub-matrices
+    and ld padding (16-byte alignment of the merged op from its first tile only); alpha, beta !=
+    0 on half the cases; bit-exact vs the oracle"""
+    if trans == "C" and dtype not in (2, 3):
+        pytest.skip("conjugate: complex types only")
+    m, n, mb, nb, ia, ja, pad = geo
+    rng = np.random.default_rng(29 + mb + pad)
+    tr = trans != "N"
+    if tr:
+        a_case = BC(n + ja, m + ia, nb, mb, ia=ja, ja=ia, subm=n, subn=m, lld_pad=pad)
+    else:
+        a_case = BC(m + ia, n + ja, mb, nb, ia=ia, ja=ja, subm=m, subn=n, lld_pad=pad)
+    c_case = BC(m + ia, n + ja, mb, nb, ia=ia, ja=ja, subm=m, subn=n, lld_pad=pad)
+    npd = oracle.NP[dtype]
+    na, nc = a_case.buf_elems(0, 1), c_case.buf_elems(0, 1)
+    axpby = (m + dtype) % 2 == 0
+    if dtype == 4:
+        a = rng.integers(-2**20, 2**20, na).astype(npd)
+        c = rng.integers(-2**20, 2**20, nc).astype(npd)
+        alpha, beta = (3, -2) if axpby else (1, 0)
+    else:
+        a = oracle.gen(dtype, 3, 0, na)
+        c = oracle.gen(dtype, 4, 0, nc)
+        alpha, beta = ((0.75 - 0.5j, 1.25 + 0.25j) if dtype in (2, 3) else (-1.5, 0.25)) if axpby else (1, 0)
+    expected = c.copy()
+    oracle.transform(dtype, trans, alpha, beta, a_case.geom(1), [a], c_case.geom(1), [expected])
+    da, dc = dev(a), dev(c)
+    A = a_case.make_layout(0, da.data_ptr(), 1, dtype)
+    Cl = c_case.make_layout(0, dc.data_ptr(), 1, dtype)
+    gpu.transform(A, Cl, gpu.Comm.self(0), trans, alpha, beta)
+    got = host(dc, npd)
+    assert got.tobytes() == expected.tobytes()
