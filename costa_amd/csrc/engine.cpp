@@ -667,6 +667,8 @@ struct wave_knobs {  // defaults, overridable for tuning runs
                          // ms; copy lists untested under 2; tools/order_run.sh,
                          // tools/f32_order_run.sh, profiles/r2/order/)
     int band_h = 2;  // COSTA_BAND_H: destination rows merged per band (sort mode 7)
+    int force_sq = 0;   // COSTA_FORCE_SQ=1 (tuning): transposing lists of fp64 / c64 / c128 take the
+                        // square sub-tile whatever their ops' size
     int merge = 1;      // COSTA_MERGE=0: ops that continue each other are not merged (tuning; the
                         // skew list always merges)
     int xcd_bands = 1;  // COSTA_XCD_BANDS=k: destination-ordered wavefront lists in 8 k column
@@ -699,6 +701,7 @@ const wave_knobs& knobs() {
         if (const char* s = std::getenv("COSTA_BAND_H")) x.band_h = std::max(1, std::atoi(s));
         if (const char* s = std::getenv("COSTA_XCD_BANDS")) x.xcd_bands = std::atoi(s);
         if (const char* s = std::getenv("COSTA_MERGE")) x.merge = std::atoi(s);
+        if (const char* s = std::getenv("COSTA_FORCE_SQ")) x.force_sq = std::atoi(s);
         return x;
     }();
     return k;
@@ -793,7 +796,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         const costa_tile_op_t& op = ops[li];
         if (op.nf <= 0 || op.ns <= 0 || !is_large(op, q_lo)) continue;
         ++n_cand;
-        sq = op.nf <= sh.bf_q && op.ns <= sh.bs_q;
+        sq = kn.force_sq || (op.nf <= sh.bf_q && op.ns <= sh.bs_q);
     }
     sq = sq && n_cand > 0;
     const int64_t large_lo = sq ? q_lo : sub_elems;
