@@ -12,6 +12,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import costa_amd as costa  # noqa: E402
 
 
+OP = os.environ.get("COSTA_PROBE_OP", "T")  # op of the probe transform (tuning: N for copies)
+
+
 def main():
     dt, n, b, beta = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), float(sys.argv[4])
     steps = int(sys.argv[5]) if len(sys.argv) > 5 else 10
@@ -29,12 +32,12 @@ def main():
                                    dtype=cd)
     al = 0.5 if beta != 0 else 1.0
     for _ in range(3):
-        costa.transform_async(LA, LC, comm, "T", al, beta)
+        costa.transform_async(LA, LC, comm, OP, al, beta)
     costa.synchronize(comm)
     costa.set_profiling(True)
     costa.get_stats(reset=True)
     for _ in range(steps):
-        costa.transform_async(LA, LC, comm, "T", al, beta)
+        costa.transform_async(LA, LC, comm, OP, al, beta)
     costa.synchronize(comm)
     st = costa.get_stats(reset=True)
     ms = st["local_ms"] / steps
