@@ -962,6 +962,21 @@ struct lin {  // (f, s) of linear element index e = f + s*n, stepped by 64
 #ifndef COSTA_TINY_GLDS_AUX  // cache policy bits of the LDS-DMA loads (tuning builds: 2 = nt)
 #define COSTA_TINY_GLDS_AUX 0
 #endif
+template <typename T> __device__ __forceinline__ T nt_elem_load(const T* p) { return __builtin_nontemporal_load(p); }
+template <typename R> __device__ __forceinline__ cpx<R> nt_elem_load(const cpx<R>* p) {
+    return {__builtin_nontemporal_load(&p->re), __builtin_nontemporal_load(&p->im)};
+}
+template <typename T> __device__ __forceinline__ void nt_elem_store(T v, T* p) { __builtin_nontemporal_store(v, p); }
+template <typename R> __device__ __forceinline__ void nt_elem_store(cpx<R> v, cpx<R>* p) {
+    __builtin_nontemporal_store(v.re, &p->re);
+    __builtin_nontemporal_store(v.im, &p->im);
+}
+#ifndef COSTA_TINY_NT_ST  // tuning builds: nontemporal destination stores / old-value loads
+#define COSTA_TINY_NT_ST 0
+#endif
+#ifndef COSTA_TINY_NT_LD
+#define COSTA_TINY_NT_LD 0
+#endif
 #ifndef COSTA_TINY_Y_BYTES  // old destination values requested before the wait: a whole staged op
 #define COSTA_TINY_Y_BYTES kTinyLdsDefault
 #endif
@@ -1002,7 +1017,11 @@ __device__ __forceinline__ void tiny_transpose_glds(const T* src, T* dst, int nf
 #pragma unroll
             for (int u = 0; u < NY; ++u) {
                 if (u * 64 >= total) break;
+#if COSTA_TINY_NT_LD
+                if (u * 64 + lane < total) y[u] = nt_elem_load(dst + int64_t(q.s) * ldd + q.f);
+#else
                 if (u * 64 + lane < total) y[u] = dst[int64_t(q.s) * ldd + q.f];
+#endif
                 q.step();
             }
         }
@@ -1017,7 +1036,11 @@ __device__ __forceinline__ void tiny_transpose_glds(const T* src, T* dst, int nf
             T* d = dst + int64_t(q.s) * ldd + q.f;
             T old = e_zero<T>();
             if (AX && kind == COSTA_SCALE_AXPBY) old = u < NY ? y[AX && u < NY ? u : 0] : *d;
+#if COSTA_TINY_NT_ST
+            nt_elem_store(scale(v, old, kind, conj, alpha, beta), d);
+#else
             *d = scale(v, old, kind, conj, alpha, beta);
+#endif
         }
         q.step();
     }
