@@ -376,9 +376,17 @@ wave_grid wave_pieces(const costa_tile_op_t& op, int64_t E, bool local) {
     const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
     const int64_t budget = (tr ? tiny_lds_budget() : tiny_copy_budget(E, local)) / E;  // elements
     const int64_t nf = op.nf, ns = op.ns;
-    // transpose: near-square pieces (both the source columns and the destination rows stay
-    // long); copy: whole columns when one fits, else tall pieces
-    const int64_t side = tr ? std::max<int64_t>(1, int64_t(std::sqrt(double(budget)))) : budget;
+    // transpose: pieces at most 16 elements wide along f (the source's contiguous dimension),
+    // as tall along s as the budget allows: the destination runs (which a beta != 0 op both reads
+    // and writes) stay long.  cfg 5 'T' 0.726 ms with near-square pieces (32 wide), 0.716 with 16,
+    // 0.728 with 12, 0.758 with 8, 0.754 cut along s first; fp64 / c64 / c128 pack and unpack
+    // lists equal at 16 (profiles/r3b/side/).  Copy: whole columns when one fits, else tall pieces
+    static const int64_t side_env = [] {  // COSTA_TR_SIDE (tuning): the cut's side along f
+        const char* v = std::getenv("COSTA_TR_SIDE");
+        return v ? std::max<int64_t>(1, std::atoll(v)) : int64_t(0);
+    }();
+    const int64_t sq_side = std::max<int64_t>(1, int64_t(std::sqrt(double(budget))));
+    const int64_t side = tr ? (side_env ? side_env : std::min<int64_t>(16, sq_side)) : budget;
     g.nfc = (nf + side - 1) / side;
     const int64_t cf = (nf + g.nfc - 1) / g.nfc;
     const int64_t cs_max = std::max<int64_t>(1, budget / (tr ? (cf | 1) : cf));

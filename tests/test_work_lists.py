@@ -29,7 +29,7 @@ def test_work_lists_cfg5(tmp_path):
     env = {k: v for k, v in os.environ.items()
            if k not in ("COSTA_WAVE_POLICY", "COSTA_TINY_SORT", "COSTA_LARGE_SORT", "COSTA_XCD_BANDS",
                         "COSTA_SKEW_XCD", "COSTA_TINY_LDS", "COSTA_TINY_COPY", "COSTA_MISALIGNED_VEC", "COSTA_SKEW",
-                        "COSTA_MERGE")}
+                        "COSTA_MERGE", "COSTA_TR_SIDE")}
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300,
                        env=dict(env, COSTA_MERGE="0"))
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
