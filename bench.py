@@ -40,6 +40,7 @@ import argparse
 import json
 import math
 import os
+import re
 import sys
 import time
 
@@ -47,6 +48,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+METRIC = "GB/s device-resident tile pack+transpose+unpack (fp64), % HBM peak"
 
 
 def grid_for(n: int):
@@ -87,21 +89,95 @@ def launch_decision(gpus: int, env, argv, port=None):
     return "spawn", cmd
 
 
-def run_ranks(cmd) -> int:
+RUN_BUDGET_S = 540.0  # wall-clock budget of an N-rank child (below the driver's own limit)
+_PHASE = re.compile(r"^\[bench rank (\d+)\] phase: (.*)$")
+
+
+def run_ranks(cmd, budget_s: float = RUN_BUDGET_S, n_gpus: int = 0) -> int:
     """Run the N-rank child and relay its output: JSON lines (rank 0's result) to stdout,
-    everything else to stderr, as it arrives.  Returns the child's exit code."""
+    everything else to stderr, as it arrives.  Returns the child's exit code.
+    The child runs in its own process group under a wall-clock budget: if it has not finished by
+    then (a rank stuck in an RCCL call, say), the whole group is killed (SIGTERM, SIGKILL 10 s
+    later), one JSON line with "error": "timeout", n_gpus and the last phase each rank reported
+    is printed, and 124 is returned."""
+    import signal
     import subprocess
+    import threading
     env = dict(os.environ)
     env.setdefault("OMP_NUM_THREADS", "1")
+    # the ranks' own watchdog fires first, so that rank 0's error line names its phase
+    env.setdefault("COSTA_BENCH_RANK_BUDGET_S", str(max(1.0, budget_s - 30.0)))
     p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
-                         env=env, bufsize=1)
-    for line in p.stdout:
-        if line.startswith("{"):
-            sys.stdout.write(line)
-            sys.stdout.flush()
-        else:
-            sys.stderr.write(line)
-    return p.wait()
+                         env=env, bufsize=1, start_new_session=True)
+    last = {}
+
+    def relay():
+        for line in p.stdout:
+            if line.startswith("{"):
+                sys.stdout.write(line)
+                sys.stdout.flush()
+            else:
+                m = _PHASE.match(line.rstrip("\n"))
+                if m:
+                    last[int(m.group(1))] = m.group(2)
+                sys.stderr.write(line)
+                sys.stderr.flush()
+
+    t = threading.Thread(target=relay, daemon=True)
+    t.start()
+    try:
+        rc = p.wait(timeout=budget_s)
+    except subprocess.TimeoutExpired:
+        for sig, grace in ((signal.SIGTERM, 10.0), (signal.SIGKILL, 5.0)):
+            try:
+                os.killpg(p.pid, sig)
+            except ProcessLookupError:
+                break
+            try:
+                p.wait(timeout=grace)
+                break
+            except subprocess.TimeoutExpired:
+                continue
+        t.join(timeout=5.0)
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": n_gpus,
+                          "error": "timeout", "budget_s": budget_s,
+                          "last_phase": {str(k): v for k, v in sorted(last.items())}}),
+              flush=True)
+        return 124
+    t.join(timeout=5.0)
+    return rc
+
+
+_last_phase = ["start"]
+
+
+def phase(rank: int, msg: str):
+    """progress line of one rank (stderr), parsed by run_ranks and kept for the watchdog"""
+    _last_phase[0] = msg
+    print(f"[bench rank {rank}] phase: {msg}", file=sys.stderr, flush=True)
+
+
+def start_watchdog(rank: int, world: int, budget_s: float):
+    """A rank of an N-rank run (started by run_ranks or by an outside launcher) that is still
+    running after budget_s seconds (a hang inside an RCCL call, say) reports its last phase and
+    exits with 124; rank 0 first prints the error JSON line.  The launcher then tears down the
+    other ranks.  A daemon timer thread: ctypes calls release the GIL, so it fires while the main
+    thread waits inside the library."""
+    import threading
+
+    def fire():
+        msg = f"watchdog: {budget_s:.0f} s budget exceeded in phase '{_last_phase[0]}'"
+        print(f"[bench rank {rank}] {msg}", file=sys.stderr, flush=True)
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world,
+                              "error": "timeout", "budget_s": budget_s,
+                              "last_phase": {"0": _last_phase[0]}}), flush=True)
+        os._exit(124)
+
+    t = threading.Timer(budget_s, fire)
+    t.daemon = True
+    t.start()
+    return t
 
 
 # ------------------------------------------------------------------ synthetic data
@@ -335,6 +411,34 @@ def cpu_baseline_reference(n=16384, b=256, target_s=10.0):
     return out
 
 
+def copy_ceiling(src, dst, col_bytes: int, reps: int = 20):
+    """SURVEY §8(d)'s measured ceiling: what plain device copies of the headline's bytes reach on
+    this box, in this process, after the timed region (src -> dst, both device buffers of the
+    workload; dst is overwritten).  costa_amd/lib/libcosta_ceiling.so (costa_amd/csrc/
+    ceiling.hip): kind 0 hipMemcpyDtoD, kind 1 the strided nt copy of 1 KiB column segments
+    (16 columns per 256-thread workgroup, DESIGN §3a's fastest copy of these bytes), kind 2 a flat
+    nt copy of 16 KiB chunks.  Median of `reps` HIP-event-timed repetitions each; bytes counted
+    like the transform's (read + write)."""
+    import ctypes as C
+    import statistics
+    lib = C.CDLL(os.path.join(ROOT, "costa_amd", "lib", "libcosta_ceiling.so"))
+    f = lib.costa_ceiling_copy_ms
+    f.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_int,
+                  C.POINTER(C.c_float)]
+    nbytes = src.numel() * src.element_size()
+    out = {}
+    for kind, name in ((0, "hipMemcpyDtoD"), (1, "strided_nt_1KiB_segments"), (2, "flat_nt_16KiB")):
+        ms = (C.c_float * reps)()
+        rc = f(kind, src.data_ptr(), dst.data_ptr(), nbytes, col_bytes, reps, ms)
+        if rc != 0:
+            out[name] = {"error": rc}
+            continue
+        med = statistics.median(list(ms))
+        out[name] = {"ms": round(med, 4), "GBps": round(2 * nbytes / (med * 1e-3) / 1e9, 1),
+                     "min_ms": round(min(ms), 4), "reps": reps}
+    return out
+
+
 def cfg5_workload(costa, torch, rank, world, op):
     """BASELINE configs[4]: fp32 16384^2 custom_layout; A tile edges uniform in
     [8, 96] (seeds 0xC5A1 rows / 0xC5A2 cols), C edges uniform in [16, 160] (0xC5A3 / 0xC5A4),
@@ -465,7 +569,8 @@ def main():
         if have < args.gpus:
             print(f"bench.py: --gpus {args.gpus} but {have} GPU(s) visible", file=sys.stderr)
             raise SystemExit(2)
-        raise SystemExit(run_ranks(cmd))
+        budget = float(os.environ.get("COSTA_BENCH_BUDGET_S", RUN_BUDGET_S))
+        raise SystemExit(run_ranks(cmd, budget, args.gpus))
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -485,6 +590,9 @@ def main():
     device = local_rank
     torch.cuda.set_device(device)
     if world > 1:
+        start_watchdog(rank, world, float(os.environ.get("COSTA_BENCH_RANK_BUDGET_S",
+                                                         RUN_BUDGET_S - 30.0)))
+        phase(rank, "init_process_group (gloo control plane)")
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
     def barrier():
@@ -504,7 +612,10 @@ def main():
         if rank == 0:
             uid = torch.frombuffer(bytearray(costa.Comm.unique_id()), dtype=torch.uint8).clone()
         dist.broadcast(uid, 0)
+        phase(rank, f"ncclCommInitRank (RCCL {costa.rccl_version()}, {world} ranks, device {device})")
+        t0 = time.perf_counter()
         comm = costa.Comm.create(bytes(uid.numpy().tobytes()), world, rank, device)
+        phase(rank, f"communicator ready: ncclCommInitRank took {(time.perf_counter() - t0) * 1e3:.1f} ms")
     else:
         comm = costa.Comm.self(device)
 
@@ -669,8 +780,12 @@ def main():
             verified.append(w["check"]())  # before any further call changes C
         planning = {"planner": "device" if st0["device_plans"] else "host",
                     "plan_ms": round(max_over_ranks(st0["plan_ms"]), 2)}
-        if planning_modes:  # warm plan-cache misses with each planner
-            for mode, key in ((1, "default"), (0, "host"), (2, "device")):
+        if planning_modes:
+            # plan-cache misses with each planner.  The first GPU plan of a process loads the
+            # planner's kernels (rocPRIM sort + scan, ~15 ms with the device allocations):
+            # "device_cold" is that first one, "device" the next miss on the same layouts (warm),
+            # the figure DESIGN §2b tabulates
+            for mode, key in ((1, "default"), (0, "host"), (2, "device_cold"), (2, "device")):
                 costa.set_planner(mode)
                 costa.release_caches()
                 t0 = time.perf_counter()
@@ -735,7 +850,9 @@ def main():
                 out[k] = w[k]
         return out
 
+    phase(rank, f"build workload {args.workload}")
     wmain = build(args.workload)
+    phase(rank, f"measure workload {args.workload} (first call, warmup, {args.steps} timed steps)")
     torch.cuda.synchronize()
     res = measure(wmain, args.steps, args.warmup, planning_modes=world == 1)
     el, el_block, el_ev, st = res["el"], res["el_block"], res["el_ev"], res["st"]
@@ -764,6 +881,23 @@ def main():
                        f"tiny_kernel<float> ({name} list: every op is below the large shape)"),
             "bytes_per_launch": int(per_launch),
             "avg_launch_ms": round(avg_ms, 4)}
+
+    roof["events_pass_ms_per_step"] = round(el_ev / args.steps * 1e3, 4)
+    roof["avg_launch_ms_note"] = (
+        "avg_launch_ms comes from the events pass (events_pass_ms_per_step, the same K steps "
+        "with a HIP event pair around every phase); ms_per_step / value from the events-off pass")
+    # the copy ceiling of the same bytes on this box, measured after the timed
+    # region (it overwrites C, whose checks have run)
+    if world == 1 and args.workload == "pxtran":
+        torch.cuda.synchronize()
+        cc = copy_ceiling(A, Cm, col_bytes=(M // pm) * 8)
+        best = max((v.get("GBps", 0.0) for v in cc.values()), default=0.0)
+        cc["best_GBps"] = best
+        cc["note"] = ("plain copies of the headline's A into C (2 GiB read + 2 GiB written), "
+                      "median of 20 event-timed repetitions each, measured in this process "
+                      "after the timed region")
+        roof["copy_ceiling"] = cc
+        roof["frac_of_ceiling"] = round(achieved / best, 4) if best > 0 else None
 
     # end-to-end from host memory (H2D + kernels + D2H), reported, never `value`
     e2e = None
@@ -837,7 +971,9 @@ def main():
         for kind, edge in plan_x:
             costa.release_caches()
             torch.cuda.empty_cache()
+            phase(rank, f"extra config {kind}:{edge}: build")
             wx = build(kind, edge)
+            phase(rank, f"extra config {kind}:{edge}: measure")
             ksteps = max(1, min(args.steps, 5 if kind != "cfg5" else 10))
             rx = measure(wx, ksteps, 1)
             key = kind if kind not in extra else f"{kind}_{edge}"
@@ -846,6 +982,7 @@ def main():
             costa.release_caches()
             torch.cuda.empty_cache()
 
+    phase(rank, "report")
     cpu = None
     if want_cpu:
         port = cpu_baseline(n=n, b=b)  # our restatement of the tile loop (oracle/), same tiles
@@ -864,7 +1001,7 @@ def main():
         if args.workload in ("pxtran", "cfg3", "cfg4"):
             cfg.update({"m": M, "n": N, "block": wmain.get("block", b), "grid": f"{pm}x{pn}"})
         line = {
-            "metric": "GB/s device-resident tile pack+transpose+unpack (fp64), % HBM peak",
+            "metric": METRIC,
             "value": round(value, 2),
             "unit": "GB/s",
             "pct_hbm_peak": round(100 * value / (HBM_PEAK_GBPS * world), 2),

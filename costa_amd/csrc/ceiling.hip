@@ -1,0 +1,104 @@
+// Measurement support for bench.py (not part of the transform path): what a plain device copy
+// of the headline workload's bytes reaches on THIS box, so that the tile kernel's roofline
+// fraction can be read against a ceiling the same run measured ("also report a
+// measured hipMemcpyDtoD ceiling").  Built as its own library, libcosta_ceiling.so; the product
+// library does not link it.
+//
+//   kind 0  hipMemcpyDtoD of `bytes` (one call)
+//   kind 1  strided column-segment copy: the source and destination are column-major matrices of
+//           `col_bytes`-byte columns; a 256-thread workgroup copies 16 KiB as 16 segments of
+//           1 KiB (one per column), consecutive workgroups continue down the same 16 columns,
+//           nontemporal 16-byte loads and stores.  This is the fastest copy of cfg 2's bytes
+//           measured on MI355X (tools/copy_ceiling.hip "seg 1024 nt/nt").
+//   kind 2  flat copy, one 16 KiB chunk per 256-thread workgroup, nontemporal loads and stores
+//
+// costa_ceiling_copy_ms runs `reps` timed repetitions (HIP events on its own stream) after one
+// untimed one and writes every repetition's milliseconds to ms_out[0..reps).  Returns 0, or a
+// negative code: -1 bad arguments, -2 a HIP error.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kThreads = 256;
+constexpr int kSegBytes = 1024;
+constexpr int kSegs = 16;  // 16 KiB per workgroup
+constexpr int kLanesPerSeg = kSegBytes / 16;
+
+__global__ __launch_bounds__(kThreads) void seg_copy(const u32x4* __restrict__ a,
+                                                     u32x4* __restrict__ c, long col16,
+                                                     long segs_per_col) {
+    const long w = blockIdx.x;
+    const long g = w / segs_per_col, q = w % segs_per_col;
+    const long base = g * kSegs * col16 + q * kLanesPerSeg;
+    u32x4 x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int e = u * kThreads + int(threadIdx.x);
+        x[u] = __builtin_nontemporal_load(a + base + (e / kLanesPerSeg) * col16 + e % kLanesPerSeg);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int e = u * kThreads + int(threadIdx.x);
+        __builtin_nontemporal_store(x[u], c + base + (e / kLanesPerSeg) * col16 + e % kLanesPerSeg);
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void flat_copy(const u32x4* __restrict__ a,
+                                                      u32x4* __restrict__ c) {
+    const long base = long(blockIdx.x) * 4 * kThreads;
+    u32x4 x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        x[u] = __builtin_nontemporal_load(a + base + u * kThreads + threadIdx.x);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        __builtin_nontemporal_store(x[u], c + base + u * kThreads + threadIdx.x);
+}
+
+}  // namespace
+
+extern "C" int costa_ceiling_copy_ms(int kind, const void* src, void* dst, uint64_t bytes,
+                                     uint64_t col_bytes, int reps, float* ms_out) {
+    if (!src || !dst || !ms_out || reps <= 0 || bytes == 0 || bytes % (kSegs * kSegBytes))
+        return -1;
+    const long grid = long(bytes / (kSegs * kSegBytes));
+    if (kind == 1) {
+        // whole 16-column groups of whole 1 KiB segments only: no tail handling needed
+        if (col_bytes == 0 || col_bytes % kSegBytes || bytes % (kSegs * col_bytes)) return -1;
+    } else if (kind != 0 && kind != 2) {
+        return -1;
+    }
+    if (grid > 0x7fffffffL) return -1;
+    hipStream_t s;
+    hipEvent_t e0, e1;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return -2;
+    if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return -2;
+    const u32x4* a = static_cast<const u32x4*>(src);
+    u32x4* c = static_cast<u32x4*>(dst);
+    const long col16 = long(col_bytes / 16), spc = long(col_bytes / kSegBytes);
+    auto once = [&]() -> hipError_t {
+        if (kind == 0) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s);
+        if (kind == 1)
+            hipLaunchKernelGGL(seg_copy, dim3(unsigned(grid)), dim3(kThreads), 0, s, a, c, col16, spc);
+        else
+            hipLaunchKernelGGL(flat_copy, dim3(unsigned(grid)), dim3(kThreads), 0, s, a, c);
+        return hipGetLastError();
+    };
+    int rc = 0;
+    if (once() != hipSuccess) rc = -2;
+    for (int r = 0; r < reps && rc == 0; ++r) {
+        if (hipEventRecord(e0, s) != hipSuccess || once() != hipSuccess ||
+            hipEventRecord(e1, s) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+            hipEventElapsedTime(&ms_out[r], e0, e1) != hipSuccess)
+            rc = -2;
+    }
+    if (hipStreamSynchronize(s) != hipSuccess) rc = -2;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipStreamDestroy(s);
+    return rc;
+}

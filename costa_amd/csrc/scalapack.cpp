@@ -79,14 +79,16 @@ grid_info grid_of(int ctxt) {
 
 // The processes of `ctxt`'s grid as one communicator, rank k = grid cell k (row-major); made
 // once per process set and kept (its RCCL communicator is cached on it, costa/transform.hpp
-// comm_from_mpi).  BLACS reuses context handles after Cblacs_gridexit, and a reused handle may
-// name a grid of another system communicator with the same process numbers: a cached entry is
-// therefore reused only when its processes are exactly the grid's (MPI_Group_compare, local).
+// comm_from_mpi).  The cache is keyed by the processes themselves -- their MPI_COMM_WORLD ranks
+// in cell order -- not by the context handle: BLACS reuses handles after Cblacs_gridexit
+// (possibly over another system communicator), and handles are local to each process.  Every
+// process of a grid computes the same key, and it holds an entry for it exactly when it took part
+// in the MPI_Comm_create_group that made one, so the members of a grid always agree on reusing
+// or creating (a handle-keyed cache let one member reuse while another created, and hang).
 // The cached communicators (and with them their RCCL communicators) are freed at the start of
 // MPI_Finalize, through an attribute of MPI_COMM_SELF (MPI-3.1 §8.7.1).
 struct comm_cache {
-    std::map<std::pair<int, std::vector<int>>, MPI_Comm> by_key;
-    std::vector<MPI_Comm> all;  // every communicator made, including replaced ones
+    std::map<std::vector<int>, MPI_Comm> by_procs;
 };
 
 comm_cache& cached_comms() {
@@ -96,9 +98,8 @@ comm_cache& cached_comms() {
 
 int free_cached_comms(MPI_Comm, int, void*, void*) {
     comm_cache& c = cached_comms();
-    for (MPI_Comm& x : c.all) MPI_Comm_free(&x);
-    c.all.clear();
-    c.by_key.clear();
+    for (auto& kv : c.by_procs) MPI_Comm_free(&kv.second);
+    c.by_procs.clear();
     return MPI_SUCCESS;
 }
 
@@ -113,31 +114,27 @@ void free_at_finalize() {
 
 MPI_Comm grid_comm(int ctxt, const grid_info& g) {
     comm_cache& cache = cached_comms();
-    auto key = std::make_pair(ctxt, g.pnum);
     MPI_Comm sys = sys_comm(ctxt);
-    MPI_Group all, grp;
+    MPI_Group all, grp, world;
     MPI_Comm_group(sys, &all);
     MPI_Group_incl(all, int(g.pnum.size()), g.pnum.data(), &grp);
     MPI_Group_free(&all);
-    auto it = cache.by_key.find(key);
-    if (it != cache.by_key.end()) {
-        MPI_Group have;
-        int same = MPI_UNEQUAL;
-        MPI_Comm_group(it->second, &have);
-        MPI_Group_compare(have, grp, &same);
-        MPI_Group_free(&have);
-        if (same == MPI_IDENT) {
-            MPI_Group_free(&grp);
-            return it->second;
-        }
+    std::vector<int> cells(g.pnum.size()), procs(g.pnum.size(), MPI_UNDEFINED);
+    for (size_t k = 0; k < cells.size(); ++k) cells[k] = int(k);
+    MPI_Comm_group(MPI_COMM_WORLD, &world);
+    MPI_Group_translate_ranks(grp, int(cells.size()), cells.data(), world, procs.data());
+    MPI_Group_free(&world);
+    auto it = cache.by_procs.find(procs);
+    if (it != cache.by_procs.end()) {
+        MPI_Group_free(&grp);
+        return it->second;
     }
     MPI_Comm out = MPI_COMM_NULL;
     MPI_Comm_create_group(sys, grp, 0x6c0d, &out);
     MPI_Group_free(&grp);
     if (out == MPI_COMM_NULL) throw std::runtime_error("could not make the context's communicator");
     free_at_finalize();
-    cache.by_key[key] = out;
-    cache.all.push_back(out);
+    cache.by_procs.emplace(std::move(procs), out);
     return out;
 }
 

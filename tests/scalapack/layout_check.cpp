@@ -8,6 +8,12 @@
 //      and 2 pass descc[CTXT] = -1 and junk in the other fields), ictxt a 1x4 grid of ranks
 //      {2, 0, 3, 1}: sub-matrices at ia, ja != 1, rank sources != 0.
 //   2. pdtran on a column-major 2x2 grid of ranks {1, 3, 0, 2}.
+//   3. communicator reuse across grids whose BLACS process numbers coincide: pdtran
+//      on a 1x2 grid of world ranks {0, 1}; then on a 1x2 grid over a sub-communicator of
+//      world ranks {0, 2} (the same process numbers {0, 1}, possibly the same handle); then on
+//      {0, 1} again.  Every member of each grid must make the same create-or-reuse choice: a
+//      cache keyed by handle and process numbers had world rank 0 create a communicator while
+//      rank 1 reused one, and the two hung in different collectives.
 // For every block of both layouts: its owner must be the rank, in the call's communicator
 // (= the call context's grid cells, row-major), of the process the BLACS grid puts it on;
 // every process's local blocks must be exactly the blocks it owns, inside its local array.
@@ -27,6 +33,9 @@ extern "C" {
 void Cblacs_pinfo(int*, int*);
 void Cblacs_gridmap(int*, int*, int, int, int);
 void Cblacs_gridexit(int);
+void Cblacs_gridinit(int*, const char*, int, int);
+int Csys2blacs_handle(MPI_Comm);
+void Cfree_blacs_system_handle(int);
 int numroc_(const int*, const int*, const int*, const int*, const int*);
 }
 
@@ -162,6 +171,44 @@ int main(int argc, char** argv) {
         double alpha = 0.5, beta = 0.25;
         const int ia = g_exp[0].ia, ja = g_exp[0].ja, ic = g_exp[1].ia, jc = g_exp[1].ja;
         costa_pdtran(&m, &n, &alpha, abuf.data(), &ia, &ja, desca, &beta, cbuf.data(), &ic, &jc, descc);
+    }
+    {  // 3. grids with equal process numbers over different system communicators
+        MPI_Comm sub = MPI_COMM_NULL;  // world ranks {0, 2}
+        MPI_Comm_split(MPI_COMM_WORLD, (g_me == 0 || g_me == 2) ? 0 : MPI_UNDEFINED, g_me, &sub);
+        const int m = 40, n = 30;
+        for (int round = 0; round < 3; ++round) {
+            const bool via_sub = round == 1;
+            const std::vector<int> w = via_sub ? std::vector<int>{0, 2} : std::vector<int>{0, 1};
+            int ctxt = -1;
+            if (via_sub) {
+                if (sub != MPI_COMM_NULL) {
+                    const int h = Csys2blacs_handle(sub);
+                    ctxt = h;
+                    Cblacs_gridinit(&ctxt, "R", 1, 2);
+                }
+            } else {
+                ctxt = make_grid(w, 1, 2);  // every process calls; those outside get no grid
+                if (g_me != 0 && g_me != 1) ctxt = -1;
+            }
+            g_exp[0] = {n, m, 8, 8, 0, 0, 1, 1, n, m, 1, 2, w, nullptr, 0};
+            g_exp[1] = {m, n, 8, 8, 0, 0, 1, 1, m, n, 1, 2, w, nullptr, 0};
+            desc_for(desca, ctxt, g_exp[0], g_me, abuf);
+            desc_for(descc, ctxt, g_exp[1], g_me, cbuf);
+            g_exp[0].base = desca[1] >= 0 ? abuf.data() : nullptr;
+            g_exp[0].bytes = abuf.size() * sizeof(double);
+            g_exp[1].base = descc[1] >= 0 ? cbuf.data() : nullptr;
+            g_exp[1].bytes = cbuf.size() * sizeof(double);
+            g_call_world = w;
+            double alpha = 1.0, beta = 0.0;
+            const int one = 1;
+            if (ctxt >= 0) {
+                costa_pdtran(&m, &n, &alpha, abuf.data(), &one, &one, desca, &beta, cbuf.data(), &one,
+                             &one, descc);
+                Cblacs_gridexit(ctxt);
+            }
+            MPI_Barrier(MPI_COMM_WORLD);
+        }
+        if (sub != MPI_COMM_NULL) MPI_Comm_free(&sub);
     }
     int total = 0;
     MPI_Allreduce(&g_fail, &total, 1, MPI_INT, MPI_SUM, MPI_COMM_WORLD);

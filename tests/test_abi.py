@@ -89,3 +89,20 @@ int main() {
     r = subprocess.run([str(exe)], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "null communicator" in r.stdout
+
+
+def test_ceiling_library_loads_and_rejects_bad_arguments():
+    """bench.py's copy-ceiling library (costa_amd/csrc/ceiling.hip): loads without a GPU, exports
+    its one entry point, and refuses arguments it cannot run before touching the GPU"""
+    path = os.path.join(ROOT, "costa_amd", "lib", "libcosta_ceiling.so")
+    lib = ctypes.CDLL(path)
+    f = lib.costa_ceiling_copy_ms
+    f.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                  ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]
+    ms = (ctypes.c_float * 4)()
+    p = ctypes.c_void_p(1 << 40)
+    assert f(1, p, p, 1 << 21, 1000, 4, ms) == -1      # column not whole 1 KiB segments
+    assert f(1, p, p, 1 << 21, 1 << 20, 4, ms) == -1   # not whole 16-column groups
+    assert f(2, p, p, 1000, 0, 4, ms) == -1            # not whole 16 KiB chunks
+    assert f(7, p, p, 1 << 21, 0, 4, ms) == -1         # unknown kind
+    assert f(0, p, p, 1 << 21, 0, 0, ms) == -1         # no repetitions

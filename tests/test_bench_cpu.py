@@ -50,6 +50,45 @@ def test_run_ranks_relays_json_and_rc():
     assert "noise" in r.stderr
 
 
+def test_run_ranks_kills_a_hung_child_and_reports():
+    """a child that never finishes (an RCCL hang, say): its process group is killed at the budget,
+    one JSON error line names the last phase each rank reported, rc 124"""
+    code = ("import sys, time, subprocess\n"
+            "print('[bench rank 0] phase: build workload pxtran', file=sys.stderr, flush=True)\n"
+            "print('[bench rank 1] phase: ncclCommInitRank (RCCL 22606)', file=sys.stderr, flush=True)\n"
+            # a grandchild in the same group must die with it
+            "subprocess.Popen([sys.executable, '-c', 'import time; time.sleep(600)'])\n"
+            "time.sleep(600)\n")
+    t0 = __import__("time").time()
+    r = subprocess.run([sys.executable, "-c",
+                        f"import bench; raise SystemExit(bench.run_ranks([{sys.executable!r}, '-c', "
+                        f"{code!r}], budget_s=3.0, n_gpus=2))"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=60)
+    assert __import__("time").time() - t0 < 40
+    assert r.returncode == 124, r.stderr
+    import json
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["error"] == "timeout" and line["n_gpus"] == 2 and line["value"] is None
+    assert line["last_phase"] == {"0": "build workload pxtran",
+                                  "1": "ncclCommInitRank (RCCL 22606)"}
+
+
+def test_rank_watchdog_reports_phase_and_exits():
+    """the in-rank watchdog (for ranks an outside launcher started): rank 0 prints the error line
+    with its last phase and the process exits 124 while the main thread is blocked"""
+    code = ("import bench, time\n"
+            "bench.phase(0, 'exchange')\n"
+            "bench.start_watchdog(0, 2, 1.0)\n"
+            "time.sleep(60)\n")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 124
+    import json
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["error"] == "timeout" and line["last_phase"] == {"0": "exchange"}
+    assert "budget exceeded in phase 'exchange'" in r.stderr
+
+
 def test_gpus_n_without_gpus_exits_nonzero():
     """no GPU here: the parent counts devices (no GPU initialisation) and refuses"""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}

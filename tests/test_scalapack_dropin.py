@@ -111,7 +111,10 @@ def test_shim_process_mapping_4_ranks(tmp_path):
     """p?gemr2d between a 2x2 grid and a 1x2 grid of two of the ranks (the other two pass
     desc[CTXT] = -1), ictxt a permuted 1x4 grid; p?tran on a permuted column-major grid: every
     block's owner is the communicator rank of the process BLACS puts it on, and every process's
-    local blocks are exactly the ones it owns (no GPU: the transform is replaced by the check)."""
+    local blocks are exactly the ones it owns (no GPU: the transform is replaced by the check).
+    Case 3 reuses BLACS process numbers over another system communicator between two calls of
+    the same process pair: with a communicator cache keyed by context handle the two processes
+    chose differently (create / reuse) and hung; the 120 s limit catches that."""
     exe = tmp_path / "layout_check"
     mkl = [f"{CONDA}/lib/lib{x[2:]}.so" for x in MKL]
     subprocess.run(["g++", "-std=c++17", "-O1", "-DCOSTA_PREFIXED", f"-I{ROOT}/include",
@@ -121,7 +124,7 @@ def test_shim_process_mapping_4_ranks(tmp_path):
                    check=True, timeout=300)
     env = dict(os.environ, PATH=f"{CONDA}/bin:" + os.environ["PATH"])
     r = subprocess.run([shutil.which("mpiexec", path=env["PATH"]) or f"{CONDA}/bin/mpiexec",
-                        "-n", "4", str(exe)], capture_output=True, text=True, env=env, timeout=300)
+                        "-n", "4", str(exe)], capture_output=True, text=True, env=env, timeout=120)
     assert r.returncode == 0 and "ALL PASSED" in r.stdout, r.stdout + r.stderr
 
 
