@@ -209,6 +209,14 @@ comm* comm_create(const unsigned char* id, int nranks, int rank, int device) {
     return c;
 }
 
+const char* tuning_env(const char* name) {
+    static const bool on = [] {
+        const char* s = std::getenv("COSTA_TUNING");
+        return s && std::atoi(s) == 1;
+    }();
+    return on ? std::getenv(name) : nullptr;
+}
+
 int loopback_exchange() {
     static const int mode = [] {
         const char* s = std::getenv("COSTA_LOOPBACK");
@@ -334,7 +342,7 @@ bool any_axpby(const std::vector<costa_tile_op_t>& ops) {
 // (COSTA_TINY_COPY: another budget in bytes up to kTinyCopyBytes, tuning runs only)
 int64_t tiny_copy_budget(int64_t E, bool local) {
     static const int64_t env = [] {
-        const char* s = std::getenv("COSTA_TINY_COPY");
+        const char* s = tuning_env("COSTA_TINY_COPY");
         const int64_t v = s ? std::atoll(s) : 0;
         return v >= 256 && v <= kTinyCopyBytes ? v : int64_t(0);
     }();
@@ -345,7 +353,7 @@ int64_t tiny_copy_budget(int64_t E, bool local) {
 // (COSTA_TINY_LDS: another budget up to kTinyLdsBytes, tuning runs only)
 int64_t tiny_lds_budget() {
     static const int64_t b = [] {
-        const char* s = std::getenv("COSTA_TINY_LDS");
+        const char* s = tuning_env("COSTA_TINY_LDS");
         const int64_t v = s ? std::atoll(s) : 0;
         return v >= 256 && v <= kTinyLdsBytes ? v : int64_t(kTinyLdsDefault);
     }();
@@ -382,7 +390,7 @@ wave_grid wave_pieces(const costa_tile_op_t& op, int64_t E, bool local) {
     // 0.728 with 12, 0.758 with 8, 0.754 cut along s first; fp64 / c64 / c128 pack and unpack
     // lists equal at 16 (profiles/r3b/side/).  Copy: whole columns when one fits, else tall pieces
     static const int64_t side_env = [] {  // COSTA_TR_SIDE (tuning): the cut's side along f
-        const char* v = std::getenv("COSTA_TR_SIDE");
+        const char* v = tuning_env("COSTA_TR_SIDE");
         return v ? std::max<int64_t>(1, std::atoll(v)) : int64_t(0);
     }();
     const int64_t sq_side = std::max<int64_t>(1, int64_t(std::sqrt(double(budget))));
@@ -521,7 +529,7 @@ void xcd_bands(const std::vector<const costa_tile_op_t*>& ops, int64_t E, int k,
 // stride further for copies, ns elements further for transposes), with the same extent along f,
 // strides and flags (16-byte alignment flags aside: the merged op keeps a's, which describe its
 // start and strides), joins a (then the same along f).  Same elements, same transform: only the
-// op boundaries move.  Order hint: the smaller one.  `root` (optional): for every input op, the
+// op boundaries move.  Order hint: a's (the tile the merged op starts at).  `root` (optional): for every input op, the
 // input op it ended up merged into (itself when it survives).
 void merge_adjacent(std::vector<costa_tile_op_t>& v, int64_t E, std::vector<uint32_t>* root = nullptr) {
     std::vector<uint32_t> id(v.size());  // input index of each op of v
@@ -557,7 +565,7 @@ void merge_adjacent(std::vector<costa_tile_op_t>& v, int64_t E, std::vector<uint
                 const int64_t total = n + (pass == 0 ? b.ns : b.nf);
                 if (!same || total > (int64_t(1) << 30)) break;
                 (pass == 0 ? a.ns : a.nf) = int32_t(total);
-                a.order = std::min(a.order ? a.order : b.order, b.order ? b.order : a.order);
+                if (!a.order) a.order = b.order;  // the merged op keeps the hint of its first tile
                 gone[it->second] = 1;
                 if (root) (*root)[id[it->second]] = id[i];
             }
@@ -702,14 +710,14 @@ constexpr int64_t kSkewWideGroup = 8;
 const wave_knobs& knobs() {
     static wave_knobs k = [] {
         wave_knobs x;
-        if (const char* s = std::getenv("COSTA_WAVE_POLICY")) x.policy = std::atoi(s) == 1 ? 1 : 2;
-        if (const char* s = std::getenv("COSTA_TINY_SORT")) x.sort = std::atoi(s);
-        if (const char* s = std::getenv("COSTA_LARGE_SORT")) x.large_sort = std::atoi(s);
-        if (const char* s = std::getenv("COSTA_SKEW_XCD")) x.skew_xcd = std::max(-1, std::atoi(s));
-        if (const char* s = std::getenv("COSTA_BAND_H")) x.band_h = std::max(1, std::atoi(s));
-        if (const char* s = std::getenv("COSTA_XCD_BANDS")) x.xcd_bands = std::atoi(s);
-        if (const char* s = std::getenv("COSTA_MERGE")) x.merge = std::atoi(s);
-        if (const char* s = std::getenv("COSTA_FORCE_SQ")) x.force_sq = std::atoi(s);
+        if (const char* s = tuning_env("COSTA_WAVE_POLICY")) x.policy = std::atoi(s) == 1 ? 1 : 2;
+        if (const char* s = tuning_env("COSTA_TINY_SORT")) x.sort = std::atoi(s);
+        if (const char* s = tuning_env("COSTA_LARGE_SORT")) x.large_sort = std::atoi(s);
+        if (const char* s = tuning_env("COSTA_SKEW_XCD")) x.skew_xcd = std::max(-1, std::atoi(s));
+        if (const char* s = tuning_env("COSTA_BAND_H")) x.band_h = std::max(1, std::atoi(s));
+        if (const char* s = tuning_env("COSTA_XCD_BANDS")) x.xcd_bands = std::atoi(s);
+        if (const char* s = tuning_env("COSTA_MERGE")) x.merge = std::atoi(s);
+        if (const char* s = tuning_env("COSTA_FORCE_SQ")) x.force_sq = std::atoi(s);
         return x;
     }();
     return k;
@@ -726,7 +734,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     // misaligned 16-byte stores lost for both (tools/unaligned_mis.sh, profiles/r3/).
     // COSTA_MISALIGNED_VEC (tuning): bit 0 destinations, bit 1 sources, for every element size.
     static const int mis_env = [] {
-        const char* s = std::getenv("COSTA_MISALIGNED_VEC");
+        const char* s = tuning_env("COSTA_MISALIGNED_VEC");
         return s ? std::atoi(s) : -1;
     }();
     // (by default only for ops of at least one large sub-tile: smaller ones keep their class)
@@ -858,7 +866,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     // element is written once: ops that read C (beta != 0) go there too.
     const int64_t k_elems = int64_t(sh.bf_k) * sh.bs_k;
     static const bool skew_on = [] {  // COSTA_SKEW=0: off (tuning)
-        const char* s = std::getenv("COSTA_SKEW");
+        const char* s = tuning_env("COSTA_SKEW");
         return !s || std::atoi(s) != 0;
     }();
     for (size_t li = 0; skew_on && k_elems > 0 && li < ops.size(); ++li) {

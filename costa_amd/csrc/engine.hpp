@@ -111,6 +111,13 @@ void set_planner_mode(int mode);
 // a single GPU (two ranks cannot share one GPU under RCCL).  0 = off.
 int loopback_exchange();
 
+// A tuning override `name` from the environment, or nullptr.  Tuning overrides (work-list orders,
+// wavefront budgets, shape choices, host-staging slots and threads) are read only when
+// COSTA_TUNING=1: a user's environment cannot select shapes and orders that the GPU tests never
+// run.  Behaviour switches (COSTA_LOOPBACK, COSTA_MAX_MSG_BYTES, COSTA_EXCHANGE_ROUNDS,
+// COSTA_PLANNER, COSTA_HOST_STAGING) and the trace switches are read as documented.
+const char* tuning_env(const char* name);
+
 // largest single ncclSend/ncclRecv of the exchange (COSTA_MAX_MSG_BYTES, default 256 MiB)
 size_t max_message_bytes();
 

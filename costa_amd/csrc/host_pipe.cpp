@@ -61,9 +61,9 @@ namespace engine {
 
 namespace {
 
-// source (and target) bytes per group; COSTA_HOST_SLOT_MIB overrides (tuning)
+// source (and target) bytes per group; COSTA_HOST_SLOT_MIB overrides (tuning, COSTA_TUNING=1)
 const size_t kSlot = [] {
-    const char* s = std::getenv("COSTA_HOST_SLOT_MIB");
+    const char* s = tuning_env("COSTA_HOST_SLOT_MIB");
     const long v = s ? std::atol(s) : 64;
     return size_t(std::max(1L, std::min(1024L, v))) << 20;
 }();
@@ -169,7 +169,7 @@ class pool {
 };
 
 int host_threads() {
-    if (const char* s = std::getenv("COSTA_HOST_THREADS")) return std::max(1, std::atoi(s));
+    if (const char* s = tuning_env("COSTA_HOST_THREADS")) return std::max(1, std::atoi(s));
     const int hw = int(std::thread::hardware_concurrency());
     return std::max(1, std::min(16, hw));
 }

@@ -26,6 +26,7 @@ def test_loopback_exchange_matches_golden(mode, slot, planner):
     env = dict(os.environ, COSTA_LOOPBACK=mode)
     if slot:
         env["COSTA_HOST_SLOT_MIB"] = slot
+        env["COSTA_TUNING"] = "1"  # the slot size is a tuning override
     if planner:
         env["COSTA_PLANNER"] = planner
     r = subprocess.run([sys.executable, child], env=env, capture_output=True, text=True,

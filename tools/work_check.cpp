@@ -18,6 +18,7 @@
 //   `work_check merge` checks the merging itself.
 // Prints "ok" and exits 0, or prints the first violation and exits 1.
 #include <chrono>
+#include <complex>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -135,8 +136,10 @@ static bool check_list(const std::string& name, costa_dtype_t dt, const std::vec
         CHECK(parent.count(s.order) && shaped.count(s.order), "shaped op %lld has no shaped parent", (long long)i);
         costa_tile_op_t q = *parent[s.order];
         if (E == 4 && int64_t(q.nf) * q.ns >= big_elems(dt, ops) && q.src % 4 == 0) q.flags |= COSTA_TILE_VEC_SRC;
+        // an op merged from tiles that continue each other (merge_small / merge_adjacent, copy or
+        // transpose mode) starts at the tile whose hint it keeps
         const bool merged = s.src == q.src && s.dst == q.dst && s.flags == q.flags && s.lds == q.lds &&
-                            s.ldd == q.ldd && s.nf >= q.nf && s.ns >= q.ns && (s.flags & COSTA_TILE_TRANSPOSE);
+                            s.ldd == q.ldd && s.nf >= q.nf && s.ns >= q.ns;
         CHECK(std::memcmp(&s, &q, sizeof(s)) == 0 || merged, "shaped op %lld", (long long)i);
         restarts += i > 0 && ord[size_t(i) - 1].order > s.order;
         CHECK(restarts <= 2, "shaped op %lld out of hint order", (long long)i);
@@ -239,7 +242,75 @@ static bool check_merge() {
     return true;
 }
 
+// FNV-1a over the work lists of a set of geometries (cfg 5 'N' / 'T', cfg 2's 256^2 fp64 'T',
+// cfg 4's 128^2 c128 'T' with alpha / beta, 24^2 fp32 blocks that merge, fp32 with lld 4097):
+// `work_check digest` prints it, so that tests/test_work_lists.py can compare builds of the
+// library under different environments
+static uint64_t fnv(uint64_t h, const void* p, size_t n) {
+    const unsigned char* b = static_cast<const unsigned char*>(p);
+    for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 0x100000001b3ull;
+    return h;
+}
+static uint64_t digest_of(uint64_t h, const plan& p) {
+    for (int kind = 0; kind < 3; ++kind) {
+        const auto& ops = kind == 0 ? p.local_ops : kind == 1 ? p.pack_ops : p.unpack_ops;
+        std::vector<costa_tile_op_t> ord;
+        std::vector<uint64_t> work;
+        const work_split w = build_work(p.dtype, ops, ord, work, kind == 0 ? list_local : kind == 1 ? list_pack : list_unpack);
+        h = fnv(h, ord.data(), ord.size() * sizeof(costa_tile_op_t));
+        h = fnv(h, work.data(), work.size() * sizeof(uint64_t));
+        h = fnv(h, &w, sizeof(w));
+    }
+    return h;
+}
+static int digest() {
+    uint64_t h = 0xcbf29ce484222325ull;
+    const int n = 16384;
+    auto LA = layout(splits(0xC5A1, 8, 96, n), splits(0xC5A2, 8, 96, n), uint64_t(1) << 40);
+    auto LC = layout(splits(0xC5A3, 16, 160, n), splits(0xC5A4, 16, 160, n), uint64_t(1) << 41);
+    elayout a = erase(LA), c = erase(LC);
+    for (char op : {'N', 'T'}) h = digest_of(h, *plan_of(a, c, op, op == 'N' ? 1.f : -0.5f, op == 'N' ? 0.f : 2.f));
+    {
+        auto A = block_cyclic_layout<double>(n, n, 256, 256, 1, 1, n, n, 1, 1, 'R', 0, 0,
+                                             reinterpret_cast<double*>(uint64_t(1) << 40), n, 'C', 0);
+        auto C = block_cyclic_layout<double>(n, n, 256, 256, 1, 1, n, n, 1, 1, 'R', 0, 0,
+                                             reinterpret_cast<double*>(uint64_t(1) << 41), n, 'C', 0);
+        elayout ea = erase(A), ec = erase(C);
+        job j{&ea, &ec, 'T', {}};
+        const double one = 1.0, zero = 0.0;
+        std::memcpy(j.s.alpha.data(), &one, 8);
+        std::memcpy(j.s.beta.data(), &zero, 8);
+        h = digest_of(h, *make_plan({j}, 0, 1));
+    }
+    {
+        using z = std::complex<double>;
+        const int m = 8192;
+        auto A = block_cyclic_layout<z>(m, m, 128, 128, 1, 1, m, m, 1, 1, 'R', 0, 0,
+                                        reinterpret_cast<z*>(uint64_t(1) << 40), m, 'C', 0);
+        auto C = block_cyclic_layout<z>(m, m, 128, 128, 1, 1, m, m, 1, 1, 'R', 0, 0,
+                                        reinterpret_cast<z*>(uint64_t(1) << 41), m, 'C', 0);
+        elayout ea = erase(A), ec = erase(C);
+        job j{&ea, &ec, 'T', {}};
+        const z al(0.75, -0.5), be(1.25, 0.25);
+        std::memcpy(j.s.alpha.data(), &al, 16);
+        std::memcpy(j.s.beta.data(), &be, 16);
+        h = digest_of(h, *make_plan({j}, 0, 1));
+    }
+    for (int lld : {4096, 4097}) {
+        const int m = 4096, nb = lld == m ? 24 : 256;
+        auto A = block_cyclic_layout<float>(m, m, nb, nb, 1, 1, m, m, 1, 1, 'R', 0, 0,
+                                            reinterpret_cast<float*>(uint64_t(1) << 40), lld, 'C', 0);
+        auto C = block_cyclic_layout<float>(m, m, nb, nb, 1, 1, m, m, 1, 1, 'R', 0, 0,
+                                            reinterpret_cast<float*>(uint64_t(1) << 41), lld, 'C', 0);
+        elayout ea = erase(A), ec = erase(C);
+        for (char op : {'T', 'N'}) h = digest_of(h, *plan_of(ea, ec, op, 1.f, 0.f));
+    }
+    std::printf("digest %016llx\n", (unsigned long long)h);
+    return 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc > 1 && std::string(argv[1]) == "digest") return digest();
     if (argc > 1 && std::string(argv[1]) == "time") {  // build_work on cfg 5's 'N' list (host cost)
         const int n = 16384;
         auto LA = layout(splits(0xC5A1, 8, 96, n), splits(0xC5A2, 8, 96, n), uint64_t(1) << 40);
