@@ -184,14 +184,19 @@ struct __attribute__((aligned(16))) raw16 {
 #define COSTA_NT_STORES 1
 #endif
 typedef uint32_t u32x4a __attribute__((ext_vector_type(4)));
+// 16-byte loads need only dword alignment on gfx950 (global_load_dwordx4): sources of 4-byte
+// elements off the 16-byte grid are read this way too (engine.cpp build_work marks them
+// COSTA_TILE_VEC_SRC), so the load goes through a type that promises 4-byte alignment only
+typedef uint32_t u32x4d __attribute__((ext_vector_type(4), aligned(4)));
 
 __device__ __forceinline__ raw16 ld16(const void* p) {
     raw16 r;
 #if COSTA_NT_LOADS
-    const u32x4a v = __builtin_nontemporal_load(reinterpret_cast<const u32x4a*>(p));
+    const u32x4d v = __builtin_nontemporal_load(reinterpret_cast<const u32x4d*>(p));
     __builtin_memcpy(&r, &v, 16);
 #else
-    r = *reinterpret_cast<const raw16*>(p);
+    const u32x4d v = *reinterpret_cast<const u32x4d*>(p);
+    __builtin_memcpy(&r, &v, 16);
 #endif
     return r;
 }

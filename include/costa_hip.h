@@ -82,7 +82,10 @@ typedef struct {
  * launch's base pointers (absolute addresses when the base is NULL). */
 #define COSTA_TILE_TRANSPOSE 0x1u
 #define COSTA_TILE_CONJ 0x2u
-#define COSTA_TILE_VEC_SRC 0x4u /* src tile columns are 16-byte aligned */
+#define COSTA_TILE_VEC_SRC 0x4u /* src tile columns may be read as 16-byte vectors: 16-byte aligned, or
+                                  (4-byte elements, ops of at least one large sub-tile) dword aligned;
+                                  the planner sets it for 16-byte alignment, the executor's work
+                                  lists add the dword-aligned case */
 #define COSTA_TILE_VEC_DST 0x8u /* dst tile rows/columns are 16-byte aligned */
 #define COSTA_SCALE_SHIFT 4
 #define COSTA_SCALE_MASK 0x30u
