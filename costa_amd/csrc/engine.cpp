@@ -426,73 +426,6 @@ void emit_pieces(const costa_tile_op_t& op, int64_t E, const wave_grid& g, bool 
     }
 }
 
-// Source neighbours: the tiles one source block is cut into by the target grid continue each
-// other's columns (the op starting at src + nf * E with the same stride holds the rows below),
-// and each pair shares the cache lines where a column of the upper one ends and the same
-// column of the lower one begins.  In destination-address order the two run one target
-// block-row apart (cfg 5: ~5 MB of traffic, far beyond an XCD's L2), so those lines are fetched
-// twice.  This pulls every op's chain of lower neighbours right behind it (keeping the order
-// otherwise): the shared lines then meet in one L2.
-void chain_source_neighbours(const std::vector<const costa_tile_op_t*>& ops, int64_t E,
-                             std::vector<uint32_t>& perm) {
-    const size_t n = ops.size();
-    std::vector<std::pair<uint64_t, uint32_t>> by_src(n);
-    for (size_t i = 0; i < n; ++i) by_src[i] = {ops[i]->src, uint32_t(i)};
-    std::sort(by_src.begin(), by_src.end());
-    auto below = [&](uint32_t i) -> int64_t {
-        const costa_tile_op_t& o = *ops[i];
-        const uint64_t want = o.src + uint64_t(int64_t(o.nf) * E);
-        auto it = std::lower_bound(by_src.begin(), by_src.end(), std::make_pair(want, uint32_t(0)));
-        if (it == by_src.end() || it->first != want) return -1;
-        const costa_tile_op_t& b = *ops[it->second];
-        if (b.lds != o.lds || b.ns != o.ns || (b.flags & COSTA_TILE_TRANSPOSE) != (o.flags & COSTA_TILE_TRANSPOSE))
-            return -1;
-        return int64_t(it->second);
-    };
-    std::vector<char> done(n, 0);
-    std::vector<uint32_t> out;
-    out.reserve(n);
-    for (const uint32_t i : perm) {
-        if (done[i]) continue;
-        for (int64_t j = i; j >= 0 && !done[size_t(j)]; j = below(uint32_t(j))) {
-            done[size_t(j)] = 1;
-            out.push_back(uint32_t(j));
-        }
-    }
-    perm.swap(out);
-}
-
-// Destination rows merged in bands (tuning mode COSTA_TINY_SORT=7): in destination order, a
-// maximal run of ops with one destination stride is taken as one target block-row (custom
-// layouts: every block-row has its own ld); `h` consecutive runs are merged by each op's
-// relative position within its run (~ its target column), so the ops one source block is cut
-// into by a block-row boundary run close together in time.
-void merge_row_bands(const std::vector<const costa_tile_op_t*>& ops, int h, std::vector<uint32_t>& perm) {
-    const size_t n = perm.size();
-    std::vector<uint32_t> run(n);
-    std::vector<std::pair<uint64_t, uint64_t>> span;  // per run: first / last destination
-    for (size_t k = 0; k < n; ++k) {
-        const costa_tile_op_t& o = *ops[perm[k]];
-        if (k == 0 || o.ldd != ops[perm[k - 1]]->ldd) span.push_back({o.dst, o.dst});
-        span.back().second = o.dst;
-        run[k] = uint32_t(span.size() - 1);
-    }
-    struct key_t {
-        uint64_t band, pos, r, k;
-        bool operator<(const key_t& y) const { return std::tie(band, pos, r, k) < std::tie(y.band, y.pos, y.r, y.k); }
-    };
-    std::vector<key_t> key(n);
-    for (size_t k = 0; k < n; ++k) {
-        const auto& sp = span[run[k]];
-        const double f = sp.second > sp.first ? double(ops[perm[k]]->dst - sp.first) / double(sp.second - sp.first) : 0.0;
-        key[k] = {run[k] / uint64_t(h), uint64_t(f * double(1 << 20)), run[k], k};
-    }
-    std::sort(key.begin(), key.end());
-    std::vector<uint32_t> out(n);
-    for (size_t k = 0; k < n; ++k) out[k] = perm[key[k].k];
-    perm.swap(out);
-}
-
 // XCD column bands (wave_knobs::xcd_bands): the tiny kernel gives XCD x the x-th eighth of
 // the list; destination order alone makes that eighth a run of whole target block-rows, so an A
 // cache line shared by the tiles above and below a block-row boundary is fetched again one
@@ -680,9 +613,7 @@ struct wave_knobs {  // defaults, overridable for tuning runs
                          // with 256^2 blocks, 0.709 against 0.797 with 512^2; fp32 with its
                          // 128 x 128 sub-tiles 0.366 against 0.396 with 256^2, 0.366 against
                          // 0.454 with 512^2), else 1 (c128 with 128^2 blocks: 2.87 against 2.27
-                         // ms; copy lists untested under 2; tools/order_run.sh,
-                         // tools/f32_order_run.sh, profiles/r2/order/)
-    int band_h = 2;  // COSTA_BAND_H: destination rows merged per band (sort mode 7)
+                         // ms; copy lists untested under 2; profiles/r2/order/)
     int force_sq = 0;   // COSTA_FORCE_SQ=1 (tuning): transposing lists of fp64 / c64 / c128 take the
                         // square sub-tile whatever their ops' size
     int merge = 1;      // COSTA_MERGE=0: ops that continue each other are not merged (tuning; the
@@ -711,10 +642,9 @@ const wave_knobs& knobs() {
     static wave_knobs k = [] {
         wave_knobs x;
         if (const char* s = tuning_env("COSTA_WAVE_POLICY")) x.policy = std::atoi(s) == 1 ? 1 : 2;
-        if (const char* s = tuning_env("COSTA_TINY_SORT")) x.sort = std::atoi(s);
-        if (const char* s = tuning_env("COSTA_LARGE_SORT")) x.large_sort = std::atoi(s);
+        if (const char* s = tuning_env("COSTA_TINY_SORT")) x.sort = std::max(0, std::min(5, std::atoi(s)));
+        if (const char* s = tuning_env("COSTA_LARGE_SORT")) x.large_sort = std::max(0, std::min(3, std::atoi(s)));
         if (const char* s = tuning_env("COSTA_SKEW_XCD")) x.skew_xcd = std::max(-1, std::atoi(s));
-        if (const char* s = tuning_env("COSTA_BAND_H")) x.band_h = std::max(1, std::atoi(s));
         if (const char* s = tuning_env("COSTA_XCD_BANDS")) x.xcd_bands = std::atoi(s);
         if (const char* s = tuning_env("COSTA_MERGE")) x.merge = std::atoi(s);
         if (const char* s = tuning_env("COSTA_FORCE_SQ")) x.force_sq = std::atoi(s);
@@ -925,7 +855,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
             if (n > 0xFFFFFFFFull) throw error(COSTA_ERR_ARG, "costa: tile too large");
             for (uint64_t q = 0; q < n; ++q) work.push_back((i << 32) | q);
         }
-        bool by_address = kn.large_sort == 2 || kn.large_sort >= 4;
+        bool by_address = kn.large_sort == 2;
         if (kn.large_sort == 3) {
             by_address = (E == 4 || E == 8) && ordered.size() > op0;
             for (size_t i = op0; i < ordered.size(); ++i)
@@ -940,15 +870,6 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
                 const uint64_t q = wx & 0xFFFFFFFFull, nbf = uint64_t((op.nf + bf - 1) / bf);
                 const int64_t f0 = int64_t(q % nbf) * bf, s0 = int64_t(q / nbf) * bs;
                 const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
-                if (kn.large_sort >= 4 && tr) {
-                    // tuning: COSTA_LARGE_SORT=4+k pairs 2^k f-neighbours (sub-tiles continuing
-                    // each other's source columns) at each destination position
-                    const int64_t span = int64_t(bf) << (kn.large_sort - 3);
-                    const int64_t fp = f0 / span * span;
-                    const uint64_t a = op.dst + uint64_t((fp * op.ldd + s0) * E);
-                    key[x] = {(a << 4) | uint64_t((f0 - fp) / bf), wx};
-                    continue;
-                }
                 key[x] = {op.dst + uint64_t((tr ? f0 * op.ldd + s0 : s0 * op.ldd + f0) * E), wx};
             }
             std::sort(key.begin(), key.end());
@@ -992,10 +913,8 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         tr = tr || (o->flags & COSTA_TILE_TRANSPOSE);
     }
     const int mode = kn.sort == 5   ? (pack_list ? 1 : 2)
-                     : kn.sort == 6 || kn.sort == 7 ? (pack_list ? 1 : 2)
                      : kn.sort == 4 ? (tr || top == 0 ? 2 : 3)
                      : kn.sort == 3 && top == 0 ? 2 : kn.sort;
-    const bool chain = kn.sort == 6 && !pack_list;
     std::vector<uint32_t> perm(nw);
     if (mode == 3 && size_t(top) <= 4 * nw + 1024) {
         // the planner's hints are ranks within the list: a stable counting sort
@@ -1043,9 +962,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     } else {
         for (size_t i = 0; i < nw; ++i) perm[i] = uint32_t(i);
     }
-    if (chain && nw > 1) chain_source_neighbours(wave_ops, E, perm);
     if (kn.xcd_bands && mode == 2 && top > 0 && nw > 1) xcd_bands(wave_ops, E, kn.xcd_bands, local, perm);
-    if (kn.sort == 7 && !pack_list && nw > 1) merge_row_bands(wave_ops, kn.band_h, perm);
     // pieces: count per op, scan, fill (host threads for long lists)
     std::vector<wave_grid> grid(nw);
     std::vector<size_t> at_piece(nw + 1, 0);

@@ -175,14 +175,7 @@ struct __attribute__((aligned(16))) raw16 {
 // transform is read once and written once, and on MI355X the nt policy moves such streams
 // faster (tools/copy_ceiling.hip, profiles/r2/: a strided 2 GiB copy in 1 KiB column segments
 // 6.37-6.49 TB/s with nt loads and stores against 6.02-6.23 without; cfg 2's transposed access
-// pattern 6.27 against 5.73).  COSTA_NT_LOADS / COSTA_NT_STORES = 0 build the default-policy
-// variant (tuning builds only).
-#ifndef COSTA_NT_LOADS
-#define COSTA_NT_LOADS 1
-#endif
-#ifndef COSTA_NT_STORES
-#define COSTA_NT_STORES 1
-#endif
+// pattern 6.27 against 5.73).
 typedef uint32_t u32x4a __attribute__((ext_vector_type(4)));
 // 16-byte loads need only dword alignment on gfx950 (global_load_dwordx4): sources of 4-byte
 // elements off the 16-byte grid are read this way too (engine.cpp build_work marks them
@@ -191,16 +184,11 @@ typedef uint32_t u32x4d __attribute__((ext_vector_type(4), aligned(4)));
 
 __device__ __forceinline__ raw16 ld16(const void* p) {
     raw16 r;
-#if COSTA_NT_LOADS
     const u32x4d v = __builtin_nontemporal_load(reinterpret_cast<const u32x4d*>(p));
     __builtin_memcpy(&r, &v, 16);
-#else
-    const u32x4d v = *reinterpret_cast<const u32x4d*>(p);
-    __builtin_memcpy(&r, &v, 16);
-#endif
     return r;
 }
-template <bool NT = bool(COSTA_NT_STORES)>
+template <bool NT = true>
 __device__ __forceinline__ void st16(void* p, const raw16& r) {
     if constexpr (NT) {
         u32x4a v;
@@ -224,7 +212,7 @@ __device__ __forceinline__ void vload(vec<T>& out, const T* p, int n, bool vec_o
     }
 }
 
-template <typename T, bool NT = bool(COSTA_NT_STORES)>
+template <typename T, bool NT = true>
 __device__ __forceinline__ void vstore(T* p, const vec<T>& in, int n, bool vec_ok) {
     constexpr int V = vec<T>::V;
     if (vec_ok && n >= V) {
@@ -242,11 +230,8 @@ __device__ __forceinline__ void vstore(T* p, const vec<T>& in, int n, bool vec_o
 // lane k holds column k.  Round r: every lane offers element (k - r) mod V and reads the
 // offer of lane (k + r) mod V.  All indices are compile-time after unrolling.  The cross-lane
 // read is a DPP quad permutation (a VALU move; V <= 4 lanes sit in one quad), not an LDS
-// permute: the large shape spends its non-overlapped LDS time on the tile itself
-// (COSTA_DPP_XCHG=0 builds the ds_bpermute form, tuning builds only).
-#ifndef COSTA_DPP_XCHG
-#define COSTA_DPP_XCHG 1
-#endif
+// permute: the large shape spends its non-overlapped LDS time on the tile itself (the
+// ds_bpermute form ran equally fast, 0.7063 ms both, with the LDS busier).
 template <int V, int R>
 constexpr int quad_ctrl() {  // quad_perm: lane q of each quad reads lane sel(q)
     int c = 0;
@@ -278,13 +263,7 @@ __device__ __forceinline__ void xround(const vec<T>& in, vec<T>& out, int lane) 
     for (int e = 1; e < V; ++e)
         if (e == give) offer = in.e[e];
     T got = offer;
-    if constexpr (R != 0) {
-#if COSTA_DPP_XCHG
-        got = dpp_move<quad_ctrl<V, R>()>(offer);
-#else
-        got = shfl(offer, lane - k + from);
-#endif
-    }
+    if constexpr (R != 0) got = dpp_move<quad_ctrl<V, R>()>(offer);
 #pragma unroll
     for (int e = 0; e < V; ++e)
         if (e == from) out.e[e] = got;
@@ -314,17 +293,10 @@ __device__ __forceinline__ vec<T> lane_transpose(const vec<T>& in, int lane) {
         const T r1 = sel4(k, in.e[1], in.e[2], in.e[3], in.e[0]);
         const T r2 = sel4(k, in.e[2], in.e[3], in.e[0], in.e[1]);
         const T r3 = sel4(k, in.e[3], in.e[0], in.e[1], in.e[2]);
-#if COSTA_DPP_XCHG
         const T g0 = r0;
         const T g1 = dpp_move<quad_ctrl<4, 3>()>(r1);  // from lane (k - 1) & 3
         const T g2 = dpp_move<quad_ctrl<4, 2>()>(r2);  // from lane (k - 2) & 3
         const T g3 = dpp_move<quad_ctrl<4, 1>()>(r3);  // from lane (k - 3) & 3
-#else
-        const T g0 = r0;
-        const T g1 = shfl(r1, lane - k + ((k + 3) & 3));
-        const T g2 = shfl(r2, lane - k + ((k + 2) & 3));
-        const T g3 = shfl(r3, lane - k + ((k + 1) & 3));
-#endif
         out.e[0] = sel4(k, g0, g1, g2, g3);
         out.e[1] = sel4(k, g3, g0, g1, g2);
         out.e[2] = sel4(k, g2, g3, g0, g1);
@@ -418,53 +390,26 @@ struct shape {
 // 128 x 64 slower (0.765-0.811); fp32 'T' 128 x 128 against 256 x 128 / 1024 threads 0.367
 // against 0.578 ms with 128^2 blocks (half-filled sub-tiles before), 0.397 against 0.402 with
 // 256^2; the copy of BASELINE cfg 3 (fp64, 128^2 blocks) 3.17 ms with 64 x 128 against 2.87 with
-// 128 x 128.  COSTA_LARGE_{D,F}_{NT,BF,BS}: tuning builds only (tools/tiny_variants.sh).
-#ifndef COSTA_LARGE_F_BF
-#define COSTA_LARGE_F_NT 512
-#define COSTA_LARGE_F_BF 128
-#define COSTA_LARGE_F_BS 128
-#endif
-#ifndef COSTA_LARGE_D_BF
-#define COSTA_LARGE_D_NT 512
-#define COSTA_LARGE_D_BF 64
-#define COSTA_LARGE_D_BS 128
-#endif
+// 128 x 128.
 // `medium_tr`: 256 threads, 16 KiB sub-tiles, for aligned transposing ops of at least half of
 // one that are below half a large sub-tile (before: cut into wavefront pieces of ~128-byte
 // runs): fp32 64^2 blocks 3.60 -> 4.77 TB/s, 96^2 4.18 -> 4.60; fp64 32^2 4.27 -> 4.97, 48^2
 // 4.27 -> 5.26 (profiles/r2/shapes/medium.log).  None for c64 / c128 (has_medium).
-#ifndef COSTA_MEDIUM  // 0: no medium tier (tuning builds only)
-#define COSTA_MEDIUM 1
-#endif
 template <typename T> struct shapes;
-#ifndef COSTA_COPY_F_BF
-#define COSTA_COPY_F_NT 1024
-#define COSTA_COPY_F_BF 256
-#define COSTA_COPY_F_BS 128
-#endif
 // `small_tr` (fp64): the square 64 x 64 variant of the large transposing shape, 512 threads, for
 // transposing lists whose large ops all fit in it (engine.cpp build_work): a 64^2 block then fills
 // one sub-tile instead of half of a 64 x 128 one, and four workgroups fit a CU.  fp64 16384^2 'T'
 // with 64^2 blocks 0.683-0.726 ms against 0.783 (profiles/r2d/small_blocks/).
-// medium shapes' threads (tuning builds only).  4-byte types take 128 threads when every medium op
+// medium shapes: 256 threads.  4-byte types take 128 threads when every medium op
 // of the list is a whole number of sub-tiles (`medium_tr_full`, engine.cpp work_split::med_full):
 // fp32 64^2 blocks 0.455 -> 0.408 ms (beta = 0 only: with C read 0.628 against 0.610); with
 // ragged ops 128 / 512 threads lost 12-21 % (48^2, 80^2)
 // and fp64 lost 12-14 % at 32^2 / 48^2 (profiles/r2d/medium_threads.log)
-#ifndef COSTA_MED_F_NT
-#define COSTA_MED_F_NT 256
-#endif
-#ifndef COSTA_MED_D_NT
-#define COSTA_MED_D_NT 256
-#endif
-#ifndef COSTA_SQ_COMPLEX  // 0: no square variant for complex types (tuning builds only)
-#define COSTA_SQ_COMPLEX 1
-#endif
 template <> struct shapes<float> {
-    using large = shape<float, COSTA_COPY_F_NT, COSTA_COPY_F_BF, COSTA_COPY_F_BS>;
-    using large_tr = shape<float, COSTA_LARGE_F_NT, COSTA_LARGE_F_BF, COSTA_LARGE_F_BS>;
-    using medium_tr = shape<float, COSTA_MED_F_NT, 64, 64>;
-    static constexpr bool has_medium = COSTA_MEDIUM;
+    using large = shape<float, 1024, 256, 128>;
+    using large_tr = shape<float, 512, 128, 128>;
+    using medium_tr = shape<float, 256, 64, 64>;
+    static constexpr bool has_medium = true;
     using small_tr = large_tr;
     static constexpr bool has_small = false;
     using large_tr_full = large_tr;
@@ -472,10 +417,10 @@ template <> struct shapes<float> {
     using small32_tr = shape<float, 128, 32, 32>;
 };
 template <> struct shapes<int> {
-    using large = shape<int, COSTA_COPY_F_NT, COSTA_COPY_F_BF, COSTA_COPY_F_BS>;
-    using large_tr = shape<int, COSTA_LARGE_F_NT, COSTA_LARGE_F_BF, COSTA_LARGE_F_BS>;
-    using medium_tr = shape<int, COSTA_MED_F_NT, 64, 64>;
-    static constexpr bool has_medium = COSTA_MEDIUM;
+    using large = shape<int, 1024, 256, 128>;
+    using large_tr = shape<int, 512, 128, 128>;
+    using medium_tr = shape<int, 256, 64, 64>;
+    static constexpr bool has_medium = true;
     using small_tr = large_tr;
     static constexpr bool has_small = false;
     using large_tr_full = large_tr;
@@ -486,55 +431,40 @@ template <> struct shapes<int> {
 // flight, one workgroup per CU), c128 512 threads: BASELINE cfg 3's copy (32768^2 fp64, 128^2
 // blocks) 2.80-2.81 ms against 2.89-3.06 with 1024 threads, c128 16384^2 copies 1.469 against
 // 1.577 ms; fp64 256^2 blocks, fp32 and c64 unchanged or slower that way (tools/copy_probe.py,
-// profiles/r2c/copy_shapes/).  COSTA_COPY_{D,F}_{NT,BF,BS}, COSTA_COPY_{C,Z}_NT: tuning builds.
-#ifndef COSTA_COPY_D_BF
-#define COSTA_COPY_D_NT 256
-#define COSTA_COPY_D_BF 128
-#define COSTA_COPY_D_BS 128
-#endif
+// profiles/r2c/copy_shapes/).
 template <> struct shapes<double> {
-    using large = shape<double, COSTA_COPY_D_NT, COSTA_COPY_D_BF, COSTA_COPY_D_BS>;
-    using large_tr = shape<double, COSTA_LARGE_D_NT, COSTA_LARGE_D_BF, COSTA_LARGE_D_BS>;
-    using medium_tr = shape<double, COSTA_MED_D_NT, 32, 64>;
-    static constexpr bool has_medium = COSTA_MEDIUM;
+    using large = shape<double, 256, 128, 128>;
+    using large_tr = shape<double, 512, 64, 128>;
+    using medium_tr = shape<double, 256, 32, 64>;
+    static constexpr bool has_medium = true;
     using small_tr = shape<double, 512, 64, 64>;
     static constexpr bool has_small = true;
     using large_tr_full = large_tr;
     using medium_tr_full = medium_tr;
     using small32_tr = shape<double, 128, 32, 32>;
 };
-#ifndef COSTA_COPY_C_NT
-#define COSTA_COPY_C_NT 1024
-#endif
-#ifndef COSTA_COPY_Z_NT
-#define COSTA_COPY_Z_NT 512
-#endif
-#ifndef COSTA_TR_C_NT  // transposing-list shapes of complex types (tuning builds only)
-#define COSTA_TR_C_NT 1024
-#endif
-#ifndef COSTA_TR_Z_NT  // c128 transposes: 1024 threads.  256 gain 3 % when every op is a whole
-#define COSTA_TR_Z_NT 1024  // number of sub-tiles (cfg 4's 128^2 blocks: 2.19 against 2.26 ms; the
-#endif                      // `large_tr_full` launch, engine.cpp work_split::full) and lose 35-55 %
-                            // with blocks that half-fill them (80^2 3.05 against 1.98 ms, 96^2 2.35
-                            // against 1.74; profiles/r2c/tr_shapes/, profiles/r2d/c128_threads.log)
+// c128 transposes: 1024 threads.  256 gain 3 % when every op is a whole number of sub-tiles (cfg
+// 4's 128^2 blocks: 2.19 against 2.26 ms; the `large_tr_full` launch, engine.cpp
+// work_split::full) and lose 35-55 % with blocks that half-fill them (80^2 3.05 against 1.98 ms,
+// 96^2 2.35 against 1.74; profiles/r2c/tr_shapes/, profiles/r2d/c128_threads.log)
 template <> struct shapes<cpx<float>> {
-    using large = shape<cpx<float>, COSTA_COPY_C_NT, 128, 128>;
-    using large_tr = shape<cpx<float>, COSTA_TR_C_NT, 128, 128>;
+    using large = shape<cpx<float>, 1024, 128, 128>;
+    using large_tr = shape<cpx<float>, 1024, 128, 128>;
     using medium_tr = large_tr;
     static constexpr bool has_medium = false;
     using small_tr = shape<cpx<float>, 512, 64, 64>;
-    static constexpr bool has_small = COSTA_SQ_COMPLEX;
+    static constexpr bool has_small = true;
     using large_tr_full = large_tr;
     using medium_tr_full = medium_tr;
     using small32_tr = shape<cpx<float>, 128, 32, 32>;
 };
 template <> struct shapes<cpx<double>> {
-    using large = shape<cpx<double>, COSTA_COPY_Z_NT, 64, 128>;
-    using large_tr = shape<cpx<double>, COSTA_TR_Z_NT, 64, 128>;
+    using large = shape<cpx<double>, 512, 64, 128>;
+    using large_tr = shape<cpx<double>, 1024, 64, 128>;
     using medium_tr = large_tr;
     static constexpr bool has_medium = false;
     using small_tr = shape<cpx<double>, 256, 64, 64>;
-    static constexpr bool has_small = COSTA_SQ_COMPLEX;
+    static constexpr bool has_small = true;
     using large_tr_full = shape<cpx<double>, 256, 64, 128>;
     using medium_tr_full = medium_tr;
     using small32_tr = shape<cpx<double>, 128, 32, 32>;
@@ -543,7 +473,7 @@ template <> struct shapes<cpx<double>> {
 // One sub-tile.  FULL: the sub-tile is a whole BF x BS block with 16-byte aligned rows on
 // both sides, so every guard below folds away and each thread issues its loads and stores
 // back to back with no per-lane branches (the common case: block-cyclic tiles).
-template <typename T, typename S, bool FULL, bool NT = bool(COSTA_NT_STORES)>
+template <typename T, typename S, bool FULL, bool NT = true>
 __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int s0, int tf_, int ts_,
                                          const char* src_base, char* dst_base, T alpha, T beta,
                                          T* tile) {
@@ -741,7 +671,7 @@ __global__ __launch_bounds__(S::NT) void tile_kernel(const costa_tile_op_t* __re
     const T alpha = scalars[2 * slot];
     const T beta = scalars[2 * slot + 1];
     const uint32_t vec_both = COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST;
-    constexpr bool NT = bool(COSTA_NT_STORES);
+    constexpr bool NT = true;
     if (tf == S::BF && ts == S::BS && (op.flags & vec_both) == vec_both)
         run_tile<T, S, true, NT>(op, f0, s0, tf, ts, src_base, dst_base, alpha, beta, tile);
     else
@@ -761,18 +691,7 @@ __global__ __launch_bounds__(S::NT) void tile_kernel(const costa_tile_op_t* __re
 // ops that read C (beta != 0) are as safe here as anywhere.  The source rows [s0 - G, s0 + BS)
 // are staged (odd pitch: the column-wise LDS reads of the store phase are conflict-free); lanes
 // then walk each destination column in 16-byte chunks, 64 consecutive chunks per instruction.
-#ifndef COSTA_SKEW_BF4  // tuning builds: the skew sub-tile of 4- / 8-byte types
-#define COSTA_SKEW_BF4 32
-#define COSTA_SKEW_BS4 512
-#endif
-#ifndef COSTA_SKEW_BF4W  // 4-byte types whose source columns are off the 16-byte grid too
-#define COSTA_SKEW_BF4W 64
-#define COSTA_SKEW_BS4W 256
-#endif
-#ifndef COSTA_SKEW_BF8
-#define COSTA_SKEW_BF8 64
-#define COSTA_SKEW_BS8 128
-#endif
+// Sub-tiles: 4-byte types 32 x 512, fp64 64 x 128.
 // WIDE (4-byte types, lists whose skew ops also read sources off the 16-byte grid): 64 x 256
 // instead of 32 x 512, so every misaligned source run is 256 bytes, not 128 (its two partial
 // lines shared with the f-neighbour sub-tiles, which engine.cpp build_work then puts on one XCD);
@@ -782,8 +701,8 @@ __global__ __launch_bounds__(S::NT) void tile_kernel(const costa_tile_op_t* __re
 template <typename T, bool WIDE = false>
 struct skew_shape {
     static constexpr int NT = 512;
-    static constexpr int BF = sizeof(T) == 4 ? (WIDE ? COSTA_SKEW_BF4W : COSTA_SKEW_BF4) : COSTA_SKEW_BF8;
-    static constexpr int BS = sizeof(T) == 4 ? (WIDE ? COSTA_SKEW_BS4W : COSTA_SKEW_BS4) : COSTA_SKEW_BS8;
+    static constexpr int BF = sizeof(T) == 4 ? (WIDE ? 64 : 32) : 64;
+    static constexpr int BS = sizeof(T) == 4 ? (WIDE ? 256 : 512) : 128;
     static constexpr int E = int(sizeof(T)), G = 64 / E, RS = BS + G, P = BF + 1;
     static constexpr int V = 16 / E, LPC = BF / V, CPP = NT / LPC, PL = (RS + CPP - 1) / CPP;
     static constexpr int NW = NT / 64;
@@ -867,7 +786,7 @@ __global__ __launch_bounds__(512) void skew_kernel(const costa_tile_op_t* __rest
             for (int e = 0; e < V; ++e)
                 o.e[e] = scale(tcol[(c + e) * P], kind == COSTA_SCALE_AXPBY ? y.e[e] : T(0), kind, false,
                                alpha, beta);
-            vstore<T, bool(COSTA_NT_STORES)>(col + c, o, V, true);
+            vstore<T, true>(col + c, o, V, true);
         }
     }
 }
@@ -915,22 +834,10 @@ void launch_skew(const launch_args& a, const uint64_t* work, int64_t n, hipStrea
 // workgroup), 0.722 with 8; without the early old-value loads 0.948 (profiles/r3b/glds/).
 // Wavefronts per workgroup: 8 (4 KiB of LDS each for lists that transpose; copy-only lists
 // without LDS: profiles/r06/c5_knobs.log).
-#ifndef COSTA_TINY_WAVES_TR  // build-time overrides for tuning builds (tools/tiny_variants.sh)
-#define COSTA_TINY_WAVES_TR 8  // r3 (LDS-DMA staging): cfg 5 'T' 0.736-0.738 ms with 4, 0.721-0.723
-#endif                         // with 8, 0.728-0.729 with 16, 0.759-0.761 with 2
-                               // (profiles/r3b/glds/); r2 (register staging) had 4 best
-#ifndef COSTA_TINY_WAVES_COPY
-#define COSTA_TINY_WAVES_COPY 8
-#endif
-#ifndef COSTA_TINY_BYTES
-#define COSTA_TINY_BYTES 32
-#endif
-constexpr int TINY_WAVES_TR = COSTA_TINY_WAVES_TR;
-constexpr int TINY_WAVES_COPY = COSTA_TINY_WAVES_COPY;
-// bytes in flight per lane per pass of the transpose path: 32 since r11 (cfg 5 'T' 3.80 TB/s
-// against 3.51 at 64 and 3.65 at 16, 4 KiB staged, profiles/r11/tiny_variants*.log; before the
-// XCD remap 64 was best: 96 -3 %, 128 -35 %, profiles/r07/c5_bytes.log)
-constexpr int TINY_BYTES = COSTA_TINY_BYTES;
+// r3 (LDS-DMA staging): cfg 5 'T' 0.736-0.738 ms with 4 wavefronts per workgroup, 0.721-0.723
+// with 8, 0.728-0.729 with 16, 0.759-0.761 with 2 (profiles/r3b/glds/)
+constexpr int TINY_WAVES_TR = 8;
+constexpr int TINY_WAVES_COPY = 8;
 // the same for the copy path (engine.hpp tiny_copy_lane_bytes): 64 for every type since r11
 template <typename T> constexpr int tiny_copy_bytes() { return tiny_copy_lane_bytes(sizeof(T)); }
 
@@ -961,30 +868,6 @@ struct lin {  // (f, s) of linear element index e = f + s*n, stepped by 64
 // (element (f, s) at s * pitch + f, pitch odd): an LDS-DMA instruction writes its 64 dwords
 // lane-linearly from a wave-uniform base, so lane j of instruction k takes dword 64 k + j of the
 // padded image and loads whatever source word belongs there (pad words: lane inactive).
-#ifndef COSTA_TINY_GLDS  // 0: register staging (tuning builds only)
-#define COSTA_TINY_GLDS 1
-#endif
-#ifndef COSTA_TINY_GLDS_AUX  // cache policy bits of the LDS-DMA loads (tuning builds: 2 = nt)
-#define COSTA_TINY_GLDS_AUX 0
-#endif
-template <typename T> __device__ __forceinline__ T nt_elem_load(const T* p) { return __builtin_nontemporal_load(p); }
-template <typename R> __device__ __forceinline__ cpx<R> nt_elem_load(const cpx<R>* p) {
-    return {__builtin_nontemporal_load(&p->re), __builtin_nontemporal_load(&p->im)};
-}
-template <typename T> __device__ __forceinline__ void nt_elem_store(T v, T* p) { __builtin_nontemporal_store(v, p); }
-template <typename R> __device__ __forceinline__ void nt_elem_store(cpx<R> v, cpx<R>* p) {
-    __builtin_nontemporal_store(v.re, &p->re);
-    __builtin_nontemporal_store(v.im, &p->im);
-}
-#ifndef COSTA_TINY_NT_ST  // tuning builds: nontemporal destination stores / old-value loads
-#define COSTA_TINY_NT_ST 0
-#endif
-#ifndef COSTA_TINY_NT_LD
-#define COSTA_TINY_NT_LD 0
-#endif
-#ifndef COSTA_TINY_Y_BYTES  // old destination values requested before the wait: a whole staged op
-#define COSTA_TINY_Y_BYTES kTinyLdsDefault
-#endif
 typedef __attribute__((address_space(3))) void lds_void;
 typedef const __attribute__((address_space(1))) void glob_void;
 template <typename T, bool AX>
@@ -993,8 +876,8 @@ __device__ __forceinline__ void tiny_transpose_glds(const T* src, T* dst, int nf
                                                     int lane, T* t) {
     constexpr int W = int(sizeof(T)) / 4;         // dwords per element
     constexpr int DP = 64 / W;                    // image positions per instruction
-    constexpr int NY = COSTA_TINY_Y_BYTES / (64 * int(sizeof(T)));  // passes with old values held
-    constexpr int NP = kTinyLdsBytes / (64 * int(sizeof(T)));         // destination passes at most
+    constexpr int NY = kTinyLdsDefault / (64 * int(sizeof(T)));  // passes with old values held
+    constexpr int NP = kTinyLdsBytes / (64 * int(sizeof(T)));    // destination passes at most
     const int pitch = nf | 1, total = nf * ns, nd = pitch * ns * W;
     {
         const int w = lane % W;
@@ -1005,7 +888,7 @@ __device__ __forceinline__ void tiny_transpose_glds(const T* src, T* dst, int nf
         for (int d0 = 0; d0 < nd; d0 += 64) {
             if (f < nf && d0 + lane < nd)
                 __builtin_amdgcn_global_load_lds((glob_void*)(sb + (int64_t(s) * lds + f) * int64_t(sizeof(T))),
-                                                 (lds_void*)(tb + 4 * d0), 4, 0, COSTA_TINY_GLDS_AUX);
+                                                 (lds_void*)(tb + 4 * d0), 4, 0, 0);
             f += df;
             s += ds;
             if (f >= pitch) {
@@ -1022,11 +905,7 @@ __device__ __forceinline__ void tiny_transpose_glds(const T* src, T* dst, int nf
 #pragma unroll
             for (int u = 0; u < NY; ++u) {
                 if (u * 64 >= total) break;
-#if COSTA_TINY_NT_LD
-                if (u * 64 + lane < total) y[u] = nt_elem_load(dst + int64_t(q.s) * ldd + q.f);
-#else
                 if (u * 64 + lane < total) y[u] = dst[int64_t(q.s) * ldd + q.f];
-#endif
                 q.step();
             }
         }
@@ -1041,11 +920,7 @@ __device__ __forceinline__ void tiny_transpose_glds(const T* src, T* dst, int nf
             T* d = dst + int64_t(q.s) * ldd + q.f;
             T old = e_zero<T>();
             if (AX && kind == COSTA_SCALE_AXPBY) old = u < NY ? y[AX && u < NY ? u : 0] : *d;
-#if COSTA_TINY_NT_ST
-            nt_elem_store(scale(v, old, kind, conj, alpha, beta), d);
-#else
             *d = scale(v, old, kind, conj, alpha, beta);
-#endif
         }
         q.step();
     }
@@ -1055,7 +930,7 @@ __device__ __forceinline__ void tiny_transpose_glds(const T* src, T* dst, int nf
 // compiled out, so copy-only lists keep a high occupancy).  AX = false: no op of the list reads
 // its destination (beta == 0 everywhere), so the copy path holds no old values.  UC: bytes per
 // lane of one copy pass.
-template <typename T, int UB, bool TR, bool AX, int UC>
+template <typename T, bool TR, bool AX, int UC>
 __device__ __forceinline__ void tiny_op(const costa_tile_op_t& op, int lane, T* t,
                                         const char* src_base, char* dst_base,
                                         const T* __restrict__ scalars) {
@@ -1072,7 +947,6 @@ __device__ __forceinline__ void tiny_op(const costa_tile_op_t& op, int lane, T* 
     T* dst = reinterpret_cast<T*>(dst_base + op.dst);
     const int nf = op.nf, ns = op.ns, total = nf * ns;
     const int64_t lds = op.lds, ldd = op.ldd;
-    constexpr int U = UB / int(sizeof(T)) > 0 ? UB / int(sizeof(T)) : 1;
 
     if (!TR || !(flags & COSTA_TILE_TRANSPOSE)) {
         // copy mode: dst(f, s) = g(src(f, s)).  Every load of a pass is issued before the first
@@ -1117,66 +991,8 @@ __device__ __forceinline__ void tiny_op(const costa_tile_op_t& op, int lane, T* 
         }
         return;
     }
-    // transpose mode: stage in LDS (pitch odd), then write in destination order
-    const int pitch = nf | 1;
-#if COSTA_TINY_GLDS
-    if constexpr (sizeof(T) % 4 == 0) {
-        tiny_transpose_glds<T, AX>(src, dst, nf, ns, lds, ldd, kind, conj, alpha, beta, lane, t);
-        return;
-    }
-#endif
-    // (requesting the first pass's old values before the staging loads was measured slower on
-    // cfg 5 'T': 2.92 against 3.13 TB/s; the 16 extra VGPRs cost a wavefront per SIMD)
-    {
-        lin<T> p(lane, nf);
-        for (int e0 = 0; e0 < total; e0 += 64 * U) {
-            T x[U];
-            int fs[U], ss[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                x[u] = e_zero<T>();
-                fs[u] = p.f;
-                ss[u] = p.s;
-                if (e0 + u * 64 + lane < total) x[u] = src[ss[u] * lds + fs[u]];
-                p.step();
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (e0 + u * 64 + lane < total) t[ss[u] * pitch + fs[u]] = x[u];
-        }
-    }
-    // LDS writes of this wave complete before its reads (in-order per wave + explicit wait)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    {
-        lin<T> q(lane, ns);  // destination order: s fastest (dst row f is contiguous in s)
-        for (int e0 = 0; e0 < total; e0 += 64 * U) {
-            T v[U], y[U];
-            int fs[U], ss[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                v[u] = y[u] = e_zero<T>();
-                ss[u] = q.f;  // q.f walks s, q.s walks f
-                fs[u] = q.s;
-                if (e0 + u * 64 + lane < total) v[u] = t[ss[u] * pitch + fs[u]];
-                q.step();
-            }
-            if (kind == COSTA_SCALE_AXPBY) {
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-                    if (e0 + u * 64 + lane < total) y[u] = dst[fs[u] * ldd + ss[u]];
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (e0 + u * 64 + lane >= total) continue;
-                const T r = scale(v[u], kind == COSTA_SCALE_AXPBY ? y[u] : e_zero<T>(), kind, conj,
-                                  alpha, beta);
-                dst[fs[u] * ldd + ss[u]] = r;
-            }
-        }
-    }
+    // transpose mode: staged in LDS by LDS-DMA (pitch odd), then written in destination order
+    tiny_transpose_glds<T, AX>(src, dst, nf, ns, lds, ldd, kind, conj, alpha, beta, lane, t);
 }
 
 // One op per wavefront.  Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md,
@@ -1189,7 +1005,7 @@ __device__ __forceinline__ void tiny_op(const costa_tile_op_t& op, int lane, T* 
 // spills; profiles/r2/w8ab/).  Complex types would spill under it (tests/test_kernel_resources.py).
 template <typename T> struct tiny_min_waves { static constexpr int value = 8; };
 template <typename R> struct tiny_min_waves<cpx<R>> { static constexpr int value = 1; };
-template <typename T, int W, int UB, bool TR, bool AX, int UC>
+template <typename T, int W, bool TR, bool AX, int UC>
 __global__ __launch_bounds__(64 * W, tiny_min_waves<T>::value) void tiny_kernel(const costa_tile_op_t* __restrict__ ops,
                                                       int64_t n_ops, const char* src_base,
                                                       char* dst_base, const T* __restrict__ scalars,
@@ -1203,7 +1019,7 @@ __global__ __launch_bounds__(64 * W, tiny_min_waves<T>::value) void tiny_kernel(
     const int64_t w = b * W + wave;
     if (w >= n_ops) return;
     T* t = reinterpret_cast<T*>(smem) + int64_t(wave) * lds_per_wave;
-    tiny_op<T, UB, TR, AX, UC>(ops[w], lane, t, src_base, dst_base, scalars);
+    tiny_op<T, TR, AX, UC>(ops[w], lane, t, src_base, dst_base, scalars);
 }
 
 template <typename T, int W, bool TR, bool AX>
@@ -1214,7 +1030,7 @@ void launch_tiny_v(const launch_args& a, hipStream_t stream) {
     const size_t lds = size_t(per_wave) * sizeof(T) * W;
     const int64_t blocks = (n + W - 1) / W;
     if (blocks >= (int64_t(1) << 31)) throw error(COSTA_ERR_ARG, "costa: tile list too long");
-    hipLaunchKernelGGL((tiny_kernel<T, W, TINY_BYTES, TR, AX, UC>), dim3(unsigned(blocks)),
+    hipLaunchKernelGGL((tiny_kernel<T, W, TR, AX, UC>), dim3(unsigned(blocks)),
                        dim3(64 * W), lds, stream, a.ops + a.tiny_first, n, a.src_base, a.dst_base,
                        static_cast<const T*>(a.scalars), per_wave);
 }
