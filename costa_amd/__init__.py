@@ -103,7 +103,7 @@ class Stats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
-# COSTA_LIB: another build of the library (tuning builds, tools/tiny_variants.sh)
+# COSTA_LIB: another build of the library (A/B runs against a tuning build of the sources)
 LIB_PATH = os.environ.get("COSTA_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                        "lib", "libcosta_amd.so")
 _lib = None

@@ -384,7 +384,7 @@ struct shape {
 // transpose.  Transposes of fp64 / fp32 / int32 take 512 threads and 64 KiB sub-tiles (~67 KiB
 // of LDS: two workgroups per CU, whose load and store phases overlap); copies, and c64 / c128,
 // 1024 threads and 128 KiB (copies stream 1 KiB column segments; c64 and c128 gained nothing
-// from the halving).  Measured on 16384^2 (r2, tools/shape_sweep.sh, profiles/r2/shapes/):
+// from the halving).  Measured on 16384^2 (r2, profiles/r2/shapes/):
 // fp64 'T' 64 x 128 against 128 x 128 / 1024 threads 0.698 against 0.712 ms with 256^2 and
 // 128^2 blocks, 0.779 against 1.057 with 64^2 blocks (those went to the wavefront path);
 // 128 x 64 slower (0.765-0.811); fp32 'T' 128 x 128 against 256 x 128 / 1024 threads 0.367

@@ -1,5 +1,5 @@
 """Tuning probe (not product): per-phase kernel time of BASELINE cfg 5 (bench.py's workload)
-under the wavefront sort modes (COSTA_TINY_SORT, engine.cpp wave_knobs::sort).  With
+under the wavefront sort modes (COSTA_TUNING=1 COSTA_TINY_SORT, engine.cpp wave_knobs::sort).  With
 COSTA_LOOPBACK=1 every tile goes through PACK -> RCCL self send/recv -> UNPACK, so the pack and
 unpack lists of a multi-rank run are timed on one GPU.
     COSTA_TINY_SORT=5 COSTA_LOOPBACK=1 python tools/c5_sort_probe.py N [steps]"""

@@ -50,7 +50,7 @@ def main():
     for mode in ("0", "1"):
         settings.append({"PROBE_MODE": mode, "COSTA_LOOPBACK": "1"})
     for s in settings:
-        env = dict(os.environ, COSTA_HOST_PIPE_TRACE="1", **s)
+        env = dict(os.environ, COSTA_HOST_PIPE_TRACE="1", COSTA_TUNING="1", **s)
         r = subprocess.run([sys.executable, os.path.abspath(__file__), "child"], env=env,
                            capture_output=True, text=True, timeout=240)
         lines = [l for l in r.stdout.splitlines() if l.startswith("{")]

@@ -1,5 +1,5 @@
 """Tuning probe (not product): one 'T' transform of an n x n matrix on one GPU, kernel time from
-the library's own events.  Used to compare large-shape sub-tile orders (COSTA_LARGE_SORT) across
+the library's own events.  Used to compare large-shape sub-tile orders (COSTA_TUNING=1 COSTA_LARGE_SORT) across
 element types, block sizes and beta:
     python tools/order_probe.py DTYPE N BLOCK BETA [steps]      DTYPE in f32 f64 c64 c128
 """
