@@ -551,6 +551,8 @@ def main():
                          "pztranu c128 alpha,beta != 0, 128^2 blocks (16384^2 per rank); cfg5: "
                          "configs[4] custom_layout many-small fp32 tiles")
     ap.add_argument("--cfg5-op", choices=["N", "T"], default="N")
+    ap.add_argument("--cfg4-beta0", action="store_true",
+                    help="cfg4 with beta = 0 (A/B of the third stream; not a BASELINE config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-extra", action="store_true",
@@ -709,8 +711,10 @@ def main():
             LC = costa.block_cyclic_layout(N, M, b, b, 1, 1, N, M, pm, pn, "R", 0, 0,
                                            Cm.data_ptr(), lr_c, "C", rank, dtype=costa.CDOUBLE)
             al, be = complex(0.75, -0.5), complex(1.25, 0.25)
+            if args.cfg4_beta0:  # A/B only: the same transpose without reading C
+                be = complex(0.0, 0.0)
             wl = (f"pztranu c128 {M}x{N} on a {pm}x{pn} rank grid, 128x128 blocks, op T, "
-                  f"alpha=(0.75,-0.5) beta=(1.25,0.25) (BASELINE configs[3]"
+                  f"alpha=(0.75,-0.5) beta=({be.real},{be.imag}) (BASELINE configs[3]"
                   f"{', single-GPU slice' if world == 1 else ''}"
                   f"{', weak-scaled 16384^2 per rank' if world > 1 and not edge else ''})")
             w.update(LA=LA, LC=LC, A=A, C=Cm, op="T", al=al, be=be, wl=wl, grid=f"{pm}x{pn}",

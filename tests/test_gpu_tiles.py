@@ -338,3 +338,56 @@ def test_full_tile_list(gpu, code):
     bad = np.flatnonzero((got.view(np.uint8).reshape(dst_off, E)
                           != exp.view(np.uint8).reshape(dst_off, E)).any(1))
     assert bad.size == 0, f"{bad.size} elements differ, first at {bad[0]}: {got[bad[0]]} vs {exp[bad[0]]}"
+
+
+@pytest.mark.parametrize("code", [0, 4], ids=["f32", "i32"])
+@pytest.mark.parametrize("seed", [1, 2])
+def test_wavefront_transposes_chunked(gpu, code, seed):
+    """wavefront transposes of 4-byte elements write their destination columns in aligned
+    16-byte chunks with element-wise heads and tails (tile_kernels.hip tiny_transpose_chunked):
+    every destination offset mod 4, leading dimensions ns .. ns + 3 (each column starting at
+    another phase), heights 1 .. 160 (all edges, no full chunk, a single chunk), widths 1 .. 64,
+    ops the host cuts into pieces, every scale kind; neighbouring ops' destination columns share
+    16-byte chunks (no op may write outside its own elements).  Bit-exact against the oracle."""
+    rng = np.random.default_rng(9300 + 10 * seed + code)
+    dt = oracle.NP[code]
+    E = np.dtype(dt).itemsize
+    n_ops = 600
+    ops = np.zeros(n_ops, costa_amd.TILE_OP_DTYPE)
+    src_off = dst_off = 0
+    for i in range(n_ops):
+        nf = int(rng.integers(1, 65))
+        ns = int(rng.choice([int(rng.integers(1, 12)), int(rng.integers(8, 161))]))
+        lds = nf + int(rng.integers(0, 4))
+        ldd = ns + int(rng.integers(0, 4))
+        src_off += int(rng.integers(0, 4))
+        dst_off += int(rng.integers(0, 4))
+        kind = int(rng.integers(1, 4))
+        slot = (0, 1, 2, 3)[kind] if kind != 2 else int(rng.choice([0, 2]))
+        flags = 1 | (kind << 4) | (slot << 16)
+        if (src_off * E) % 16 == 0 and (lds * E) % 16 == 0:
+            flags |= 4
+        if (dst_off * E) % 16 == 0 and (ldd * E) % 16 == 0:
+            flags |= 8
+        ops[i] = (src_off * E, dst_off * E, nf, ns, lds, ldd, flags, 0)
+        src_off += (ns - 1) * lds + nf
+        # the next op's destination starts inside this op's last column's padding (ldd > ns) or
+        # right after it: 16-byte chunks are shared between ops
+        dst_off += (nf - 1) * ldd + ns
+    src = _values(rng, dt, src_off)
+    dst0 = _values(rng, dt, dst_off + 8)
+    if dt == np.int32:
+        scal = np.array([1, 0, 0, 0, 2, 0, -3, 5], dt)
+    else:
+        a, b = _values(rng, dt, 2)
+        scal = np.array([1, 0, 0, 0, a, 0, a, b], dt)
+    exp = dst0.copy()
+    oracle.exec_tile_ops(code, ops, scal, src.ctypes.data, exp.ctypes.data)
+    d_src = torch.from_numpy(src.view(np.uint8).copy()).cuda()
+    d_dst = torch.from_numpy(dst0.view(np.uint8).copy()).cuda()
+    gpu.execute_tiles(code, ops, scal, d_src.data_ptr(), d_dst.data_ptr())
+    torch.cuda.synchronize()
+    got = d_dst.cpu().numpy().view(dt)
+    n = dst0.size
+    bad = np.flatnonzero((got.view(np.uint8).reshape(n, E) != exp.view(np.uint8).reshape(n, E)).any(1))
+    assert bad.size == 0, f"{bad.size} elements differ, first at {bad[0]}: {got[bad[0]]} vs {exp[bad[0]]}"

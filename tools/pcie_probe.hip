@@ -143,6 +143,37 @@ int main(int argc, char** argv) {
         std::printf("hipHostUnregister both: %.2f ms\n", (now() - t0) * 1e3);
     }
 
+    std::printf("-- mixed: one direction pageable (the runtime's path), the other pinned\n");
+    {
+        char* pin;
+        CK(hipHostMalloc(reinterpret_cast<void**>(&pin), N, hipHostMallocDefault));
+        std::memset(pin, 3, N);
+        auto d2h_pin = [&](hipStream_t s, size_t chunk) {
+            for (size_t o = 0; o < N; o += chunk)
+                CK(hipMemcpyAsync(pin + o, dC + o, std::min(chunk, N - o), hipMemcpyDeviceToHost, s));
+        };
+        auto h2d_pin = [&](hipStream_t s, size_t chunk) {
+            for (size_t o = 0; o < N; o += chunk)
+                CK(hipMemcpyAsync(dA + o, pin + o, std::min(chunk, N - o), hipMemcpyHostToDevice, s));
+        };
+        timeit("H2D pageable + D2H pinned, two streams", 2 * D, reps,
+               [&] { h2d(hA, s1, N); d2h_pin(s2, N); sync2(); });
+        timeit("H2D pageable + D2H pinned, 64 MiB chunks", 2 * D, reps,
+               [&] { h2d(hA, s1, 64 << 20); d2h_pin(s2, 64 << 20); sync2(); });
+        timeit("H2D pinned + D2H pageable, two streams", 2 * D, reps,
+               [&] { h2d_pin(s1, N); d2h(hC, s2, N); sync2(); });
+        timeit("H2D pinned + D2H pinned, two streams", 2 * D, reps,
+               [&] { h2d_pin(s1, N); d2h_pin(s2, N); sync2(); });
+        // the pinned D2H while 16 host threads copy pinned -> pageable (the scatter) at once
+        timeit("H2D pageable + D2H pinned + 16-thread host copy of 2 GiB", 2 * D, reps, [&] {
+            h2d(hA, s1, 64 << 20);
+            d2h_pin(s2, 64 << 20);
+            par_memcpy(hC, pin, N, 16);
+            sync2();
+        });
+        CK(hipHostFree(pin));
+    }
+
     std::printf("-- pinned staging ring (hipHostMalloc) + host threads\n");
     {
         const size_t ring = 256 << 20;

@@ -31,9 +31,21 @@ if "SQ_WAVE_CYCLES" in vals and "GRBM_GUI_ACTIVE" in vals:
     wc = vals["SQ_WAVE_CYCLES"]
     res["kernel_cycles_per_xcd"] = cyc
     res["avg_waves_resident_per_cu"] = round(4 * wc / (cus * cyc), 2)
-    res["wave_life_cycles"] = round(4 * wc / vals["SQ_WAVES"], 1)
-    res["share_wait_any"] = round(vals["SQ_WAIT_ANY"] / wc, 3)
-    res["share_wait_inst_any"] = round(vals["SQ_WAIT_INST_ANY"] / wc, 3)
-    res["share_active_inst_any"] = round(vals["SQ_ACTIVE_INST_ANY"] / wc, 3)
+    if "SQ_WAVES" in vals:
+        res["wave_life_cycles"] = round(4 * wc / vals["SQ_WAVES"], 1)
+    for c, k in (("SQ_WAIT_ANY", "share_wait_any"), ("SQ_WAIT_INST_ANY", "share_wait_inst_any"),
+                 ("SQ_ACTIVE_INST_ANY", "share_active_inst_any")):
+        if c in vals:
+            res[k] = round(vals[c] / wc, 3)
+if "GRBM_GUI_ACTIVE" in vals:
+    cyc = vals["GRBM_GUI_ACTIVE"] / 8
+    for c in ("TA_TA_BUSY_sum", "TA_ADDR_STALLED_BY_TC_CYCLES_sum", "TA_DATA_STALLED_BY_TC_CYCLES_sum",
+              "TA_ADDR_STALLED_BY_TD_CYCLES_sum", "TD_TD_BUSY_sum", "TD_TC_STALL_sum",
+              "TCP_PENDING_STALL_CYCLES_sum"):
+        if c in vals:  # per CU, as a share of the kernel's cycles
+            res[c.replace("_sum", "") + "_share"] = round(vals[c] / cus / cyc, 3)
+    vm = vals.get("SQ_INSTS_VMEM_RD", 0) + vals.get("SQ_INSTS_VMEM_WR", 0)
+    if vm and "TA_TA_BUSY_sum" in vals:
+        res["TA_busy_cycles_per_vmem_inst"] = round(vals["TA_TA_BUSY_sum"] / vm, 2)
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps({k: v for k, v in res.items() if k != "counters_median_per_dispatch"}))
