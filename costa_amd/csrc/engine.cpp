@@ -217,14 +217,6 @@ const char* tuning_env(const char* name) {
     return on ? std::getenv(name) : nullptr;
 }
 
-int tiny_chunk_mode() {
-    static const int v = [] {
-        const char* s = tuning_env("COSTA_TINY_CHUNK");
-        return s ? (std::atoi(s) != 0) : 1;
-    }();
-    return v;
-}
-
 int loopback_exchange() {
     static const int mode = [] {
         const char* s = std::getenv("COSTA_LOOPBACK");

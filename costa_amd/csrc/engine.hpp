@@ -118,10 +118,6 @@ int loopback_exchange();
 // COSTA_PLANNER, COSTA_HOST_STAGING) and the trace switches are read as documented.
 const char* tuning_env(const char* name);
 
-// wavefront transposes of 4-byte elements: destination side in aligned 16-byte chunks (1) or
-// element by element (0) (tile_kernels.hip tiny_transpose_chunked; COSTA_TINY_CHUNK, tuning)
-int tiny_chunk_mode();
-
 // largest single ncclSend/ncclRecv of the exchange (COSTA_MAX_MSG_BYTES, default 256 MiB)
 size_t max_message_bytes();
 

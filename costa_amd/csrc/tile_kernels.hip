@@ -933,121 +933,6 @@ __device__ __forceinline__ void tiny_transpose_glds(const T* src, T* dst, int nf
     }
 }
 
-// The same with the destination side in aligned 16-byte chunks (4-byte elements, V = 4): every
-// destination column f is a run of ns elements starting eps_f elements past a 16-byte boundary;
-// its body, the aligned chunks [h_f + V k, h_f + V k + V), is read (old values) and written with
-// one 16-byte access per lane, and only the head (h_f < V elements before the first boundary) and
-// the tail (fewer than V after the last) element by element.  A wavefront's vector-memory
-// instructions on the destination side drop from 2 per 64 elements to ~2 per 256 plus the edges:
-// cfg 5 'T''s texture-address units were busy 86 % of the kernel with every access 4 bytes wide
-// (profiles/r3b/pmc_sq_cfg5T.json).  Full-chunk slots run k fastest within a column (a lane's
-// neighbours continue its column: few cache lines per instruction); LDS reads t[(s + e) * pitch
-// + f].
-template <typename T, bool AX>
-__device__ __forceinline__ void tiny_transpose_chunked(const T* src, T* dst, int nf, int ns, int64_t lds,
-                                                       int64_t ldd, uint32_t kind, bool conj, T alpha,
-                                                       T beta, int lane, T* t) {
-    constexpr int V = 16 / int(sizeof(T));
-    static_assert(V == 4, "4-byte elements");
-    constexpr int NC = kTinyLdsBytes / (64 * 16);      // full-chunk passes at most
-    constexpr int NYC = kTinyLdsDefault / (64 * 16);   // ... with old values requested early
-    constexpr int NYP = 2;                             // edge passes with old values requested early
-    const int pitch = nf | 1;
-    tiny_stage(src, nf, ns, lds, pitch, lane, t);
-    const bool ax = AX && kind == COSTA_SCALE_AXPBY;
-    // column f's head: elements before its first 16-byte boundary (eps_f = offset past one)
-    auto head_of = [&](int f) {
-        const int eps = int((reinterpret_cast<uintptr_t>(dst + int64_t(f) * ldd) / sizeof(T)) & (V - 1));
-        return min(ns, (V - eps) & (V - 1));
-    };
-    // edge slots per column: the most any column needs (eps_f repeats with period <= 4 in f)
-    int pe = 0;
-    for (int f = 0; f < min(nf, 4); ++f) {
-        const int h = head_of(f);
-        pe = max(pe, h + ((ns - h) & (V - 1)));
-    }
-    const int ks = ns / V;  // full-chunk slots per column (one may stay empty)
-    const int nchunk = nf * ks, nedge = nf * pe;
-    // slot -> (column, chunk) and (column, edge element); both request their old values now
-    vec<T> yc[AX ? NYC : 1];
-    T ye[AX ? NYP : 1];
-    if constexpr (AX) {
-        if (ax) {
-            lin<T> q(lane, max(ks, 1));  // q.f: chunk k, q.s: column f
-#pragma unroll
-            for (int u = 0; u < NYC; ++u) {
-                if (u * 64 >= nchunk) break;
-                if (q.s < nf) {
-                    const int h = head_of(q.s), s0 = h + V * q.f;
-                    if (s0 + V <= ns) {
-                        const raw16 r = *reinterpret_cast<const raw16*>(dst + int64_t(q.s) * ldd + s0);
-                        __builtin_memcpy(&yc[u], &r, 16);
-                    }
-                }
-                q.step();
-            }
-            lin<T> e(lane, max(pe, 1));  // e.f: edge element j, e.s: column f
-#pragma unroll
-            for (int u = 0; u < NYP; ++u) {
-                if (u * 64 >= nedge) break;
-                if (e.s < nf) {
-                    const int h = head_of(e.s), j = e.f;
-                    const int s = j < h ? j : h + V * ((ns - h) / V) + (j - h);
-                    if (s < ns) ye[u] = dst[int64_t(e.s) * ldd + s];
-                }
-                e.step();
-            }
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA writes (and old values) landed
-    {
-        lin<T> q(lane, max(ks, 1));
-#pragma unroll
-        for (int u = 0; u < NC; ++u) {
-            if (u * 64 >= nchunk) break;
-            if (q.s < nf) {
-                const int f = q.s, h = head_of(f), s0 = h + V * q.f;
-                if (s0 + V <= ns) {
-                    T* d = dst + int64_t(f) * ldd + s0;
-                    vec<T> y;
-                    if (ax) {
-                        if (u < NYC) {
-                            y = yc[AX && u < NYC ? u : 0];
-                        } else {
-                            const raw16 r = *reinterpret_cast<const raw16*>(d);
-                            __builtin_memcpy(&y, &r, 16);
-                        }
-                    }
-                    vec<T> o;
-#pragma unroll
-                    for (int k = 0; k < V; ++k)
-                        o.e[k] = scale(t[(s0 + k) * pitch + f], ax ? y.e[k] : e_zero<T>(), kind, conj, alpha, beta);
-                    raw16 r;
-                    __builtin_memcpy(&r, &o, 16);
-                    *reinterpret_cast<raw16*>(d) = r;
-                }
-            }
-            q.step();
-        }
-    }
-    {
-        lin<T> e(lane, max(pe, 1));
-        for (int u = 0; u * 64 < nedge; ++u) {
-            if (e.s < nf) {
-                const int f = e.s, h = head_of(f), j = e.f;
-                const int s = j < h ? j : h + V * ((ns - h) / V) + (j - h);
-                if (s < ns) {
-                    T* d = dst + int64_t(f) * ldd + s;
-                    T old = e_zero<T>();
-                    if (ax) old = u < NYP ? ye[AX && u < NYP ? u : 0] : *d;
-                    *d = scale(t[s * pitch + f], old, kind, conj, alpha, beta);
-                }
-            }
-            e.step();
-        }
-    }
-}
-
 // TR = false: the list has no transposing op (the transpose path and its registers are
 // compiled out, so copy-only lists keep a high occupancy).  AX = false: no op of the list reads
 // its destination (beta == 0 everywhere), so the copy path holds no old values.  UC: bytes per
@@ -1055,7 +940,7 @@ __device__ __forceinline__ void tiny_transpose_chunked(const T* src, T* dst, int
 template <typename T, bool TR, bool AX, int UC>
 __device__ __forceinline__ void tiny_op(const costa_tile_op_t& op, int lane, T* t,
                                         const char* src_base, char* dst_base,
-                                        const T* __restrict__ scalars, int chunk) {
+                                        const T* __restrict__ scalars) {
     const uint32_t flags = op.flags;
     const uint32_t kind = (flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT;
     const bool conj = flags & COSTA_TILE_CONJ;
@@ -1114,12 +999,9 @@ __device__ __forceinline__ void tiny_op(const costa_tile_op_t& op, int lane, T* 
         return;
     }
     // transpose mode: staged in LDS by LDS-DMA (pitch odd), then written in destination order
-    if constexpr (sizeof(T) == 4) {
-        if (chunk && ns >= 8) {
-            tiny_transpose_chunked<T, AX>(src, dst, nf, ns, lds, ldd, kind, conj, alpha, beta, lane, t);
-            return;
-        }
-    }
+    // (the destination side in aligned 16-byte chunks, element-wise heads and tails, halved the
+    // vector-memory instructions of cfg 5 'T' and ran 10 % slower with 25 % more L2 requests:
+    // profiles/r4a/cfg5T_chunk_ab.txt, profiles/r4b/)
     tiny_transpose_glds<T, AX>(src, dst, nf, ns, lds, ldd, kind, conj, alpha, beta, lane, t);
 }
 
@@ -1137,7 +1019,7 @@ template <typename T, int W, bool TR, bool AX, int UC>
 __global__ __launch_bounds__(64 * W, tiny_min_waves<T>::value) void tiny_kernel(const costa_tile_op_t* __restrict__ ops,
                                                       int64_t n_ops, const char* src_base,
                                                       char* dst_base, const T* __restrict__ scalars,
-                                                      int lds_per_wave, int chunk) {
+                                                      int lds_per_wave) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = int(threadIdx.x) % 64;
     const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / 64);
@@ -1147,7 +1029,7 @@ __global__ __launch_bounds__(64 * W, tiny_min_waves<T>::value) void tiny_kernel(
     const int64_t w = b * W + wave;
     if (w >= n_ops) return;
     T* t = reinterpret_cast<T*>(smem) + int64_t(wave) * lds_per_wave;
-    tiny_op<T, TR, AX, UC>(ops[w], lane, t, src_base, dst_base, scalars, chunk);
+    tiny_op<T, TR, AX, UC>(ops[w], lane, t, src_base, dst_base, scalars);
 }
 
 template <typename T, int W, bool TR, bool AX>
@@ -1160,7 +1042,7 @@ void launch_tiny_v(const launch_args& a, hipStream_t stream) {
     if (blocks >= (int64_t(1) << 31)) throw error(COSTA_ERR_ARG, "costa: tile list too long");
     hipLaunchKernelGGL((tiny_kernel<T, W, TR, AX, UC>), dim3(unsigned(blocks)),
                        dim3(64 * W), lds, stream, a.ops + a.tiny_first, n, a.src_base, a.dst_base,
-                       static_cast<const T*>(a.scalars), per_wave, tiny_chunk_mode());
+                       static_cast<const T*>(a.scalars), per_wave);
 }
 
 template <typename T>

@@ -342,10 +342,10 @@ def test_full_tile_list(gpu, code):
 
 @pytest.mark.parametrize("code", [0, 4], ids=["f32", "i32"])
 @pytest.mark.parametrize("seed", [1, 2])
-def test_wavefront_transposes_chunked(gpu, code, seed):
-    """wavefront transposes of 4-byte elements write their destination columns in aligned
-    16-byte chunks with element-wise heads and tails (tile_kernels.hip tiny_transpose_chunked):
-    every destination offset mod 4, leading dimensions ns .. ns + 3 (each column starting at
+def test_wavefront_transposes_every_phase(gpu, code, seed):
+    """wavefront transposes of 4-byte elements into destination columns at every 16-byte phase
+    (r4 measured a variant that writes aligned 16-byte chunks with element-wise heads and tails;
+    this pins the edges any such variant must get right): every destination offset mod 4, leading dimensions ns .. ns + 3 (each column starting at
     another phase), heights 1 .. 160 (all edges, no full chunk, a single chunk), widths 1 .. 64,
     ops the host cuts into pieces, every scale kind; neighbouring ops' destination columns share
     16-byte chunks (no op may write outside its own elements).  Bit-exact against the oracle."""
