@@ -164,6 +164,41 @@ int main(int argc, char** argv) {
                [&] { h2d_pin(s1, N); d2h(hC, s2, N); sync2(); });
         timeit("H2D pinned + D2H pinned, two streams", 2 * D, reps,
                [&] { h2d_pin(s1, N); d2h_pin(s2, N); sync2(); });
+        // does an async D2H into pageable memory return before it completes?  (the host
+        // pipeline's issuing thread must not stall on it)
+        {
+            const size_t c = size_t(64) << 20;
+            double ret = 0, done = 0;
+            for (int r = 0; r < 5; ++r) {
+                CK(hipDeviceSynchronize());
+                const double t0 = now();
+                CK(hipMemcpyAsync(hC, dC, c, hipMemcpyDeviceToHost, s2));
+                const double t1 = now();
+                CK(hipStreamSynchronize(s2));
+                const double t2 = now();
+                if (r) ret += t1 - t0, done += t2 - t0;
+            }
+            std::printf("D2H pageable 64 MiB hipMemcpyAsync: call returns after %.3f ms, done after %.3f ms\n",
+                        ret / 4 * 1e3, done / 4 * 1e3);
+            for (int r = 0; r < 5; ++r) {
+                CK(hipDeviceSynchronize());
+                const double t0 = now();
+                CK(hipMemcpyAsync(pin, dC, c, hipMemcpyDeviceToHost, s2));
+                const double t1 = now();
+                CK(hipStreamSynchronize(s2));
+                const double t2 = now();
+                if (r) ret += t1 - t0, done += t2 - t0;
+            }
+        }
+        timeit("H2D pinned + D2H pageable, 64 MiB chunks", 2 * D, reps,
+               [&] { h2d_pin(s1, 64 << 20); d2h(hC, s2, 64 << 20); sync2(); });
+        timeit("H2D pinned + D2H pageable 64 MiB chunks + 16-thread host copy of 2 GiB", 2 * D, reps, [&] {
+            h2d_pin(s1, 64 << 20);
+            std::thread t([&] { par_memcpy(pin, hA, N, 15); });
+            d2h(hC, s2, 64 << 20);
+            t.join();
+            sync2();
+        });
         // the pinned D2H while 16 host threads copy pinned -> pageable (the scatter) at once
         timeit("H2D pageable + D2H pinned + 16-thread host copy of 2 GiB", 2 * D, reps, [&] {
             h2d(hA, s1, 64 << 20);
