@@ -599,8 +599,6 @@ struct wave_knobs {  // defaults, overridable for tuning runs
     int skew_xcd = -1;   // COSTA_SKEW_XCD=F (tuning): F skew sub-tiles continuing each other's
                          // source rows on one XCD (one L2) at the same time; -1 (default):
                          // kSkewWideGroup for lists on the wide skew variant, else none
-    int interleave = 1;  // COSTA_LARGE_INTERLEAVE=K (tuning): the shaped work list cut into K equal
-                         // runs dealt out round-robin (position p takes run p % K)
     int large_sort = 3;  // COSTA_LARGE_SORT 1: large ops in the order of the planner's locality
                          // hint (column-major target order: consecutive ops continue down the
                          // same target columns, so the write stream is sequential in aggregate);
@@ -646,7 +644,6 @@ const wave_knobs& knobs() {
         if (const char* s = tuning_env("COSTA_WAVE_POLICY")) x.policy = std::atoi(s) == 1 ? 1 : 2;
         if (const char* s = tuning_env("COSTA_TINY_SORT")) x.sort = std::max(0, std::min(5, std::atoi(s)));
         if (const char* s = tuning_env("COSTA_LARGE_SORT")) x.large_sort = std::max(0, std::min(3, std::atoi(s)));
-        if (const char* s = tuning_env("COSTA_LARGE_INTERLEAVE")) x.interleave = std::max(1, std::atoi(s));
         if (const char* s = tuning_env("COSTA_SKEW_XCD")) x.skew_xcd = std::max(-1, std::atoi(s));
         if (const char* s = tuning_env("COSTA_XCD_BANDS")) x.xcd_bands = std::atoi(s);
         if (const char* s = tuning_env("COSTA_MERGE")) x.merge = std::atoi(s);
@@ -884,22 +881,6 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
             }
             std::sort(key.begin(), key.end());
             for (size_t x = 0; x < key.size(); ++x) work[w0 + x] = key[x].second;
-        }
-        if (c == 0 && kn.interleave > 1 && work.size() - w0 > 1) {
-            const size_t n = work.size() - w0, K = size_t(kn.interleave);
-            std::vector<uint64_t> w(work.begin() + int64_t(w0), work.end());
-            for (size_t p = 0; p < n; ++p) {
-                const size_t run = p % K, i = p / K;
-                const size_t lo = n * run / K, hi = n * (run + 1) / K;
-                work[w0 + p] = lo + i < hi ? w[lo + i] : w[p];
-            }
-            // (ragged runs: positions past a short run keep their item; fix up by a stable pass)
-            bool ok = true;
-            for (size_t p = 0; p < n && ok; ++p) {
-                const size_t run = p % K, i = p / K, lo = n * run / K, hi = n * (run + 1) / K;
-                ok = lo + i < hi;
-            }
-            if (!ok) std::copy(w.begin(), w.end(), work.begin() + int64_t(w0));
         }
         if (c == 2 && skew_group > 1 && work.size() - w0 > 1) {
             // runs of F f-neighbours at one destination position, then run r of every 8 runs
