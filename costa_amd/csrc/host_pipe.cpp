@@ -247,6 +247,10 @@ void release_host_rings() { rings().clear(); }
 // ---------------------------------------------------------------- the pipeline of one plan
 struct host_pipeline {
     enum kind_t { PACK, LOCAL, UNPACK };
+    struct rect {         // h rows of w elements at a stride of pitch elements from host address base
+        uintptr_t base = 0;
+        int64_t w = 0, h = 0, pitch = 0;
+    };
     struct hop {          // one op (or piece of one) with its host addresses
         costa_tile_op_t op;
         uint64_t in_off, out_off;  // offsets in the group's source / target packages
@@ -267,6 +271,12 @@ struct host_pipeline {
         size_t ord_first = 0, work_first = 0;
         bool any_tr = false;
         int64_t alg_bytes = 0;
+        // direct mode (page-locked caller memory): the group's source and target footprints as
+        // host rectangles, each moved by one strided DMA into / out of a dense device image,
+        // and the op list that reads / writes those images
+        rect src_rect, dst_rect;
+        work_split split_d;
+        size_t ord_first_d = 0, work_first_d = 0;
     };
     costa_dtype_t dtype = COSTA_DOUBLE;
     size_t E = 8;
@@ -280,9 +290,15 @@ struct host_pipeline {
     std::vector<int> rounds_after;    // ... issued once group t is enqueued (cumulative)
     void* d_ops = nullptr;   // every group's ordered device ops (package offsets)
     void* d_work = nullptr;
+    bool direct_ok = false;  // every group LOCAL with rectangle footprints (direct mode possible)
+    void* d_ops_d = nullptr;  // ... and its device ops (image offsets)
+    void* d_work_d = nullptr;
+    // the caller's host byte ranges the ops read or write (merged): when all of them are
+    // page-locked the pipeline moves tiles by strided DMA instead of host copies
+    std::vector<std::pair<uintptr_t, uintptr_t>> host_ranges;
     ~host_pipeline() {
-        if (d_ops) (void)hipFree(d_ops);
-        if (d_work) (void)hipFree(d_work);
+        for (void* p : {d_ops, d_work, d_ops_d, d_work_d})
+            if (p) (void)hipFree(p);
     }
 };
 
@@ -328,6 +344,39 @@ void cut(const costa_tile_op_t& op, size_t E, bool whole_columns, std::vector<co
 }
 
 }  // namespace
+
+// The union of footprints (h rows of w elements at address a, stride pitch; one per hop) as one
+// rectangle of the caller's array: every footprint must share the pitch and lie on the same 2D
+// grid as the first, and together they must tile their bounding box exactly (the ops of a
+// transform are disjoint, so equal areas suffice).  Returns false otherwise.
+struct foot {
+    uintptr_t a;
+    int64_t w, h, pitch;
+};
+bool rectangle_of(const std::vector<foot>& f, size_t E, host_pipeline::rect& r,
+                  std::vector<std::pair<int64_t, int64_t>>& xy) {
+    if (f.empty()) return false;
+    const int64_t P = f[0].pitch;
+    int64_t x0 = INT64_MAX, x1 = INT64_MIN, y0 = INT64_MAX, y1 = INT64_MIN, area = 0;
+    xy.clear();
+    for (const auto& q : f) {
+        if (q.pitch != P || P <= 0 || q.w > P) return false;
+        const int64_t d = int64_t(q.a) - int64_t(f[0].a);
+        if (d % int64_t(E)) return false;
+        const int64_t e = d / int64_t(E);
+        const int64_t y = e >= 0 ? e / P : -((-e + P - 1) / P), x = e - y * P;
+        if (x + q.w > P) return false;
+        xy.push_back({x, y});
+        x0 = std::min(x0, x), x1 = std::max(x1, x + q.w);
+        y0 = std::min(y0, y), y1 = std::max(y1, y + q.h);
+        area += q.w * q.h;
+    }
+    if (area != (x1 - x0) * (y1 - y0)) return false;
+    r.base = uintptr_t(int64_t(f[0].a) + (y0 * P + x0) * int64_t(E));
+    r.w = x1 - x0, r.h = y1 - y0, r.pitch = P;
+    for (auto& p : xy) p = {p.first - x0, p.second - y0};  // position inside the rectangle
+    return true;
+}
 
 bool host_pipeline_accepts(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& pack_ops) {
     const size_t E = dtype_size(dtype);
@@ -381,7 +430,43 @@ std::shared_ptr<host_pipeline> make_host_pipeline(costa_dtype_t dtype,
         close();
         g.kind = kind;
         g.round = sg.second;
-        for (const auto& p : pieces) {
+        // LOCAL: pieces come in target row-band order (the planner's key order); a band is a run
+        // of pieces whose targets cover the same rows of one array.  A group takes whole bands
+        // while they fit, so that its footprints stay rectangles of the caller's arrays (direct
+        // mode, below); a band larger than a slot is cut piece by piece as before.
+        std::vector<size_t> band_end(pieces.size(), 0);
+        if (kind == hpl::LOCAL) {
+            size_t b0 = 0;
+            auto xrange = [&](const costa_tile_op_t& q, int64_t& x, int64_t& w) {
+                int64_t run, runs;
+                target_shape(q, run, runs);
+                const int64_t e = (int64_t(q.dst) - int64_t(pieces[b0].dst)) / int64_t(E);
+                const int64_t P = std::max<int64_t>(1, q.ldd);
+                x = ((e % P) + P) % P;
+                w = run;
+            };
+            for (size_t i = 0; i <= pieces.size(); ++i) {
+                bool same = false;
+                if (i < pieces.size() && i > b0) {
+                    int64_t x, w, xb, wb;
+                    xrange(pieces[i], x, w);
+                    xrange(pieces[b0], xb, wb);
+                    same = pieces[i].ldd == pieces[b0].ldd && x == xb && w == wb;
+                }
+                if (i == pieces.size() || (i > b0 && !same)) {
+                    for (size_t j = b0; j < i; ++j) band_end[j] = i;
+                    b0 = i;
+                }
+            }
+        }
+        for (size_t pi = 0; pi < pieces.size(); ++pi) {
+            const auto& p = pieces[pi];
+            if (kind == hpl::LOCAL && g.count && (pi == 0 || band_end[pi - 1] == pi)) {
+                size_t bin = 0;  // a band starts here: close the group if the whole band won't fit
+                for (size_t j = pi; j < band_end[pi]; ++j)
+                    bin += align_up(size_t(pieces[j].nf) * size_t(pieces[j].ns) * E);
+                if (bin <= kSlot && (g.in_bytes + bin > kSlot || g.out_bytes + bin > kSlot)) close();
+            }
             const size_t bytes = size_t(p.nf) * size_t(p.ns) * E;
             if (kind == hpl::PACK) {  // dense; a group is one contiguous range of the package
                 if (g.count && (g.in_bytes + bytes > kSlot || p.dst != g.send_off + g.in_bytes)) close();
@@ -480,6 +565,87 @@ std::shared_ptr<host_pipeline> make_host_pipeline(costa_dtype_t dtype,
         all_ord.insert(all_ord.end(), ord.begin(), ord.end());
         all_work.insert(all_work.end(), work.begin(), work.end());
     }
+    // direct mode: every group LOCAL and both footprints rectangles of the caller's arrays
+    std::vector<costa_tile_op_t> all_ord_d;
+    std::vector<uint64_t> all_work_d;
+    hp->direct_ok = !hp->groups.empty();
+    for (auto& gr : hp->groups) {
+        if (!hp->direct_ok) break;
+        if (gr.kind != hpl::LOCAL) {
+            hp->direct_ok = false;
+            break;
+        }
+        std::vector<foot> fs, ft;
+        for (size_t i = gr.first; i < gr.first + gr.count; ++i) {
+            const auto& op = hp->hops[i].op;
+            int64_t run, runs;
+            target_shape(op, run, runs);
+            fs.push_back({uintptr_t(op.src), op.nf, op.ns, op.lds});
+            ft.push_back({uintptr_t(op.dst), run, runs, op.ldd});
+        }
+        std::vector<std::pair<int64_t, int64_t>> ps, pt;
+        if (!rectangle_of(fs, E, gr.src_rect, ps) || !rectangle_of(ft, E, gr.dst_rect, pt)) {
+            hp->direct_ok = false;
+            break;
+        }
+        std::vector<costa_tile_op_t> dev_ops;
+        for (size_t i = gr.first; i < gr.first + gr.count; ++i) {
+            const size_t j = i - gr.first;
+            costa_tile_op_t d = hp->hops[i].op;
+            d.src = uint64_t((ps[j].second * gr.src_rect.w + ps[j].first) * int64_t(E));
+            d.lds = int32_t(gr.src_rect.w);
+            d.dst = uint64_t((pt[j].second * gr.dst_rect.w + pt[j].first) * int64_t(E));
+            d.ldd = int32_t(gr.dst_rect.w);
+            d.flags &= ~uint32_t(COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST);
+            if (d.src % 16 == 0 && (int64_t(d.lds) * int64_t(E)) % 16 == 0) d.flags |= COSTA_TILE_VEC_SRC;
+            if (d.dst % 16 == 0 && (int64_t(d.ldd) * int64_t(E)) % 16 == 0) d.flags |= COSTA_TILE_VEC_DST;
+            dev_ops.push_back(d);
+        }
+        std::vector<costa_tile_op_t> ord;
+        std::vector<uint64_t> work;
+        gr.split_d = build_work(dtype, dev_ops, ord, work);
+        gr.ord_first_d = all_ord_d.size();
+        gr.work_first_d = all_work_d.size();
+        all_ord_d.insert(all_ord_d.end(), ord.begin(), ord.end());
+        all_work_d.insert(all_work_d.end(), work.begin(), work.end());
+    }
+    if (hp->direct_ok) {
+        if (!all_ord_d.empty()) {
+            HP_CHECK(hipMalloc(&hp->d_ops_d, all_ord_d.size() * sizeof(costa_tile_op_t)));
+            HP_CHECK(hipMemcpy(hp->d_ops_d, all_ord_d.data(), all_ord_d.size() * sizeof(costa_tile_op_t),
+                               hipMemcpyHostToDevice));
+        }
+        if (!all_work_d.empty()) {
+            HP_CHECK(hipMalloc(&hp->d_work_d, all_work_d.size() * sizeof(uint64_t)));
+            HP_CHECK(hipMemcpy(hp->d_work_d, all_work_d.data(), all_work_d.size() * sizeof(uint64_t),
+                               hipMemcpyHostToDevice));
+        }
+    }
+    {  // host footprints: sources of PACK / LOCAL hops, targets of LOCAL / UNPACK hops
+        auto& r = hp->host_ranges;
+        for (const auto& gr : hp->groups)
+            for (size_t i = gr.first; i < gr.first + gr.count; ++i) {
+                const auto& op = hp->hops[i].op;
+                if (gr.kind != hpl::UNPACK)
+                    r.push_back({uintptr_t(op.src),
+                                 uintptr_t(op.src + ((uint64_t(op.ns) - 1) * uint64_t(op.lds) + uint64_t(op.nf)) * E)});
+                if (gr.kind != hpl::PACK) {
+                    int64_t run, runs;
+                    target_shape(op, run, runs);
+                    r.push_back({uintptr_t(op.dst),
+                                 uintptr_t(op.dst + ((uint64_t(runs) - 1) * uint64_t(op.ldd) + uint64_t(run)) * E)});
+                }
+            }
+        std::sort(r.begin(), r.end());
+        size_t o = 0;
+        for (size_t i = 0; i < r.size(); ++i) {
+            if (o && r[i].first <= r[o - 1].second)
+                r[o - 1].second = std::max(r[o - 1].second, r[i].second);
+            else
+                r[o++] = r[i];
+        }
+        r.resize(o);
+    }
     if (!all_ord.empty()) {
         HP_CHECK(hipMalloc(&hp->d_ops, all_ord.size() * sizeof(costa_tile_op_t)));
         HP_CHECK(hipMemcpy(hp->d_ops, all_ord.data(), all_ord.size() * sizeof(costa_tile_op_t),
@@ -495,6 +661,24 @@ std::shared_ptr<host_pipeline> make_host_pipeline(costa_dtype_t dtype,
 
 size_t host_pipeline_groups(const host_pipeline& hp) { return hp.groups.size(); }
 
+namespace {
+// every byte range page-locked host memory (hipHostMalloc / hipHostRegister), checked at both
+// ends of each range (a range is one layout's footprint inside one caller array)
+bool all_pinned(const std::vector<std::pair<uintptr_t, uintptr_t>>& ranges) {
+    if (ranges.empty()) return false;
+    for (const auto& r : ranges)
+        for (uintptr_t p : {r.first, r.second - 1}) {
+            hipPointerAttribute_t a{};
+            if (hipPointerGetAttributes(&a, reinterpret_cast<void*>(p)) != hipSuccess) {
+                (void)hipGetLastError();  // pageable memory: an error the runtime keeps otherwise
+                return false;
+            }
+            if (a.type != hipMemoryTypeHost) return false;
+        }
+    return true;
+}
+}  // namespace
+
 void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void* exchange_stream,
                        char* send_buf, char* recv_buf,
                        const std::function<void(void*, int)>& exchange, const void* d_scalars) {
@@ -507,6 +691,11 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
     const size_t E = hp.E;
     const size_t G = hp.groups.size();
     const bool prof = profiling();
+    // page-locked caller memory: tiles move by strided DMA between the caller's arrays and the
+    // device slots (no host gather / scatter, no pinned slots); the host only issues, stream
+    // events order everything.  pinned H2D + D2H of 1-16 KiB rows at once: 94-97 GB/s
+    // (tools/pcie_probe.hip, profiles/r4h/)
+    const bool direct = hp.direct_ok && all_pinned(hp.host_ranges);
     // timing brackets (profiling only): per group kernel, the exchange, and the spans of both
     // copy streams
     std::vector<hipEvent_t> evs;
@@ -585,6 +774,16 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
         });
     };
 
+    // direct mode: one strided DMA per rectangle between the caller's array and the device image
+    auto move_rect = [&](const hpl::rect& r, char* image, bool up) {
+        const size_t w = size_t(r.w) * E, pitch = size_t(r.pitch) * E;
+        void* host = reinterpret_cast<void*>(r.base);
+        if (up)
+            HP_CHECK(hipMemcpy2DAsync(image, w, host, pitch, w, size_t(r.h), hipMemcpyHostToDevice, R.up));
+        else
+            HP_CHECK(hipMemcpy2DAsync(host, pitch, image, w, w, size_t(r.h), hipMemcpyDeviceToHost, R.down));
+    };
+
     // COSTA_HOST_PIPE_TRACE=1: host-side time split (copies / waits / issue) on stderr
     static const bool trace = std::getenv("COSTA_HOST_PIPE_TRACE") != nullptr;
     double t_copy = 0, t_wait_up = 0, t_wait_down = 0, t_issue = 0;
@@ -602,12 +801,12 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
         char* dev = R.dev + size_t(k) * 2 * S;
         double t0 = now();
         // the pinned source slot is free once its previous upload has landed
-        if (g) HP_CHECK(hipEventSynchronize(R.up_done[k]));
+        if (g && !direct) HP_CHECK(hipEventSynchronize(R.up_done[k]));
         double t1 = now();
         // group t - kLag's target package has landed in its pinned slot
-        if (o) HP_CHECK(hipEventSynchronize(R.down_done[ko]));
+        if (o && !direct) HP_CHECK(hipEventSynchronize(R.down_done[ko]));
         double t2 = now();
-        host_step(g, pin, o, R.pin_out + size_t(ko) * S);
+        if (!direct) host_step(g, pin, o, R.pin_out + size_t(ko) * S);
         double t3 = now();
         t_wait_up += t1 - t0;
         t_wait_down += t2 - t1;
@@ -630,30 +829,45 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
         HP_CHECK(hipStreamWaitEvent(R.up, R.down_done[k], 0));
         if (g->in_bytes || g->reads_old) {
             if (prof && !up0) up0 = ev(R.up);
-            if (g->in_bytes) HP_CHECK(hipMemcpyAsync(dev, pin, g->in_bytes, hipMemcpyHostToDevice, R.up));
-            if (g->reads_old)
-                HP_CHECK(hipMemcpyAsync(dev + S, pin + S, g->out_bytes, hipMemcpyHostToDevice,
-                                        R.up));
+            if (direct) {
+                move_rect(g->src_rect, dev, true);
+                if (g->reads_old) move_rect(g->dst_rect, dev + S, true);
+            } else {
+                if (g->in_bytes) HP_CHECK(hipMemcpyAsync(dev, pin, g->in_bytes, hipMemcpyHostToDevice, R.up));
+                if (g->reads_old)
+                    HP_CHECK(hipMemcpyAsync(dev + S, pin + S, g->out_bytes, hipMemcpyHostToDevice,
+                                            R.up));
+            }
             if (prof) up1 = ev(R.up);
         }
         HP_CHECK(hipEventRecord(R.up_done[k], R.up));
         HP_CHECK(hipStreamWaitEvent(comp, R.up_done[k], 0));
         if (unpack) HP_CHECK(hipStreamWaitEvent(comp, R.moved[g->round], 0));
         hipEvent_t k0 = prof ? ev(comp) : nullptr;
-        launch_tiles(hp.dtype,
-                     make_launch(g->split, static_cast<const costa_tile_op_t*>(hp.d_ops) + g->ord_first,
-                                 static_cast<const uint64_t*>(hp.d_work) + g->work_first,
-                                 unpack ? recv_buf : dev, dev + S, d_scalars, g->any_tr,
-                                 g->reads_old),
-                     comp);
+        if (direct)
+            launch_tiles(hp.dtype,
+                         make_launch(g->split_d, static_cast<const costa_tile_op_t*>(hp.d_ops_d) + g->ord_first_d,
+                                     static_cast<const uint64_t*>(hp.d_work_d) + g->work_first_d, dev,
+                                     dev + S, d_scalars, g->any_tr, g->reads_old),
+                         comp);
+        else
+            launch_tiles(hp.dtype,
+                         make_launch(g->split, static_cast<const costa_tile_op_t*>(hp.d_ops) + g->ord_first,
+                                     static_cast<const uint64_t*>(hp.d_work) + g->work_first,
+                                     unpack ? recv_buf : dev, dev + S, d_scalars, g->any_tr,
+                                     g->reads_old),
+                         comp);
         if (prof) kern_t.push_back({k0, ev(comp), unpack});
         HP_CHECK(hipEventRecord(R.kern_done[k], comp));
         // the pinned target slot's previous group (t - kRing) was scattered at step
         // t - kRing + kLag < t
         HP_CHECK(hipStreamWaitEvent(R.down, R.kern_done[k], 0));
         if (prof && !dn0) dn0 = ev(R.down);
-        HP_CHECK(hipMemcpyAsync(R.pin_out + size_t(k) * S, dev + S, g->out_bytes,
-                                hipMemcpyDeviceToHost, R.down));
+        if (direct)
+            move_rect(g->dst_rect, dev + S, false);
+        else
+            HP_CHECK(hipMemcpyAsync(R.pin_out + size_t(k) * S, dev + S, g->out_bytes,
+                                    hipMemcpyDeviceToHost, R.down));
         HP_CHECK(hipEventRecord(R.down_done[k], R.down));
         if (prof) dn1 = ev(R.down);
         issue_rounds(hp.rounds_after[t]);
@@ -662,9 +876,10 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
     issue_rounds(hp.rounds);  // a rank with nothing to upload still takes part in the exchange
     if (trace)
         std::fprintf(stderr,
-                     "[costa host pipe] groups %zu, %d exchange round(s), slot %zu MiB threads %d: "
+                     "[costa host pipe] groups %zu, %d exchange round(s), slot %zu MiB threads %d%s: "
                      "total %.2f ms, copies %.2f, wait-up %.2f, wait-down %.2f, issue %.2f\n",
-                     G, exchange ? hp.rounds : 0, S >> 20, host_threads(), (now() - t_begin) * 1e3,
+                     G, exchange ? hp.rounds : 0, S >> 20, host_threads(), direct ? " (direct DMA)" : "",
+                     (now() - t_begin) * 1e3,
                      t_copy * 1e3, t_wait_up * 1e3, t_wait_down * 1e3, t_issue * 1e3);
     HP_CHECK(hipStreamSynchronize(R.up));
     HP_CHECK(hipStreamSynchronize(xs));
@@ -682,6 +897,7 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
         }
     }
     st.host_groups += int64_t(G);
+    if (direct) st.host_direct++;
     if (prof) {
         float ms = 0.f;
         for (auto& x : kern_t) {

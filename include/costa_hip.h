@@ -225,6 +225,8 @@ typedef struct {
     int64_t host_groups; /* tile groups moved by the pipelined host staging */
     int64_t device_plans; /* plan-cache misses planned on the GPU (costa_hip_set_planner) */
     double plan_ms;       /* host wall time spent building plans (cache misses) */
+    int64_t host_direct;  /* host-resident calls whose buffers were page-locked: tiles moved by
+                             strided DMA between the caller's memory and HBM, no host copies */
 } costa_stats_t;
 int costa_hip_set_profiling(int on);
 int costa_hip_get_stats(costa_stats_t* out, int reset);
@@ -237,7 +239,10 @@ int costa_hip_release_caches(void);
  * the tiles move in 64 MiB groups through pinned/device slot rings: host gather -> H2D ->
  * tile kernels -> D2H -> host scatter, both copy directions at once; with several ranks the
  * host gather writes the send package, the RCCL exchange follows, and the unpack kernels'
- * output comes back the same way.  0: mirror -- every byte range the layouts span is uploaded,
+ * output comes back the same way.  When every host buffer of the call is page-locked
+ * (hipHostMalloc, or registered by the caller with hipHostRegister) the pipeline skips the host
+ * copies: each tile moves by strided DMA (hipMemcpy2DAsync) straight between the caller's memory
+ * and the device slots, both directions at once.  0: mirror -- every byte range the layouts span is uploaded,
  * the kernels run on the mirror, the target ranges are copied back.  Mode 1 falls back to 0
  * for in-place layouts and target ranges shared by two batched jobs.  Results are identical. */
 int costa_hip_set_host_staging(int mode);

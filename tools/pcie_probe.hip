@@ -199,6 +199,44 @@ int main(int argc, char** argv) {
             t.join();
             sync2();
         });
+        // strided (2D) DMA straight from / to pinned host memory: column bands of w bytes of a
+        // 2 GiB matrix with 128 KiB rows (16384 rows), one call per band: the direct-DMA staging
+        // of a host pipeline over pinned caller memory
+        char* pin2;
+        CK(hipHostMalloc(reinterpret_cast<void**>(&pin2), N, hipHostMallocDefault));
+        std::memset(pin2, 4, N);
+        for (size_t w : {size_t(1) << 10, size_t(2) << 10, size_t(4) << 10, size_t(16) << 10}) {
+            const size_t pitch = 128 << 10, h = N / pitch, calls = pitch / w;
+            std::string nm = "H2D 2D pinned, " + std::to_string(w) + " B rows x 16384";
+            timeit(nm.c_str(), D, reps, [&] {
+                for (size_t c = 0; c < calls; ++c)
+                    CK(hipMemcpy2DAsync(dA + c * h * w, w, pin + c * w, pitch, w, h, hipMemcpyHostToDevice, s1));
+                sync2();
+            });
+            nm = "D2H 2D pinned, " + std::to_string(w) + " B rows x 16384";
+            timeit(nm.c_str(), D, reps, [&] {
+                for (size_t c = 0; c < calls; ++c)
+                    CK(hipMemcpy2DAsync(pin + c * w, pitch, dC + c * h * w, w, w, h, hipMemcpyDeviceToHost, s2));
+                sync2();
+            });
+            nm = "H2D 1D pinned + D2H 2D pinned " + std::to_string(w) + " B rows, together";
+            timeit(nm.c_str(), 2 * D, reps, [&] {
+                for (size_t c = 0; c < calls; ++c) {
+                    CK(hipMemcpyAsync(dA + c * h * w, pin2 + c * h * w, h * w, hipMemcpyHostToDevice, s1));
+                    CK(hipMemcpy2DAsync(pin + c * w, pitch, dC + c * h * w, w, w, h, hipMemcpyDeviceToHost, s2));
+                }
+                sync2();
+            });
+        }
+        CK(hipHostFree(pin2));
+        {
+            const double t0 = now();
+            for (int i = 0; i < 1000; ++i)
+                CK(hipMemcpy2DAsync(dA, 2048, pin, 131072, 2048, 16, hipMemcpyHostToDevice, s1));
+            const double t1 = now();
+            sync2();
+            std::printf("hipMemcpy2DAsync issue cost (pinned, 32 KiB): %.2f us per call\n", (t1 - t0) * 1e3);
+        }
         // the pinned D2H while 16 host threads copy pinned -> pageable (the scatter) at once
         timeit("H2D pageable + D2H pinned + 16-thread host copy of 2 GiB", 2 * D, reps, [&] {
             h2d(hA, s1, 64 << 20);
