@@ -15,3 +15,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o trace --output-
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 200 rocprofv3 --pmc $c -d $O/pmc_$c -o p --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-e2e --no-extra > $O/pmc_$c.log 2>&1 || exit 1
 done
+tools/c5_pmc.sh ${1:-full}_c5pmc || exit 1
+tools/c34_prof.sh ${1:-full}_c34 || exit 1

@@ -103,7 +103,19 @@ for op, share in (("N", 0.5), ("T", 2 / 3)):
     st = os.path.join(c5, f"prof_{op}", "trace_kernel_stats.csv")
     if os.path.exists(st):
         shutil.copy(st, os.path.join(dst, f"c5{op}_trace_kernel_stats.csv"))
-for name in ("bench.json", "c5N.json", "c5T.json", "extra.json"):
+# cfg 4 / cfg 3 single-GPU slices when tools/c34_prof.sh ran as <tag>_c34
+c34 = src + "_c34"
+for n, kern, share in (("cfg4", "tile_kernel<costa::engine::(anonymous namespace)::cpx<double>", 2 / 3),
+                       ("cfg3", "tile_kernel<double", 0.5)):
+    save_pmc(os.path.join(c34, f"pmc_{n}_FETCH_SIZE"), os.path.join(c34, f"pmc_{n}_WRITE_SIZE"),
+             os.path.join(c34, f"pmc_{n}_FETCH_SIZE.log"), kern, f"pmc_{n}.json", share)
+    st = os.path.join(c34, f"prof_{n}", "trace_kernel_stats.csv")
+    if os.path.exists(st):
+        shutil.copy(st, os.path.join(dst, f"{n}_trace_kernel_stats.csv"))
+    lg = os.path.join(c34, f"prof_{n}.log")
+    if os.path.exists(lg) and line(lg):
+        json.dump(line(lg), open(os.path.join(dst, f"{n}.json"), "w"))
+for name in ("bench.json", "c5N.json", "c5T.json", "extra.json", "cfg4.json", "cfg3.json"):
     d = line(os.path.join(dst, name))
     if d:
         print(name, d["value"], d["ms_per_step"], d["roofline"]["frac"], d["roofline"]["avg_launch_ms"],
