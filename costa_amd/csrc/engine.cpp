@@ -806,10 +806,17 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         const char* s = tuning_env("COSTA_SKEW");
         return !s || std::atoi(s) != 0;
     }();
+    // r4: also destinations on the 16-byte grid whose columns start off the 64-byte one (lld not
+    // a multiple of 8 fp64 / 16 fp32 elements): the large shape's column segments then share
+    // their edge granules with the neighbouring sub-tiles.  fp64 16384^2 'T' lld + 2 / + 4
+    // 1.046 / 1.015 -> 0.855 / 0.837 ms, beta != 0 1.444 -> 1.244; fp32 lld + 4 / + 8 / + 24
+    // 0.687 / 0.620 / 0.595 -> 0.466 / 0.482 / 0.466; aligned and 64-byte-aligned ld unchanged
+    // (profiles/r4l/)
     for (size_t li = 0; skew_on && k_elems > 0 && li < ops.size(); ++li) {
         const costa_tile_op_t& op = ops[li];
-        if (cls[li] == 3 || !(op.flags & COSTA_TILE_TRANSPOSE) || (op.flags & COSTA_TILE_VEC_DST))
-            continue;
+        if (cls[li] == 3 || !(op.flags & COSTA_TILE_TRANSPOSE)) continue;
+        const bool off_granule = op.dst % 64 != 0 || (uint64_t(op.ldd) * uint64_t(E)) % 64 != 0;
+        if ((op.flags & COSTA_TILE_VEC_DST) && !off_granule) continue;
         if (op.dst % uint64_t(E) != 0 || 2 * int64_t(op.nf) * op.ns < k_elems)
             continue;
         if (cls[li] == 1) --n_med;

@@ -24,11 +24,13 @@ def main():
     costa.lib()
     comm = costa.Comm.self(0)
     es = torch.tensor([], dtype=tdt).element_size()
-    A = torch.rand(n * n, dtype=tdt, device="cuda")
-    C = torch.rand(n * n, dtype=tdt, device="cuda")
-    LA = costa.block_cyclic_layout(n, n, b, b, 1, 1, n, n, 1, 1, "R", 0, 0, A.data_ptr(), n, "C", 0,
+    pad = int(os.environ.get("COSTA_PROBE_LDPAD", "0"))  # leading-dimension padding (elements)
+    ld = n + pad
+    A = torch.rand(ld * n, dtype=tdt, device="cuda")
+    C = torch.rand(ld * n, dtype=tdt, device="cuda")
+    LA = costa.block_cyclic_layout(n, n, b, b, 1, 1, n, n, 1, 1, "R", 0, 0, A.data_ptr(), ld, "C", 0,
                                    dtype=cd)
-    LC = costa.block_cyclic_layout(n, n, b, b, 1, 1, n, n, 1, 1, "R", 0, 0, C.data_ptr(), n, "C", 0,
+    LC = costa.block_cyclic_layout(n, n, b, b, 1, 1, n, n, 1, 1, "R", 0, 0, C.data_ptr(), ld, "C", 0,
                                    dtype=cd)
     al = 0.5 if beta != 0 else 1.0
     for _ in range(3):
@@ -47,7 +49,7 @@ def main():
         extra = "".join(f"  {k} {st[k + '_ms'] / steps:.4f} ms "
                         f"{st[k + '_bytes'] / steps / (st[k + '_ms'] / steps * 1e-3) / 1e9:7.1f} GB/s"
                         for k in ("pack", "unpack"))
-    print(f"{dt} {n}^2 block {b} beta {beta} sort {os.environ.get('COSTA_LARGE_SORT', '1')}: "
+    print(f"{dt} {n}^2 ld +{pad} block {b} beta {beta} sort {os.environ.get('COSTA_LARGE_SORT', '1')}: "
           f"kernel {ms:.4f} ms {gbps:8.1f} GB/s{extra}", flush=True)
 
 

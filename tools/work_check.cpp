@@ -87,7 +87,8 @@ static std::set<uint32_t> expected_shaped(costa_dtype_t dt, const std::vector<co
         if (E == 4 && e >= big && o.src % 4 == 0) o.flags |= COSTA_TILE_VEC_SRC;
         const bool al = (o.flags & both) == both, t = o.flags & COSTA_TILE_TRANSPOSE;
         const uint32_t kind = (o.flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT;
-        if (skew_elems > 0 && e > 0 && t && !(o.flags & COSTA_TILE_VEC_DST) &&
+        const bool off_granule = o.dst % 64 != 0 || (uint64_t(o.ldd) * uint64_t(E)) % 64 != 0;
+        if (skew_elems > 0 && e > 0 && t && (!(o.flags & COSTA_TILE_VEC_DST) || off_granule) &&
             o.dst % uint64_t(E) == 0 && 2 * e >= skew_elems) {
             large.insert(o.order);
             continue;
@@ -211,11 +212,11 @@ static bool check_merge() {
             // (pieces of wavefront ops are in `ord` after tiny_first; shaped ops before)
             CHECK(area == int64_t(m) * m, "%c %d: ops cover %lld of %lld elements", op, m, (long long)area,
                   (long long)int64_t(m) * m);
-            CHECK(p->local_ops.size() > 1000 && w.tiny_first <= 2 && w.n_tiny == 0 && w.n_large > 0,
+            CHECK(p->local_ops.size() > 1000 && w.tiny_first <= 2 && w.n_tiny == 0 && w.n_large + w.n_skew > 0,
                   "%c %d: %zu tiles -> %lld shaped ops, %lld pieces", op, m, p->local_ops.size(),
                   (long long)w.tiny_first, (long long)w.n_tiny);
-            std::printf("merge %c %d: %zu tiles -> %lld op(s), %lld large sub-tiles\n", op, m,
-                        p->local_ops.size(), (long long)w.tiny_first, (long long)w.n_large);
+            std::printf("merge %c %d: %zu tiles -> %lld op(s), %lld large / %lld skew sub-tiles\n", op, m,
+                        p->local_ops.size(), (long long)w.tiny_first, (long long)w.n_large, (long long)w.n_skew);
         }
     // tiles that continue each other along s only (each strip's destination elsewhere): merged
     // they would be 24-wide strips, a third of the fp64 sub-tile, so they stay apart
