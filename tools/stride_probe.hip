@@ -1,0 +1,82 @@
+// Probe (not product): does a plain strided copy lose when the column stride is a large power
+// of two plus 64 B .. 4 KiB, as the transposes do (profiles/r4l/)?  The source and
+// destination are 16384 columns of 8192 fp64 rows (64 KiB) at a stride of 128 KiB + delta bytes;
+// a 256-thread workgroup copies 16 column segments of 1 KiB, consecutive workgroups continue down
+// the same 16 columns (tools/copy_ceiling.hip "seg 1024"), nt loads and stores.  Modes: both
+// sides strided, only the source strided (destination dense), only the destination strided.
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/stride_probe.hip -o /tmp/sp && /tmp/sp
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                               \
+    do {                                                                                    \
+        hipError_t e_ = (x);                                                                \
+        if (e_ != hipSuccess) {                                                             \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            exit(1);                                                                        \
+        }                                                                                   \
+    } while (0)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// column c, segment q (1 KiB = 64 x 16 B): element e of the segment at base + c * stride16 + q * 64 + e
+__global__ __launch_bounds__(256) void seg(const u32x4* __restrict__ a, u32x4* __restrict__ c,
+                                           long sa, long sc, long segs_per_col) {
+    const long w = blockIdx.x;
+    const long g = w / segs_per_col, q = w % segs_per_col;
+    u32x4 x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int e = u * 256 + int(threadIdx.x);
+        const long col = g * 16 + e / 64;
+        x[u] = __builtin_nontemporal_load(a + col * sa + q * 64 + e % 64);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int e = u * 256 + int(threadIdx.x);
+        const long col = g * 16 + e / 64;
+        __builtin_nontemporal_store(x[u], c + col * sc + q * 64 + e % 64);
+    }
+}
+
+int main() {
+    const long cols = 16384, col_bytes = 65536;  // 8192 fp64 rows per column, 1 GiB per side
+    const long segs = col_bytes / 1024;
+    const long max_stride = 131072 + 8192;
+    char *a, *c;
+    CK(hipMalloc(&a, cols * max_stride));
+    CK(hipMalloc(&c, cols * max_stride));
+    CK(hipMemset(a, 1, cols * max_stride));
+    CK(hipMemset(c, 0, cols * max_stride));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const long deltas[] = {0, 16, 64, 128, 256, 512, 1024, 2048, 4096, 8192};
+    for (int mode = 0; mode < 3; ++mode) {
+        for (long d : deltas) {
+            const long stride = 131072 + d;
+            const long sa = (mode == 2 ? col_bytes : stride) / 16, sc = (mode == 1 ? col_bytes : stride) / 16;
+            std::vector<float> t;
+            for (int r = 0; r < 12; ++r) {
+                CK(hipEventRecord(e0));
+                hipLaunchKernelGGL(seg, dim3(unsigned(cols / 16 * segs)), dim3(256), 0, 0,
+                                   reinterpret_cast<const u32x4*>(a), reinterpret_cast<u32x4*>(c), sa, sc, segs);
+                CK(hipEventRecord(e1));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                if (r >= 2) t.push_back(ms);
+            }
+            std::sort(t.begin(), t.end());
+            const double bytes = 2.0 * cols * col_bytes;
+            printf("%-22s stride 128 KiB + %5ld B: %.4f ms  %.2f TB/s\n",
+                   mode == 0 ? "both strided" : mode == 1 ? "source strided" : "destination strided", d,
+                   t[t.size() / 2], bytes / (t[t.size() / 2] * 1e-3) / 1e12);
+        }
+    }
+    return 0;
+}
