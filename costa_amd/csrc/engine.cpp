@@ -618,7 +618,8 @@ struct wave_knobs {  // defaults, overridable for tuning runs
                          // ms; copy lists untested under 2; profiles/r2/order/)
     int force_sq = 0;   // COSTA_FORCE_SQ=1 (tuning): transposing lists of fp64 / c64 / c128 take the
                         // square sub-tile whatever their ops' size
-    int merge = 1;      // COSTA_MERGE=0: ops that continue each other are not merged (tuning; the
+    int merge = 2;      // COSTA_MERGE=0: ops that continue each other are not merged, 1: only
+                        // ops below half a large sub-tile (r3); 2 (default): every op (tuning; the
                         // skew list always merges)
     int xcd_bands = 1;  // COSTA_XCD_BANDS=k: destination-ordered wavefront lists in 8 k column
                         // bands, k per XCD (xcd_bands); 0: off.  cfg 5 'N' 0.476 -> 0.446 ms with
@@ -682,7 +683,12 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     if (kn0.merge && ops_in.size() > 1 && few_strides(ops_in)) {
         shape_dims sh0;
         tile_shapes(dtype, any_transpose(ops_in), &sh0);
-        const int64_t half_large = int64_t(sh0.bf) * sh0.bs / 2;
+        // every op is a candidate, large ones included (r4): blocks that do not fill the
+        // sub-tiles then run as whole merged ops (16384^2 'T' on one rank: c128 80^2 / 96^2
+        // 2.919 / 2.554 -> 2.101 / 2.103 ms, fp64 96^2 0.800 -> 0.699, 100^2 0.947 -> 0.700, 80^2
+        // beta != 0 1.212 -> 1.030; filled sizes unchanged; profiles/r4s/).  COSTA_MERGE=1
+        // (tuning): small ops only, as in r3
+        const int64_t half_large = kn0.merge == 1 ? int64_t(sh0.bf) * sh0.bs / 2 : INT64_MAX;
         std::vector<costa_tile_op_t> small;
         for (const auto& op : ops_in)
             (int64_t(op.nf) * op.ns < half_large ? small : ops_merged).push_back(op);
