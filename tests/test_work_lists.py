@@ -36,6 +36,14 @@ def test_work_lists_cfg5(tmp_path):
     # merging of ops that continue each other (on by default)
     r = subprocess.run([str(exe), "merge"], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
+    # the default lists' sub-tiles cover their ops exactly once, whatever order the sorts left
+    # (destination panels, XCD groups of the skew shape, merged ragged blocks, cfg 5)
+    # and unmerged (thousands of ops per list, sorted across ops)
+    clean = {k: v for k, v in os.environ.items() if not k.startswith("COSTA_")}
+    for extra in ({}, {"COSTA_MERGE": "0", "COSTA_TUNING": "1"}):
+        r = subprocess.run([str(exe), "cover"], capture_output=True, text=True, timeout=300,
+                           env=dict(clean, **extra))
+        assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
 
 
 TUNING = {"COSTA_TINY_SORT": "0", "COSTA_FORCE_SQ": "1", "COSTA_LARGE_SORT": "0", "COSTA_XCD_BANDS": "0",

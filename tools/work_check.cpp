@@ -15,7 +15,8 @@
 //     skew shape; other ops up to kUnalignedWaveCap large sub-tiles are cut into wavefront
 //     pieces (the same checks), bigger ones stay on the large shape.
 //   run with COSTA_MERGE=0 (ops that continue each other stay apart: every op has one parent);
-//   `work_check merge` checks the merging itself.
+//   `work_check merge` checks the merging itself; `work_check cover` that the sub-tiled work items
+//   of the default lists (panels, skew XCD groups, merged ragged blocks) cover their ops exactly.
 // Prints "ok" and exits 0, or prints the first violation and exits 1.
 #include <chrono>
 #include <complex>
@@ -40,7 +41,9 @@ static std::vector<int> splits(uint64_t seed, int lo, int hi, int n) {
     return s;
 }
 
-static grid_layout<float> layout(const std::vector<int>& rs, const std::vector<int>& cs, uint64_t base) {
+template <typename T = float>
+static grid_layout<T> layout(const std::vector<int>& rs, const std::vector<int>& cs, uint64_t base,
+                             uint64_t gap = 0) {
     const int nr = int(rs.size()) - 1, nc = int(cs.size()) - 1;
     std::vector<int> own(size_t(nr) * size_t(nc), 0);
     std::vector<block_t> blocks;
@@ -48,10 +51,10 @@ static grid_layout<float> layout(const std::vector<int>& rs, const std::vector<i
     for (int i = 0; i < nr; ++i)
         for (int j = 0; j < nc; ++j) {
             const int rows = rs[size_t(i) + 1] - rs[size_t(i)], cols = cs[size_t(j) + 1] - cs[size_t(j)];
-            blocks.push_back({reinterpret_cast<void*>(base + 4 * off), rows, i, j});
-            off += (uint64_t(rows) * uint64_t(cols) + 63) / 64 * 64;
+            blocks.push_back({reinterpret_cast<void*>(base + sizeof(T) * off), rows, i, j});
+            off += (uint64_t(rows) * uint64_t(cols) + 63) / 64 * 64 + gap;
         }
-    return custom_layout<float>(nr, nc, rs.data(), cs.data(), own.data(), int(blocks.size()),
+    return custom_layout<T>(nr, nc, rs.data(), cs.data(), own.data(), int(blocks.size()),
                                 blocks.data(), 'C');
 }
 
@@ -243,6 +246,121 @@ static bool check_merge() {
     return true;
 }
 
+// the sub-tiled work items cover their ops exactly: every (op, sub-tile) of ordered[0, tiny_first)
+// once, each class's items naming only its own ops, whatever order the sorts (hint, destination
+// address, 128 KiB panels, XCD groups of the skew shape) left them in; with panels, the items walk
+// the destination panel by panel
+static bool check_cover(const std::string& name, costa_dtype_t dt, const std::vector<costa_tile_op_t>& ops,
+                        bool expect_panels = false) {
+    std::vector<costa_tile_op_t> ord;
+    std::vector<uint64_t> work;
+    const work_split w = build_work(dt, ops, ord, work, list_local);
+    shape_dims sh;
+    tile_shapes(dt, w.tr_shape, &sh);
+    const int64_t E = int64_t(dtype_size(dt));
+    CHECK(int64_t(work.size()) == w.n_large + w.n_medium + w.n_skew, "%zu work items, split %lld + %lld + %lld",
+          work.size(), (long long)w.n_large, (long long)w.n_medium, (long long)w.n_skew);
+    const int bfs[3][2] = {{w.sq ? sh.bf_q : sh.bf, w.sq ? sh.bs_q : sh.bs},
+                           {w.med_sq ? sh.bf_s : sh.bf_m, w.med_sq ? sh.bs_s : sh.bs_m},
+                           {w.skew_wide ? sh.bf_kw : sh.bf_k, w.skew_wide ? sh.bs_kw : sh.bs_k}};
+    const int64_t ends[3] = {w.n_large, w.n_large + w.n_medium, w.n_large + w.n_medium + w.n_skew};
+    std::vector<int> cls(size_t(w.tiny_first), -1);
+    std::vector<std::vector<char>> seen(size_t(w.tiny_first));
+    int64_t covered = 0, want = 0, panel_back = 0;
+    for (int64_t i = 0; i < w.tiny_first; ++i) want += int64_t(ord[size_t(i)].nf) * ord[size_t(i)].ns;
+    uint64_t last_panel = 0, lo = ~uint64_t(0);
+    for (int64_t i = 0; i < w.tiny_first; ++i) lo = std::min(lo, ord[size_t(i)].dst);
+    for (int64_t x = 0; x < int64_t(work.size()); ++x) {
+        const int c = x < ends[0] ? 0 : x < ends[1] ? 1 : 2;
+        const int bf = bfs[c][0], bs = bfs[c][1];
+        CHECK(bf > 0 && bs > 0, "item %lld in class %d without a shape", (long long)x, c);
+        const uint64_t i = work[size_t(x)] >> 32, q = work[size_t(x)] & 0xFFFFFFFFull;
+        CHECK(int64_t(i) < w.tiny_first, "item %lld names op %llu past the shaped ops", (long long)x,
+              (unsigned long long)i);
+        const costa_tile_op_t& op = ord[size_t(i)];
+        const uint64_t nbf = uint64_t((op.nf + bf - 1) / bf), n = nbf * uint64_t((op.ns + bs - 1) / bs);
+        CHECK(cls[i] == -1 || cls[i] == c, "op %llu in two classes", (unsigned long long)i);
+        cls[i] = c;
+        if (seen[i].empty()) seen[i].assign(size_t(n), 0);
+        CHECK(q < n && !seen[i][q], "op %llu sub-tile %llu (of %llu) twice or out of range", (unsigned long long)i,
+              (unsigned long long)q, (unsigned long long)n);
+        seen[i][q] = 1;
+        const int64_t f0 = int64_t(q % nbf) * bf, s0 = int64_t(q / nbf) * bs;
+        covered += std::min<int64_t>(bf, op.nf - f0) * std::min<int64_t>(bs, op.ns - s0);
+        if (expect_panels && c == 0) {  // engine.cpp build_work: 128 KiB panels of destination rows
+            const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
+            const uint64_t e = (op.dst - lo) / uint64_t(E) +uint64_t(tr ? f0 * op.ldd + s0 : s0 * op.ldd + f0);
+            const uint64_t panel = (e % uint64_t(op.ldd)) / uint64_t((int64_t(128) << 10) / E);
+            panel_back += panel < last_panel;
+            last_panel = panel;
+        }
+    }
+    CHECK(covered == want, "sub-tiles cover %lld of %lld elements", (long long)covered, (long long)want);
+    for (int64_t i = 0; i < w.tiny_first; ++i) CHECK(cls[size_t(i)] >= 0, "op %lld has no work item", (long long)i);
+    CHECK(!expect_panels || panel_back == 0,"%lld steps back to an earlier panel", (long long)panel_back);
+    std::printf("cover %s: %lld shaped ops -> %zu items (%lld large, %lld medium, %lld skew)%s\n", name.c_str(),
+                (long long)w.tiny_first, work.size(), (long long)w.n_large, (long long)w.n_medium,
+                (long long)w.n_skew, expect_panels ? ", panels" : "");
+    return true;
+}
+
+template <typename T>
+static std::unique_ptr<plan> square_plan(int m, int nb, int lld, char op) {
+    auto A = block_cyclic_layout<T>(m, m, nb, nb, 1, 1, m, m, 1, 1, 'R', 0, 0,
+                                    reinterpret_cast<T*>(uint64_t(1) << 40), lld, 'C', 0);
+    auto C = block_cyclic_layout<T>(m, m, nb, nb, 1, 1, m, m, 1, 1, 'R', 0, 0,
+                                    reinterpret_cast<T*>(uint64_t(1) << 42), lld, 'C', 0);
+    elayout ea = erase(A), ec = erase(C);
+    job j{&ea, &ec, op, {}};
+    const T one = T(1), zero = T(0);
+    std::memcpy(j.s.alpha.data(), &one, sizeof(T));
+    std::memcpy(j.s.beta.data(), &zero, sizeof(T));
+    return make_plan({j}, 0, 1);
+}
+
+static bool check_covers() {
+    using z = std::complex<double>;
+    struct g {
+        const char* name;
+        std::unique_ptr<plan> p;
+        bool panels;
+    };
+    std::vector<g> gs;
+    gs.push_back({"fp64 32768^2 256^2 'T'", square_plan<double>(32768, 256, 32768, 'T'), true});
+    gs.push_back({"fp64 16384^2 256^2 'T'", square_plan<double>(16384, 256, 16384, 'T'), false});
+    gs.push_back({"c128 32768^2 128^2 'T'", square_plan<z>(32768, 128, 32768, 'T'), true});
+    gs.push_back({"c128 8192^2 80^2 'T' (merged)", square_plan<z>(8192, 80, 8192, 'T'), false});
+    gs.push_back({"fp64 8192^2 100^2 'N' (merged)", square_plan<double>(8192, 100, 8192, 'N'), false});
+    gs.push_back({"fp32 4096^2 256^2 'T' lld 4097 (skew)", square_plan<float>(4096, 256, 4097, 'T'), false});
+    gs.push_back({"fp64 8192^2 32^2 'T' lld 8196 (skew)", square_plan<double>(8192, 32, 8196, 'T'), false});
+    {
+        // eight separate 32768 x 4096 column strips of A (no merging) into one 32768^2 C: 'T'
+        // writes 256 KiB destination columns, walked in panels across the eight ops
+        std::vector<int> rs{0, 32768}, cs;
+        for (int j = 0; j <= 8; ++j) cs.push_back(4096 * j);
+        auto A = layout<double>(rs, cs, uint64_t(1) << 40, 64);
+        auto C = block_cyclic_layout<double>(32768, 32768, 32768, 32768, 1, 1, 32768, 32768, 1, 1, 'R', 0, 0,
+                                             reinterpret_cast<double*>(uint64_t(1) << 42), 32768, 'C', 0);
+        elayout ea = erase(A), ec = erase(C);
+        job j{&ea, &ec, 'T', {}};
+        const double one = 1.0, zero = 0.0;
+        std::memcpy(j.s.alpha.data(), &one, 8);
+        std::memcpy(j.s.beta.data(), &zero, 8);
+        gs.push_back({"fp64 8 strips 32768 x 4096 'T'", make_plan({j}, 0, 1), true});
+    }
+    for (const auto& x : gs)
+        if (!check_cover(x.name, x.p->dtype, x.p->local_ops, x.panels)) return false;
+    const int n = 16384;
+    auto LA = layout(splits(0xC5A1, 8, 96, n), splits(0xC5A2, 8, 96, n), uint64_t(1) << 40);
+    auto LC = layout(splits(0xC5A3, 16, 160, n), splits(0xC5A4, 16, 160, n), uint64_t(1) << 41);
+    elayout a = erase(LA), c = erase(LC);
+    for (char op : {'N', 'T'}) {
+        auto p = plan_of(a, c, op, 1.f, 0.f);
+        if (!check_cover(std::string("cfg5 ") + op, p->dtype, p->local_ops)) return false;
+    }
+    return true;
+}
+
 // FNV-1a over the work lists of a set of geometries (cfg 5 'N' / 'T', cfg 2's 256^2 fp64 'T',
 // cfg 4's 128^2 c128 'T' with alpha / beta, 24^2 fp32 blocks that merge, fp32 with lld 4097):
 // `work_check digest` prints it, so that tests/test_work_lists.py can compare builds of the
@@ -325,6 +443,11 @@ int main(int argc, char** argv) {
         for (int k = 0; k < 5; ++k) build_work(p->dtype, p->local_ops, ord, work, list_local);
         const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / 5;
         std::printf("build_work cfg 5 'N' (%zu ops): %.2f ms\n", p->local_ops.size(), ms);
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "cover") {
+        if (!check_covers()) return 1;
+        std::printf("ok\n");
         return 0;
     }
     if (argc > 1 && std::string(argv[1]) == "merge") {
