@@ -5,11 +5,14 @@
 // the same 16 columns (tools/copy_ceiling.hip "seg 1024"), nt loads and stores.  Modes: both
 // sides strided, only the source strided (destination dense), only the destination strided.
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/stride_probe.hip -o /tmp/sp && /tmp/sp
+// `/tmp/sp strides`: both sides strided at 128 / 192 / 256 / 384 / 512 KiB (delta 0, 64 B), with
+// 1 KiB and 512-byte segments (the fp64 transposes' read segment; DESIGN §3b, fp64 32768^2)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CK(x)                                                                               \
@@ -24,26 +27,73 @@
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // column c, segment q (1 KiB = 64 x 16 B): element e of the segment at base + c * stride16 + q * 64 + e
+// SEG16: 16-byte vectors per segment (64: 1 KiB, 32: 512 B); 1024 / SEG16 columns per workgroup
+template <int SEG16>
 __global__ __launch_bounds__(256) void seg(const u32x4* __restrict__ a, u32x4* __restrict__ c,
                                            long sa, long sc, long segs_per_col) {
+    constexpr int COLS = 1024 / SEG16;
     const long w = blockIdx.x;
     const long g = w / segs_per_col, q = w % segs_per_col;
     u32x4 x[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int e = u * 256 + int(threadIdx.x);
-        const long col = g * 16 + e / 64;
-        x[u] = __builtin_nontemporal_load(a + col * sa + q * 64 + e % 64);
+        const long col = g * COLS + e / SEG16;
+        x[u] = __builtin_nontemporal_load(a + col * sa + q * SEG16 + e % SEG16);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int e = u * 256 + int(threadIdx.x);
-        const long col = g * 16 + e / 64;
-        __builtin_nontemporal_store(x[u], c + col * sc + q * 64 + e % 64);
+        const long col = g * COLS + e / SEG16;
+        __builtin_nontemporal_store(x[u], c + col * sc + q * SEG16 + e % SEG16);
     }
 }
 
-int main() {
+template <int SEG16>
+static float time_seg(const char* a, char* c, long cols, long col_bytes, long sa, long sc) {
+    const long segs = col_bytes / (SEG16 * 16);
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<float> t;
+    for (int r = 0; r < 12; ++r) {
+        CK(hipEventRecord(e0));
+        hipLaunchKernelGGL(seg<SEG16>, dim3(unsigned(cols / (1024 / SEG16) * segs)), dim3(256), 0, 0,
+                           reinterpret_cast<const u32x4*>(a), reinterpret_cast<u32x4*>(c), sa / 16, sc / 16, segs);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (r >= 2) t.push_back(ms);
+    }
+    std::sort(t.begin(), t.end());
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+    return t[t.size() / 2];
+}
+
+static int strides() {
+    const long cols = 16384, col_bytes = 65536;
+    const long max_stride = 524288 + 64;
+    char *a, *c;
+    CK(hipMalloc(&a, cols * max_stride));
+    CK(hipMalloc(&c, cols * max_stride));
+    CK(hipMemset(a, 1, cols * max_stride));
+    CK(hipMemset(c, 0, cols * max_stride));
+    const double bytes = 2.0 * cols * col_bytes;
+    for (long kib : {128, 192, 256, 384, 512})
+        for (long d : {0, 64}) {
+            const long stride = kib * 1024 + d;
+            const float m1 = time_seg<64>(a, c, cols, col_bytes, stride, stride);
+            const float m2 = time_seg<32>(a, c, cols, col_bytes, stride, stride);
+            printf("stride %3ld KiB + %2ld B: 1 KiB segments %.4f ms %.2f TB/s   512 B segments %.4f ms %.2f TB/s\n",
+                   kib, d, m1, bytes / (m1 * 1e-3) / 1e12, m2, bytes / (m2 * 1e-3) / 1e12);
+        }
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    if (argc > 1 && std::string(argv[1]) == "strides") return strides();
     const long cols = 16384, col_bytes = 65536;  // 8192 fp64 rows per column, 1 GiB per side
     const long segs = col_bytes / 1024;
     const long max_stride = 131072 + 8192;
@@ -63,7 +113,7 @@ int main() {
             std::vector<float> t;
             for (int r = 0; r < 12; ++r) {
                 CK(hipEventRecord(e0));
-                hipLaunchKernelGGL(seg, dim3(unsigned(cols / 16 * segs)), dim3(256), 0, 0,
+                hipLaunchKernelGGL(seg<64>, dim3(unsigned(cols / 16 * segs)), dim3(256), 0, 0,
                                    reinterpret_cast<const u32x4*>(a), reinterpret_cast<u32x4*>(c), sa, sc, segs);
                 CK(hipEventRecord(e1));
                 CK(hipEventSynchronize(e1));
