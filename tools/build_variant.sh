@@ -4,7 +4,7 @@
 #   tools/build_variant.sh <name> '<sed expression>' ['<sed expression>' ...]
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
-V=$ROOT/build/variants
+V=${VARIANT_DIR:-$ROOT/build/variants}  # VARIANT_DIR: a directory that travels to the GPU box
 name=$1
 shift
 rm -rf "$V/$name"

@@ -23,3 +23,10 @@ for a in "f32 16384 256 0.0" "c64 16384 256 0.0" "c128 16384 128 0.0" "c64 32768
 done
 COSTA_PROBE_LDPAD=16384 timeout -k 10 200 python3 tools/order_probe.py f32 16384 256 0.0 10 >> $O/types.txt 2>> $O/err.txt || exit 1
 COSTA_PROBE_LDPAD=49152 timeout -k 10 200 python3 tools/order_probe.py f32 16384 256 0.0 10 >> $O/types.txt 2>> $O/err.txt || exit 1
+# fp64 transposing shapes at 32768^2 and 16384^2: 128 x 64 (1 KiB read segments) and 128 x 128 / 1024 threads
+for v in f64w f64big; do
+  for n in 16384 32768; do
+    echo -n "$v " >> $O/f64_shapes.txt
+    COSTA_LIB=gpuvar/$v/lib/libcosta_amd.so timeout -k 10 200 python3 tools/order_probe.py f64 $n 256 0.0 10 >> $O/f64_shapes.txt 2>> $O/err.txt || exit 1
+  done
+done
