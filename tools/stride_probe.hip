@@ -6,7 +6,10 @@
 // sides strided, only the source strided (destination dense), only the destination strided.
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/stride_probe.hip -o /tmp/sp && /tmp/sp
 // `/tmp/sp strides`: both sides strided at 128 / 192 / 256 / 384 / 512 KiB (delta 0, 64 B), with
-// 1 KiB and 512-byte segments (the fp64 transposes' read segment; DESIGN §3b, fp64 32768^2)
+// 1 KiB and 512-byte segments (the fp64 transposes' read segment; DESIGN §3b, fp64 32768^2);
+// `/tmp/sp windows`: 1 KiB segments from each column's start against 1 KiB windows aligned to the
+// address grid, strides 128 / 256 / 384 KiB + 0 / 64 / 256 / 512 B; `/tmp/sp segsizes`: segment
+// length 512 B - 4 KiB (1024 B / 16 columns per workgroup) at strides of 128 - 384 KiB
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -72,6 +75,93 @@ static float time_seg(const char* a, char* c, long cols, long col_bytes, long sa
     return t[t.size() / 2];
 }
 
+// 1 KiB windows aligned to the address grid: window q of column col covers the 16-byte vectors of
+// [align_down(base, 1 KiB) + q KiB, + 1 KiB) inside the column (base = col * stride, the same on
+// both sides); ragged windows at each column's two ends
+__global__ __launch_bounds__(256) void win(const u32x4* __restrict__ a, u32x4* __restrict__ c, long s16,
+                                           long col16, long wins_per_col) {
+    const long w = blockIdx.x;
+    const long g = w / wins_per_col, q = w % wins_per_col;
+    u32x4 x[4];
+    long idx[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int e = u * 256 + int(threadIdx.x);
+        const long col = g * 16 + e / 64;
+        const long base = col * s16, lo = base / 64 * 64;
+        const long v = lo + q * 64 + e % 64;
+        idx[u] = (v >= base && v < base + col16) ? v : -1;
+        if (idx[u] >= 0) x[u] = __builtin_nontemporal_load(a + idx[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        if (idx[u] >= 0) __builtin_nontemporal_store(x[u], c + idx[u]);
+}
+
+static float time_win(const char* a, char* c, long cols, long col_bytes, long stride) {
+    const long wins = col_bytes / 1024 + 1;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<float> t;
+    for (int r = 0; r < 12; ++r) {
+        CK(hipEventRecord(e0));
+        hipLaunchKernelGGL(win, dim3(unsigned(cols / 16 * wins)), dim3(256), 0, 0, reinterpret_cast<const u32x4*>(a),
+                           reinterpret_cast<u32x4*>(c), stride / 16, col_bytes / 16, wins);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (r >= 2) t.push_back(ms);
+    }
+    std::sort(t.begin(), t.end());
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+    return t[t.size() / 2];
+}
+
+static int windows() {
+    const long cols = 16384, col_bytes = 65536;
+    const long max_stride = 393216 + 1024;
+    char *a, *c;
+    CK(hipMalloc(&a, cols * max_stride));
+    CK(hipMalloc(&c, cols * max_stride));
+    CK(hipMemset(a, 1, cols * max_stride));
+    CK(hipMemset(c, 0, cols * max_stride));
+    const double bytes = 2.0 * cols * col_bytes;
+    for (long kib : {128, 256, 384})
+        for (long d : {0, 64, 256, 512}) {
+            const long stride = kib * 1024 + d;
+            const float m1 = time_seg<64>(a, c, cols, col_bytes, stride, stride);
+            const float m2 = time_win(a, c, cols, col_bytes, stride);
+            printf("stride %3ld KiB + %3ld B: segments from the column start %.4f ms %.2f TB/s   1 KiB-aligned windows %.4f ms %.2f TB/s\n",
+                   kib, d, m1, bytes / (m1 * 1e-3) / 1e12, m2, bytes / (m2 * 1e-3) / 1e12);
+        }
+    return 0;
+}
+
+static int segsizes() {
+    const long cols = 16384, col_bytes = 65536;
+    const long max_stride = 393216;
+    char *a, *c;
+    CK(hipMalloc(&a, cols * max_stride));
+    CK(hipMalloc(&c, cols * max_stride));
+    CK(hipMemset(a, 1, cols * max_stride));
+    CK(hipMemset(c, 0, cols * max_stride));
+    const double bytes = 2.0 * cols * col_bytes;
+    for (long kib : {128, 160, 192, 256, 320, 384}) {
+        const long stride = kib * 1024;
+        const float m0 = time_seg<32>(a, c, cols, col_bytes, stride, stride);
+        const float m1 = time_seg<64>(a, c, cols, col_bytes, stride, stride);
+        const float m2 = time_seg<128>(a, c, cols, col_bytes, stride, stride);
+        const float m3 = time_seg<256>(a, c, cols, col_bytes, stride, stride);
+        printf("stride %3ld KiB: TB/s with 512 B / 1 / 2 / 4 KiB segments: %.2f %.2f %.2f %.2f\n", kib,
+               bytes / (m0 * 1e-3) / 1e12, bytes / (m1 * 1e-3) / 1e12, bytes / (m2 * 1e-3) / 1e12,
+               bytes / (m3 * 1e-3) / 1e12);
+    }
+    return 0;
+}
+
 static int strides() {
     const long cols = 16384, col_bytes = 65536;
     const long max_stride = 524288 + 64;
@@ -94,6 +184,8 @@ static int strides() {
 
 int main(int argc, char** argv) {
     if (argc > 1 && std::string(argv[1]) == "strides") return strides();
+    if (argc > 1 && std::string(argv[1]) == "windows") return windows();
+    if (argc > 1 && std::string(argv[1]) == "segsizes") return segsizes();
     const long cols = 16384, col_bytes = 65536;  // 8192 fp64 rows per column, 1 GiB per side
     const long segs = col_bytes / 1024;
     const long max_stride = 131072 + 8192;
