@@ -9,7 +9,8 @@
 // 1 KiB and 512-byte segments (the fp64 transposes' read segment; DESIGN §3b, fp64 32768^2);
 // `/tmp/sp windows`: 1 KiB segments from each column's start against 1 KiB windows aligned to the
 // address grid, strides 128 / 256 / 384 KiB + 0 / 64 / 256 / 512 B; `/tmp/sp segsizes`: segment
-// length 512 B - 4 KiB (1024 B / 16 columns per workgroup) at strides of 128 - 384 KiB
+// length 512 B - 4 KiB (1024 B / 16 columns per workgroup) at strides of 128 - 384 KiB;
+// `/tmp/sp three`: the three-stream C = A + C (cfg 4's reads and writes) against the copy
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -162,6 +163,58 @@ static int segsizes() {
     return 0;
 }
 
+// C = A + C over 1 KiB column segments (reads A and C, writes C: cfg 4's three streams), against
+// the two-stream copy of the same geometry: c128 16384^2 (columns of 256 KiB, dense)
+__global__ __launch_bounds__(256) void axpy_seg(const u32x4* __restrict__ a, u32x4* __restrict__ c, long s16,
+                                                long segs_per_col) {
+    const long w = blockIdx.x;
+    const long g = w / segs_per_col, q = w % segs_per_col;
+    u32x4 x[4], y[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int e = u * 256 + int(threadIdx.x);
+        const long col = g * 16 + e / 64;
+        x[u] = __builtin_nontemporal_load(a + col * s16 + q * 64 + e % 64);
+        y[u] = __builtin_nontemporal_load(c + col * s16 + q * 64 + e % 64);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int e = u * 256 + int(threadIdx.x);
+        const long col = g * 16 + e / 64;
+        __builtin_nontemporal_store(x[u] ^ y[u], c + col * s16 + q * 64 + e % 64);
+    }
+}
+
+static int three() {
+    const long cols = 16384, col_bytes = 262144;
+    char *a, *c;
+    CK(hipMalloc(&a, cols * col_bytes));
+    CK(hipMalloc(&c, cols * col_bytes));
+    CK(hipMemset(a, 1, cols * col_bytes));
+    CK(hipMemset(c, 0, cols * col_bytes));
+    const long segs = col_bytes / 1024;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<float> t;
+    for (int r = 0; r < 12; ++r) {
+        CK(hipEventRecord(e0));
+        hipLaunchKernelGGL(axpy_seg, dim3(unsigned(cols / 16 * segs)), dim3(256), 0, 0,
+                           reinterpret_cast<const u32x4*>(a), reinterpret_cast<u32x4*>(c), col_bytes / 16, segs);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (r >= 2) t.push_back(ms);
+    }
+    std::sort(t.begin(), t.end());
+    const float m3 = t[t.size() / 2];
+    const float m2 = time_seg<64>(a, c, cols, col_bytes, col_bytes, col_bytes);
+    printf("c128 16384^2 geometry, 1 KiB segments: C = A + C (3 x 4 GiB) %.4f ms %.2f TB/s; copy (2 x 4 GiB) %.4f ms %.2f TB/s\n",
+           m3, 3.0 * cols * col_bytes / (m3 * 1e-3) / 1e12, m2, 2.0 * cols * col_bytes / (m2 * 1e-3) / 1e12);
+    return 0;
+}
+
 static int strides() {
     const long cols = 16384, col_bytes = 65536;
     const long max_stride = 524288 + 64;
@@ -186,6 +239,7 @@ int main(int argc, char** argv) {
     if (argc > 1 && std::string(argv[1]) == "strides") return strides();
     if (argc > 1 && std::string(argv[1]) == "windows") return windows();
     if (argc > 1 && std::string(argv[1]) == "segsizes") return segsizes();
+    if (argc > 1 && std::string(argv[1]) == "three") return three();
     const long cols = 16384, col_bytes = 65536;  // 8192 fp64 rows per column, 1 GiB per side
     const long segs = col_bytes / 1024;
     const long max_stride = 131072 + 8192;
