@@ -520,31 +520,31 @@ void merge_adjacent(std::vector<costa_tile_op_t>& v, int64_t E, std::vector<uint
         }
 }
 
-// Small ops of a list merged (merge_adjacent), keeping a merged op only when it fills the large
+// Ops of a list merged (merge_adjacent), keeping a merged op only when it fills the large
 // shape's sub-tiles at least half along each dimension (bf x bs): a strip of one block's width
 // (nf = 24 of a 64-wide sub-tile, say, a package's tiles continuing along s) would run the large
 // shape a third full, slower than its tiles on the wavefront path (loopback unpack fp64 24^2
 // beta != 0: 1.571 against 1.412 ms); its tiles stay apart instead.
-std::vector<costa_tile_op_t> merge_small(const std::vector<costa_tile_op_t>& small, int64_t E, int bf, int bs) {
-    std::vector<costa_tile_op_t> v = small;
+std::vector<costa_tile_op_t> merge_filled(const std::vector<costa_tile_op_t>& cand, int64_t E, int bf, int bs) {
+    std::vector<costa_tile_op_t> v = cand;
     std::vector<uint32_t> root;
     merge_adjacent(v, E, &root);
-    if (v.size() == small.size()) return v;
+    if (v.size() == cand.size()) return v;
     std::vector<costa_tile_op_t> out;
-    out.reserve(small.size());
-    std::vector<char> keep(small.size(), 0);  // per root: the merged op is kept
-    std::vector<uint32_t> count(small.size(), 0);
-    for (size_t i = 0; i < small.size(); ++i) ++count[root[i]];
+    out.reserve(cand.size());
+    std::vector<char> keep(cand.size(), 0);  // per root: the merged op is kept
+    std::vector<uint32_t> count(cand.size(), 0);
+    for (size_t i = 0; i < cand.size(); ++i) ++count[root[i]];
     // v holds the surviving ops in input order, i.e. in the order of their roots
     size_t k = 0;
-    for (size_t i = 0; i < small.size(); ++i) {
+    for (size_t i = 0; i < cand.size(); ++i) {
         if (root[i] != i) continue;
         const costa_tile_op_t& m = v[k++];
         keep[i] = count[i] == 1 || (2 * int64_t(m.nf) >= bf && 2 * int64_t(m.ns) >= bs);
         if (keep[i]) out.push_back(m);
     }
-    for (size_t i = 0; i < small.size(); ++i)
-        if (!keep[root[i]]) out.push_back(small[i]);
+    for (size_t i = 0; i < cand.size(); ++i)
+        if (!keep[root[i]]) out.push_back(cand[i]);
     return out;
 }
 
@@ -673,10 +673,9 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     }();
     // (by default only for ops of at least one large sub-tile: smaller ones keep their class)
     const int mis = mis_env >= 0 ? mis_env : dtype_size(dtype) == 4 ? 2 : 0;
-    // small tiles (below half a large sub-tile) of one local matrix that continue each other in
-    // source and destination become one op (a 16384^2 'T' with 24^2 blocks on one rank: one op on
-    // the large shape instead of 466 k wavefront tiles); ops already on the large shape stay as
-    // the planner cut them
+    // tiles of one local matrix that continue each other in source and destination become one op
+    // (a 16384^2 'T' with 24^2 blocks on one rank: one op on the large shape instead of 466 k
+    // wavefront tiles)
     const wave_knobs& kn0 = knobs();
     std::vector<costa_tile_op_t> ops_merged;
     const std::vector<costa_tile_op_t>* ops_src = &ops_in;
@@ -689,13 +688,13 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         // beta != 0 1.212 -> 1.030; filled sizes unchanged; profiles/r4s/).  COSTA_MERGE=1
         // (tuning): small ops only, as in r3
         const int64_t half_large = kn0.merge == 1 ? int64_t(sh0.bf) * sh0.bs / 2 : INT64_MAX;
-        std::vector<costa_tile_op_t> small;
+        std::vector<costa_tile_op_t> cand;  // the ops that may merge (the rest: ops_merged as they are)
         for (const auto& op : ops_in)
-            (int64_t(op.nf) * op.ns < half_large ? small : ops_merged).push_back(op);
-        const size_t n_small = small.size();
-        small = merge_small(small, int64_t(dtype_size(dtype)), sh0.bf, sh0.bs);
-        if (small.size() < n_small) {
-            ops_merged.insert(ops_merged.end(), small.begin(), small.end());
+            (int64_t(op.nf) * op.ns < half_large ? cand : ops_merged).push_back(op);
+        const size_t n_cand0 = cand.size();
+        cand = merge_filled(cand, int64_t(dtype_size(dtype)), sh0.bf, sh0.bs);
+        if (cand.size() < n_cand0) {
+            ops_merged.insert(ops_merged.end(), cand.begin(), cand.end());
             ops_src = &ops_merged;
         }
     }

@@ -366,7 +366,7 @@ def test_unaligned_skew_vs_oracle(gpu, dtype, pad, ab, geo):
                          ids=["b24", "ragged-sub-pad", "b16-pad"])
 def test_merged_small_blocks_vs_oracle(gpu, dtype, trans, geo):
     """small blocks on one rank: the tiles of the local matrix continue each other on both sides
-    and merge into large-shape ops (engine.cpp merge_small); ragged last blocks, sub-matrices
+    and merge into large-shape ops (engine.cpp merge_filled); ragged last blocks, sub-matrices
     and ld padding (16-byte alignment of the merged op from its first tile only); alpha, beta !=
     0 on half the cases; bit-exact vs the oracle"""
     if trans == "C" and dtype not in (2, 3):

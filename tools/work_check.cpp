@@ -140,7 +140,7 @@ static bool check_list(const std::string& name, costa_dtype_t dt, const std::vec
         CHECK(parent.count(s.order) && shaped.count(s.order), "shaped op %lld has no shaped parent", (long long)i);
         costa_tile_op_t q = *parent[s.order];
         if (E == 4 && int64_t(q.nf) * q.ns >= big_elems(dt, ops) && q.src % 4 == 0) q.flags |= COSTA_TILE_VEC_SRC;
-        // an op merged from tiles that continue each other (merge_small / merge_adjacent, copy or
+        // an op merged from tiles that continue each other (merge_filled / merge_adjacent, copy or
         // transpose mode) starts at the tile whose hint it keeps
         const bool merged = s.src == q.src && s.dst == q.dst && s.flags == q.flags && s.lds == q.lds &&
                             s.ldd == q.ldd && s.nf >= q.nf && s.ns >= q.ns;
