@@ -10,7 +10,8 @@
 // `/tmp/sp windows`: 1 KiB segments from each column's start against 1 KiB windows aligned to the
 // address grid, strides 128 / 256 / 384 KiB + 0 / 64 / 256 / 512 B; `/tmp/sp segsizes`: segment
 // length 512 B - 4 KiB (1024 B / 16 columns per workgroup) at strides of 128 - 384 KiB;
-// `/tmp/sp three`: the three-stream C = A + C (cfg 4's reads and writes) against the copy
+// `/tmp/sp three [n]`: the three-stream C = A + C (cfg 4's reads and writes) against the copy, on
+// the c128 n^2 geometry (columns of 16 n bytes; n = 16384 by default)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -185,8 +186,8 @@ __global__ __launch_bounds__(256) void axpy_seg(const u32x4* __restrict__ a, u32
     }
 }
 
-static int three() {
-    const long cols = 16384, col_bytes = 262144;
+static int three(long n) {
+    const long cols = n, col_bytes = n * 16;
     char *a, *c;
     CK(hipMalloc(&a, cols * col_bytes));
     CK(hipMalloc(&c, cols * col_bytes));
@@ -210,8 +211,8 @@ static int three() {
     std::sort(t.begin(), t.end());
     const float m3 = t[t.size() / 2];
     const float m2 = time_seg<64>(a, c, cols, col_bytes, col_bytes, col_bytes);
-    printf("c128 16384^2 geometry, 1 KiB segments: C = A + C (3 x 4 GiB) %.4f ms %.2f TB/s; copy (2 x 4 GiB) %.4f ms %.2f TB/s\n",
-           m3, 3.0 * cols * col_bytes / (m3 * 1e-3) / 1e12, m2, 2.0 * cols * col_bytes / (m2 * 1e-3) / 1e12);
+    printf("c128 %ld^2 geometry, 1 KiB segments: C = A + C (3 x %ld MiB) %.4f ms %.2f TB/s; copy (2 x %ld MiB) %.4f ms %.2f TB/s\n",
+           n, cols * col_bytes >> 20, m3, 3.0 * cols * col_bytes / (m3 * 1e-3) / 1e12, cols * col_bytes >> 20, m2, 2.0 * cols * col_bytes / (m2 * 1e-3) / 1e12);
     return 0;
 }
 
@@ -239,7 +240,7 @@ int main(int argc, char** argv) {
     if (argc > 1 && std::string(argv[1]) == "strides") return strides();
     if (argc > 1 && std::string(argv[1]) == "windows") return windows();
     if (argc > 1 && std::string(argv[1]) == "segsizes") return segsizes();
-    if (argc > 1 && std::string(argv[1]) == "three") return three();
+    if (argc > 1 && std::string(argv[1]) == "three") return three(argc > 2 ? std::atol(argv[2]) : 16384);
     const long cols = 16384, col_bytes = 65536;  // 8192 fp64 rows per column, 1 GiB per side
     const long segs = col_bytes / 1024;
     const long max_stride = 131072 + 8192;
