@@ -3,7 +3,9 @@
 numpy arrays, pipelined staging under several slot sizes / host thread counts, plus the mirror
 scheme.  One child process per setting (the knobs are read once per process).
     python3 tools/host_pipe_probe.py            (parent)
-    python3 tools/host_pipe_probe.py child      (one measurement, knobs from the env)"""
+    python3 tools/host_pipe_probe.py child      (one measurement, knobs from the env)
+    python3 tools/host_pipe_probe.py nt         (slot sizes x COSTA_HOST_NT: streaming or cached
+                                                 stores of the gather / scatter, two passes)"""
 import json
 import os
 import subprocess
@@ -38,17 +40,21 @@ def child():
     print(json.dumps({"mode": mode, "loopback": os.environ.get("COSTA_LOOPBACK", "0"),
                       "slot_mib": os.environ.get("COSTA_HOST_SLOT_MIB", "64"),
                       "threads": os.environ.get("COSTA_HOST_THREADS", "16"),
+                      "nt": os.environ.get("COSTA_HOST_NT", "3"),
                       "ms_best": round(t * 1e3, 2), "ms_all": [round(x * 1e3, 2) for x in ts],
                       "GBps_alg": round(2 * ha.nbytes / t / 1e9, 2), "verified": ok}), flush=True)
 
 
-def main():
+def main(sweep=None):
     settings = [{"PROBE_MODE": "0"}]
     for slot, th in (("32", "16"), ("64", "16"), ("128", "16")):
         settings.append({"PROBE_MODE": "1", "COSTA_HOST_SLOT_MIB": slot, "COSTA_HOST_THREADS": th})
     # the exchange path on one GPU: every tile packed, sent to itself over RCCL and unpacked
     for mode in ("0", "1"):
         settings.append({"PROBE_MODE": mode, "COSTA_LOOPBACK": "1"})
+    if sweep == "nt":
+        settings = [{"PROBE_MODE": "1", "COSTA_HOST_SLOT_MIB": slot, "COSTA_HOST_NT": nt}
+                    for _ in range(2) for slot in ("16", "32", "64") for nt in ("3", "2", "1", "0")]
     for s in settings:
         env = dict(os.environ, COSTA_HOST_PIPE_TRACE="1", COSTA_TUNING="1", **s)
         r = subprocess.run([sys.executable, os.path.abspath(__file__), "child"], env=env,
@@ -63,4 +69,7 @@ def main():
 
 
 if __name__ == "__main__":
-    child() if len(sys.argv) > 1 and sys.argv[1] == "child" else main()
+    if len(sys.argv) > 1 and sys.argv[1] == "child":
+        child()
+    else:
+        main(sys.argv[1] if len(sys.argv) > 1 else None)
