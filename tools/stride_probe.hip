@@ -11,7 +11,8 @@
 // address grid, strides 128 / 256 / 384 KiB + 0 / 64 / 256 / 512 B; `/tmp/sp segsizes`: segment
 // length 512 B - 4 KiB (1024 B / 16 columns per workgroup) at strides of 128 - 384 KiB;
 // `/tmp/sp three [n]`: the three-stream C = A + C (cfg 4's reads and writes) against the copy, on
-// the c128 n^2 geometry (columns of 16 n bytes; n = 16384 by default)
+// the c128 n^2 geometry (columns of 16 n bytes; n = 16384 by default); `/tmp/sp runs`: runs of
+// 64 B - 1 KiB at 1 - 2x their length apart (cfg 5's access shape), copy and C = A + C
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -216,6 +217,173 @@ static int three(long n) {
     return 0;
 }
 
+// Short runs (cfg 5's access shape: ~130-byte column runs of small blocks, dense-ish): run r of
+// L bytes at r * S on both sides, one dword per lane, consecutive lanes along a run; the copy
+// (two streams) and C = A + C (three, cfg 5 'T' with beta != 0); 16 dwords per thread in flight, nt
+template <bool THREE>
+__global__ __launch_bounds__(256) void runs_k(const unsigned* __restrict__ a, unsigned* __restrict__ c, long L4,
+                                              long S4, long n) {
+    constexpr int K = 16;  // dwords per thread, all loads in flight before the stores
+    const long base = long(blockIdx.x) * 256 * K + threadIdx.x;
+    unsigned v[K];
+    long idx[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const long t = base + long(j) * 256;
+        idx[j] = t < n ? (t / L4) * S4 + t % L4 : -1;
+        if (idx[j] >= 0) v[j] = __builtin_nontemporal_load(a + idx[j]);
+    }
+    if (THREE) {
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            if (idx[j] >= 0) v[j] ^= __builtin_nontemporal_load(c + idx[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        if (idx[j] >= 0) __builtin_nontemporal_store(v[j], c + idx[j]);
+}
+
+// the same C = A + C with A read as 16-byte vectors (aligned runs: the upper bound of wider source
+// loads) and C read and written as dwords
+__global__ __launch_bounds__(256) void runs_wide_a(const u32x4* __restrict__ a, unsigned* __restrict__ c, long L4,
+                                                   long S4, long n) {
+    constexpr int K = 16;
+    const long base = long(blockIdx.x) * 256 * K + threadIdx.x;
+    unsigned v[K];
+    long idx[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const long t = base + long(j) * 256;
+        idx[j] = t < n ? (t / L4) * S4 + t % L4 : -1;
+    }
+    // A: 4 of this thread's dwords (j = 4q .. 4q+3 are 256 dwords apart) come from one vector
+    // at the position of dword 4q's lane group: re-map so that lane l of pass q loads vector l
+#pragma unroll
+    for (int q = 0; q < K / 4; ++q) {
+        const long t4 = (long(blockIdx.x) * 256 * K) / 4 + q * 256 + threadIdx.x;  // vector index
+        const long e = t4 * 4;                                                     // first dword
+        const long i = e < n ? (e / L4) * S4 + e % L4 : -1;
+        u32x4 x = {0, 0, 0, 0};
+        if (i >= 0) x = __builtin_nontemporal_load(a + i / 4);
+        v[4 * q] = x[0];
+        v[4 * q + 1] = x[1];
+        v[4 * q + 2] = x[2];
+        v[4 * q + 3] = x[3];
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        if (idx[j] >= 0) v[j] ^= __builtin_nontemporal_load(c + idx[j]);
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        if (idx[j] >= 0) __builtin_nontemporal_store(v[j], c + idx[j]);
+}
+
+// C = A + C with every stream in 16-byte vectors, C's runs OFF bytes past the 16-byte grid
+// (unaligned vector loads and stores: cfg 5's destination runs start on any dword)
+typedef unsigned u32x4u __attribute__((ext_vector_type(4), aligned(4)));
+template <int OFF>
+__global__ __launch_bounds__(256) void runs_x4(const u32x4* __restrict__ a, unsigned* __restrict__ c, long L16,
+                                               long S16, long n16) {
+    constexpr int K = 4;
+    const long base = long(blockIdx.x) * 256 * K + threadIdx.x;
+    u32x4 v[K];
+    long idx[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const long t = base + long(j) * 256;
+        idx[j] = t < n16 ? (t / L16) * S16 + t % L16 : -1;
+        if (idx[j] >= 0) v[j] = __builtin_nontemporal_load(a + idx[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        if (idx[j] >= 0) {
+            const u32x4u* p = reinterpret_cast<const u32x4u*>(reinterpret_cast<const char*>(c) + idx[j] * 16 + OFF);
+            v[j] ^= *p;
+        }
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        if (idx[j] >= 0) *reinterpret_cast<u32x4u*>(reinterpret_cast<char*>(c) + idx[j] * 16 + OFF) = v[j];
+}
+
+template <int OFF>
+static float time_x4(const char* a, char* c, long L, long S, long bytes) {
+    const long n16 = bytes / 16;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<float> t;
+    for (int r = 0; r < 12; ++r) {
+        CK(hipEventRecord(e0));
+        hipLaunchKernelGGL(runs_x4<OFF>, dim3(unsigned((n16 + 1023) / 1024)), dim3(256), 0, 0,
+                           reinterpret_cast<const u32x4*>(a), reinterpret_cast<unsigned*>(c), L / 16, S / 16, n16);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (r >= 2) t.push_back(ms);
+    }
+    std::sort(t.begin(), t.end());
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+    return t[t.size() / 2];
+}
+
+static int runs() {
+    const long bytes = 1L << 30;  // moved per stream
+    const long max_span = bytes * 4;
+    char *a, *c;
+    CK(hipMalloc(&a, max_span));
+    CK(hipMalloc(&c, max_span));
+    CK(hipMemset(a, 1, max_span));
+    CK(hipMemset(c, 0, max_span));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (long L : {64, 128, 192, 256, 1024})
+        for (long S : {L, L * 3 / 2, L * 2}) {
+            const long n = bytes / 4;
+            float med[2];
+            for (int three = 0; three < 2; ++three) {
+                std::vector<float> t;
+                for (int r = 0; r < 12; ++r) {
+                    CK(hipEventRecord(e0));
+                    if (three)
+                        hipLaunchKernelGGL(runs_k<true>, dim3(unsigned((n + 4095) / 4096)), dim3(256), 0, 0,
+                                           reinterpret_cast<const unsigned*>(a), reinterpret_cast<unsigned*>(c), L / 4, S / 4, n);
+                    else
+                        hipLaunchKernelGGL(runs_k<false>, dim3(unsigned((n + 4095) / 4096)), dim3(256), 0, 0,
+                                           reinterpret_cast<const unsigned*>(a), reinterpret_cast<unsigned*>(c), L / 4, S / 4, n);
+                    CK(hipEventRecord(e1));
+                    CK(hipEventSynchronize(e1));
+                    float ms;
+                    CK(hipEventElapsedTime(&ms, e0, e1));
+                    if (r >= 2) t.push_back(ms);
+                }
+                std::sort(t.begin(), t.end());
+                med[three] = t[t.size() / 2];
+            }
+            std::vector<float> tw;
+            for (int r = 0; r < 12; ++r) {
+                CK(hipEventRecord(e0));
+                hipLaunchKernelGGL(runs_wide_a, dim3(unsigned((n + 4095) / 4096)), dim3(256), 0, 0,
+                                   reinterpret_cast<const u32x4*>(a), reinterpret_cast<unsigned*>(c), L / 4, S / 4, n);
+                CK(hipEventRecord(e1));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                if (r >= 2) tw.push_back(ms);
+            }
+            std::sort(tw.begin(), tw.end());
+            const float mw = tw[tw.size() / 2];
+            const float x0 = time_x4<0>(a, c, L, S, bytes), x4 = time_x4<4>(a, c, L, S, bytes);
+            printf("runs of %4ld B every %4ld B: copy %.2f TB/s   C = A + C dwords %.2f TB/s, A as 16 B %.2f, all 16 B %.2f, "
+                   "C 4 B off the grid %.2f\n",
+                   L, S, 2.0 * bytes / (med[0] * 1e-3) / 1e12, 3.0 * bytes / (med[1] * 1e-3) / 1e12,
+                   3.0 * bytes / (mw * 1e-3) / 1e12, 3.0 * bytes / (x0 * 1e-3) / 1e12, 3.0 * bytes / (x4 * 1e-3) / 1e12);
+        }
+    return 0;
+}
+
 static int strides() {
     const long cols = 16384, col_bytes = 65536;
     const long max_stride = 524288 + 64;
@@ -241,6 +409,7 @@ int main(int argc, char** argv) {
     if (argc > 1 && std::string(argv[1]) == "windows") return windows();
     if (argc > 1 && std::string(argv[1]) == "segsizes") return segsizes();
     if (argc > 1 && std::string(argv[1]) == "three") return three(argc > 2 ? std::atol(argv[2]) : 16384);
+    if (argc > 1 && std::string(argv[1]) == "runs") return runs();
     const long cols = 16384, col_bytes = 65536;  // 8192 fp64 rows per column, 1 GiB per side
     const long segs = col_bytes / 1024;
     const long max_stride = 131072 + 8192;
