@@ -1,5 +1,6 @@
 """Child process of test_gpu_loopback.py (run with COSTA_LOOPBACK=1 or 2): every single-rank
-golden case and a 12288^2 fp64 'T' case go through PACK -> ncclSend/ncclRecv to self -> UNPACK
+golden case, a 12288^2 fp64 'T' case and a 6144^2 alpha, beta one with 80^2 blocks (several
+exchange rounds, merged tiles) go through PACK -> ncclSend/ncclRecv to self -> UNPACK
 (mode 2: half of the tiles, the rest through the concurrent LOCAL launch), then a loop of
 stream-ordered async transforms with A updated on torch's stream between them, then the golden
 cases and a 3000 x 2500 'T' alpha/beta case from host memory through both host staging schemes
@@ -55,6 +56,20 @@ def main():
     torch.cuda.synchronize()
     if not torch.equal(Cm.view(m, m), A.view(m, m).t()):
         bad.append(f"{m}^2 fp64 T")
+    # alpha, beta through several exchange rounds (a 300 MB package: 4 rounds) with 80^2 blocks,
+    # ragged at the edge, whose tiles merge inside each round's pack and unpack lists
+    m2 = 6144
+    rng2 = np.random.default_rng(11)
+    a2 = rng2.standard_normal(m2 * m2)
+    c2 = rng2.standard_normal(m2 * m2)
+    A2, C2 = torch.from_numpy(a2).cuda(), torch.from_numpy(c2).cuda()
+    LA2 = costa.block_cyclic_layout(m2, m2, 80, 80, 1, 1, m2, m2, 1, 1, "R", 0, 0, A2.data_ptr(), m2, "C", 0)
+    LC2 = costa.block_cyclic_layout(m2, m2, 80, 80, 1, 1, m2, m2, 1, 1, "R", 0, 0, C2.data_ptr(), m2, "C", 0)
+    costa.transform(LA2, LC2, comm, "T", -0.75, 1.5)
+    exp2 = 1.5 * c2 + -0.75 * a2.reshape(m2, m2).T.copy().reshape(-1)
+    if not np.array_equal(C2.cpu().numpy().view(np.uint64), exp2.view(np.uint64)):
+        bad.append(f"{m2}^2 fp64 T alpha beta 80^2 blocks")
+    del A2, C2
     # stream-ordered: A changes on torch's stream between queued transforms
     s = torch.cuda.current_stream()
     for k in range(4):
