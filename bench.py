@@ -416,8 +416,10 @@ def copy_ceiling(src, dst, col_bytes: int, reps: int = 20):
     this box, in this process, after the timed region (src -> dst, both device buffers of the
     workload; dst is overwritten).  costa_amd/lib/libcosta_ceiling.so (costa_amd/csrc/
     ceiling.hip): kind 0 hipMemcpyDtoD, kind 1 the strided nt copy of 1 KiB column segments
-    (16 columns per 256-thread workgroup, DESIGN §3a's fastest copy of these bytes), kind 2 a flat
-    nt copy of 16 KiB chunks.  Median of `reps` HIP-event-timed repetitions each; bytes counted
+    (16 columns per 256-thread workgroup, 4 vectors per thread), kind 2 a flat nt copy of 16 KiB
+    chunks, kind 3 a flat nt copy of 1 KiB per 64-thread workgroup and kind 4 the strided copy
+    with 4 columns per workgroup, both one vector per thread (r4: the fastest copies of these
+    bytes, profiles/r4zj/).  Median of `reps` HIP-event-timed repetitions each; bytes counted
     like the transform's (read + write)."""
     import ctypes as C
     import statistics
@@ -427,7 +429,8 @@ def copy_ceiling(src, dst, col_bytes: int, reps: int = 20):
                   C.POINTER(C.c_float)]
     nbytes = src.numel() * src.element_size()
     out = {}
-    for kind, name in ((0, "hipMemcpyDtoD"), (1, "strided_nt_1KiB_segments"), (2, "flat_nt_16KiB")):
+    for kind, name in ((0, "hipMemcpyDtoD"), (1, "strided_nt_1KiB_segments"), (2, "flat_nt_16KiB"),
+                       (3, "flat_nt_1KiB_per_wave"), (4, "strided_nt_1KiB_segments_1vec")):
         ms = (C.c_float * reps)()
         rc = f(kind, src.data_ptr(), dst.data_ptr(), nbytes, col_bytes, reps, ms)
         if rc != 0:

@@ -11,6 +11,11 @@
 //           nontemporal 16-byte loads and stores.  This is the fastest copy of cfg 2's bytes
 //           measured on MI355X (tools/copy_ceiling.hip "seg 1024 nt/nt").
 //   kind 2  flat copy, one 16 KiB chunk per 256-thread workgroup, nontemporal loads and stores
+//   kind 3  flat copy, one 1 KiB chunk per 64-thread workgroup (one 16-byte vector per thread)
+//   kind 4  the strided segment copy of kind 1 with one vector per thread: a 256-thread
+//           workgroup copies 4 columns' 1 KiB segments.  Kinds 3 and 4 keep fewer loads in flight
+//           per thread (1 against 4) and ran 6.6-6.7 TB/s against kind 1's 6.2-6.3 on MI355X
+//           (profiles/r4zj/)
 //
 // costa_ceiling_copy_ms runs `reps` timed repetitions (HIP events on its own stream) after one
 // untimed one and writes every repetition's milliseconds to ms_out[0..reps).  Returns 0, or a
@@ -59,19 +64,37 @@ __global__ __launch_bounds__(kThreads) void flat_copy(const u32x4* __restrict__ 
         __builtin_nontemporal_store(x[u], c + base + u * kThreads + threadIdx.x);
 }
 
+// kinds 3 and 4: one 16-byte vector per thread
+__global__ __launch_bounds__(64) void flat_copy_1k(const u32x4* __restrict__ a, u32x4* __restrict__ c) {
+    const long i = long(blockIdx.x) * 64 + threadIdx.x;
+    __builtin_nontemporal_store(__builtin_nontemporal_load(a + i), c + i);
+}
+
+constexpr int kSegs1 = 4;  // kind 4: columns per 256-thread workgroup
+__global__ __launch_bounds__(kThreads) void seg_copy_1(const u32x4* __restrict__ a, u32x4* __restrict__ c,
+                                                       long col16, long segs_per_col) {
+    const long w = blockIdx.x;
+    const long g = w / segs_per_col, q = w % segs_per_col;
+    const int e = int(threadIdx.x);
+    const long i = (g * kSegs1 + e / kLanesPerSeg) * col16 + q * kLanesPerSeg + e % kLanesPerSeg;
+    __builtin_nontemporal_store(__builtin_nontemporal_load(a + i), c + i);
+}
+
 }  // namespace
 
 extern "C" int costa_ceiling_copy_ms(int kind, const void* src, void* dst, uint64_t bytes,
                                      uint64_t col_bytes, int reps, float* ms_out) {
     if (!src || !dst || !ms_out || reps <= 0 || bytes == 0 || bytes % (kSegs * kSegBytes))
         return -1;
-    const long grid = long(bytes / (kSegs * kSegBytes));
-    if (kind == 1) {
+    long grid = long(bytes / (kSegs * kSegBytes));
+    if (kind == 1 || kind == 4) {
         // whole 16-column groups of whole 1 KiB segments only: no tail handling needed
         if (col_bytes == 0 || col_bytes % kSegBytes || bytes % (kSegs * col_bytes)) return -1;
-    } else if (kind != 0 && kind != 2) {
+    } else if (kind != 0 && kind != 2 && kind != 3) {
         return -1;
     }
+    if (kind == 3) grid = long(bytes / kSegBytes);            // one 1 KiB chunk per workgroup
+    if (kind == 4) grid = long(bytes / (kSegs1 * kSegBytes));  // four 1 KiB segments per workgroup
     if (grid > 0x7fffffffL) return -1;
     hipStream_t s;
     hipEvent_t e0, e1;
@@ -84,8 +107,12 @@ extern "C" int costa_ceiling_copy_ms(int kind, const void* src, void* dst, uint6
         if (kind == 0) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s);
         if (kind == 1)
             hipLaunchKernelGGL(seg_copy, dim3(unsigned(grid)), dim3(kThreads), 0, s, a, c, col16, spc);
-        else
+        else if (kind == 2)
             hipLaunchKernelGGL(flat_copy, dim3(unsigned(grid)), dim3(kThreads), 0, s, a, c);
+        else if (kind == 3)
+            hipLaunchKernelGGL(flat_copy_1k, dim3(unsigned(grid)), dim3(64), 0, s, a, c);
+        else
+            hipLaunchKernelGGL(seg_copy_1, dim3(unsigned(grid)), dim3(kThreads), 0, s, a, c, col16, spc);
         return hipGetLastError();
     };
     int rc = 0;

@@ -12,7 +12,8 @@
 // length 512 B - 4 KiB (1024 B / 16 columns per workgroup) at strides of 128 - 384 KiB;
 // `/tmp/sp three [n]`: the three-stream C = A + C (cfg 4's reads and writes) against the copy, on
 // the c128 n^2 geometry (columns of 16 n bytes; n = 16384 by default); `/tmp/sp runs`: runs of
-// 64 B - 1 KiB at 1 - 2x their length apart (cfg 5's access shape), copy and C = A + C
+// 64 B - 1 KiB at 1 - 2x their length apart (cfg 5's access shape), copy and C = A + C;
+// `/tmp/sp inflight`: cfg 2's copy ceiling under other workgroup sizes and column counts
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -384,6 +385,78 @@ static int runs() {
     return 0;
 }
 
+// the strided nt copy with more bytes in flight per workgroup: NT threads, COLS column segments of
+// 1 KiB per workgroup, U 16-byte vectors per thread (U = COLS * 64 / NT), consecutive workgroups
+// continuing down the same columns
+template <int NT, int COLS>
+__global__ __launch_bounds__(NT) void segw(const u32x4* __restrict__ a, u32x4* __restrict__ c, long s16,
+                                          long segs_per_col) {
+    constexpr int U = COLS * 64 / NT;
+    const long w = blockIdx.x;
+    const long g = w / segs_per_col, q = w % segs_per_col;
+    u32x4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int e = u * NT + int(threadIdx.x);
+        x[u] = __builtin_nontemporal_load(a + (g * COLS + e / 64) * s16 + q * 64 + e % 64);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int e = u * NT + int(threadIdx.x);
+        __builtin_nontemporal_store(x[u], c + (g * COLS + e / 64) * s16 + q * 64 + e % 64);
+    }
+}
+
+template <int NT, int COLS>
+static float time_segw(const char* a, char* c, long cols, long col_bytes) {
+    const long segs = col_bytes / 1024;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<float> t;
+    for (int r = 0; r < 12; ++r) {
+        CK(hipEventRecord(e0));
+        hipLaunchKernelGGL((segw<NT, COLS>), dim3(unsigned(cols / COLS * segs)), dim3(NT), 0, 0,
+                           reinterpret_cast<const u32x4*>(a), reinterpret_cast<u32x4*>(c), col_bytes / 16, segs);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (r >= 2) t.push_back(ms);
+    }
+    std::sort(t.begin(), t.end());
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+    return t[t.size() / 2];
+}
+
+// cfg 2's bytes (16384 columns of 128 KiB, 2 GiB per side) under several workgroup shapes
+static int inflight() {
+    const long cols = 16384, col_bytes = 131072;
+    char *a, *c;
+    CK(hipMalloc(&a, cols * col_bytes));
+    CK(hipMalloc(&c, cols * col_bytes));
+    CK(hipMemset(a, 1, cols * col_bytes));
+    CK(hipMemset(c, 0, cols * col_bytes));
+    const double bytes = 2.0 * cols * col_bytes;
+    auto show = [&](const char* name, float ms) {
+        printf("%-36s %.4f ms %.2f TB/s\n", name, ms, bytes / (ms * 1e-3) / 1e12);
+    };
+    for (int rep = 0; rep < 2; ++rep) {
+        show("256 threads, 16 columns (shipped ceiling)", time_segw<256, 16>(a, c, cols, col_bytes));
+        show("64 threads, 1 column (U 1)", time_segw<64, 1>(a, c, cols, col_bytes));
+        show("256 threads, 4 columns (U 1)", time_segw<256, 4>(a, c, cols, col_bytes));
+        show("512 threads, 8 columns (U 1)", time_segw<512, 8>(a, c, cols, col_bytes));
+        show("1024 threads, 16 columns (U 1)", time_segw<1024, 16>(a, c, cols, col_bytes));
+        show("64 threads, 2 columns (U 2)", time_segw<64, 2>(a, c, cols, col_bytes));
+        show("256 threads, 8 columns (U 2)", time_segw<256, 8>(a, c, cols, col_bytes));
+        show("512 threads, 16 columns (U 2)", time_segw<512, 16>(a, c, cols, col_bytes));
+        show("1024 threads, 32 columns (U 2)", time_segw<1024, 32>(a, c, cols, col_bytes));
+        show("512 threads, 64 columns (U 8)", time_segw<512, 64>(a, c, cols, col_bytes));
+    }
+    return 0;
+}
+
 static int strides() {
     const long cols = 16384, col_bytes = 65536;
     const long max_stride = 524288 + 64;
@@ -410,6 +483,7 @@ int main(int argc, char** argv) {
     if (argc > 1 && std::string(argv[1]) == "segsizes") return segsizes();
     if (argc > 1 && std::string(argv[1]) == "three") return three(argc > 2 ? std::atol(argv[2]) : 16384);
     if (argc > 1 && std::string(argv[1]) == "runs") return runs();
+    if (argc > 1 && std::string(argv[1]) == "inflight") return inflight();
     const long cols = 16384, col_bytes = 65536;  // 8192 fp64 rows per column, 1 GiB per side
     const long segs = col_bytes / 1024;
     const long max_stride = 131072 + 8192;
