@@ -493,34 +493,10 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
     const int c0 = int(threadIdx.x) / S::LPC;
     const int nf_lane = FULL ? V : tf - lf;  // elements of this lane's strip inside the tile
     vec<T> x[S::PL];
-    constexpr int kStagePipe = 0;  // (tuning builds) staged loads in flight per thread, 0: all
-    bool staged = false;           // the pipelined path has filled the LDS tile already
-    if constexpr (FULL && kStagePipe > 0 && kStagePipe < S::PL) {
-        if ((flags & COSTA_TILE_TRANSPOSE) && kind != COSTA_SCALE_AXPBY) {
 #pragma unroll
-            for (int k = 0; k < S::PL; ++k) {
-                vload(x[k], src + (c0 + k * S::CPP) * lds + lf, V, true);
-                if (k >= kStagePipe) {
-                    raw16 r;
-                    __builtin_memcpy(&r, &x[k - kStagePipe], 16);
-                    *reinterpret_cast<raw16*>(tile + (c0 + (k - kStagePipe) * S::CPP) * P + lf) = r;
-                }
-            }
-#pragma unroll
-            for (int k = S::PL - kStagePipe; k < S::PL; ++k) {
-                raw16 r;
-                __builtin_memcpy(&r, &x[k], 16);
-                *reinterpret_cast<raw16*>(tile + (c0 + k * S::CPP) * P + lf) = r;
-            }
-            staged = true;
-        }
-    }
-    if (!staged) {
-#pragma unroll
-        for (int k = 0; k < S::PL; ++k) {
-            const int s = c0 + k * S::CPP;
-            if (FULL || (nf_lane > 0 && s < ts)) vload(x[k], src + s * lds + lf, nf_lane, vs);
-        }
+    for (int k = 0; k < S::PL; ++k) {
+        const int s = c0 + k * S::CPP;
+        if (FULL || (nf_lane > 0 && s < ts)) vload(x[k], src + s * lds + lf, nf_lane, vs);
     }
 
     if (!(flags & COSTA_TILE_TRANSPOSE)) {
@@ -602,15 +578,13 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
             if (unit(k, f, sb, n)) vload(old[k], dst + f * ldd + sb, n, vd);
         }
     }
-    if (!staged) {
 #pragma unroll
-        for (int k = 0; k < S::PL; ++k) {
-            const int s = c0 + k * S::CPP;
-            if (FULL || (nf_lane > 0 && s < ts)) {  // partial strips: the tail is junk, never stored
-                raw16 r;
-                __builtin_memcpy(&r, &x[k], 16);
-                *reinterpret_cast<raw16*>(tile + s * P + lf) = r;
-            }
+    for (int k = 0; k < S::PL; ++k) {
+        const int s = c0 + k * S::CPP;
+        if (FULL || (nf_lane > 0 && s < ts)) {  // partial strips: the tail is junk, never stored
+            raw16 r;
+            __builtin_memcpy(&r, &x[k], 16);
+            *reinterpret_cast<raw16*>(tile + s * P + lf) = r;
         }
     }
     __syncthreads();
