@@ -13,7 +13,8 @@
 // `/tmp/sp three [n]`: the three-stream C = A + C (cfg 4's reads and writes) against the copy, on
 // the c128 n^2 geometry (columns of 16 n bytes; n = 16384 by default); `/tmp/sp runs`: runs of
 // 64 B - 1 KiB at 1 - 2x their length apart (cfg 5's access shape), copy and C = A + C;
-// `/tmp/sp inflight`: cfg 2's copy ceiling under other workgroup sizes and column counts
+// `/tmp/sp inflight`: cfg 2's copy ceiling under other workgroup sizes and column counts;
+// `/tmp/sp segu`: segment length against loads in flight per thread
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -457,6 +458,72 @@ static int inflight() {
     return 0;
 }
 
+// segw with SEGB-byte segments (SEGB / 16 lanes per column)
+template <int NT, int COLS, int SEGB>
+__global__ __launch_bounds__(NT) void segv(const u32x4* __restrict__ a, u32x4* __restrict__ c, long s16,
+                                          long segs_per_col) {
+    constexpr int L = SEGB / 16, U = COLS * L / NT;
+    const long w = blockIdx.x;
+    const long g = w / segs_per_col, q = w % segs_per_col;
+    u32x4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int e = u * NT + int(threadIdx.x);
+        x[u] = __builtin_nontemporal_load(a + (g * COLS + e / L) * s16 + q * L + e % L);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int e = u * NT + int(threadIdx.x);
+        __builtin_nontemporal_store(x[u], c + (g * COLS + e / L) * s16 + q * L + e % L);
+    }
+}
+template <int NT, int COLS, int SEGB>
+static float time_segv(const char* a, char* c, long cols, long col_bytes) {
+    const long segs = col_bytes / SEGB;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<float> t;
+    for (int r = 0; r < 12; ++r) {
+        CK(hipEventRecord(e0));
+        hipLaunchKernelGGL((segv<NT, COLS, SEGB>), dim3(unsigned(cols / COLS * segs)), dim3(NT), 0, 0,
+                           reinterpret_cast<const u32x4*>(a), reinterpret_cast<u32x4*>(c), col_bytes / 16, segs);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (r >= 2) t.push_back(ms);
+    }
+    std::sort(t.begin(), t.end());
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+    return t[t.size() / 2];
+}
+// segment length against loads per thread on cfg 2's bytes
+static int segu() {
+    const long cols = 16384, col_bytes = 131072;
+    char *a, *c;
+    CK(hipMalloc(&a, cols * col_bytes));
+    CK(hipMalloc(&c, cols * col_bytes));
+    CK(hipMemset(a, 1, cols * col_bytes));
+    CK(hipMemset(c, 0, cols * col_bytes));
+    const double bytes = 2.0 * cols * col_bytes;
+    auto show = [&](const char* name, float ms) {
+        printf("%-44s %.4f ms %.2f TB/s\n", name, ms, bytes / (ms * 1e-3) / 1e12);
+    };
+    for (int rep = 0; rep < 2; ++rep) {
+        show("256 B segments, 256 threads, 16 cols (U 1)", time_segv<256, 16, 256>(a, c, cols, col_bytes));
+        show("512 B segments, 256 threads, 8 cols (U 1)", time_segv<256, 8, 512>(a, c, cols, col_bytes));
+        show("1 KiB segments, 256 threads, 4 cols (U 1)", time_segv<256, 4, 1024>(a, c, cols, col_bytes));
+        show("256 B segments, 256 threads, 32 cols (U 2)", time_segv<256, 32, 256>(a, c, cols, col_bytes));
+        show("512 B segments, 256 threads, 16 cols (U 2)", time_segv<256, 16, 512>(a, c, cols, col_bytes));
+        show("512 B segments, 1024 threads, 64 cols (U 2)", time_segv<1024, 64, 512>(a, c, cols, col_bytes));
+        show("512 B segments, 512 threads, 64 cols (U 4)", time_segv<512, 64, 512>(a, c, cols, col_bytes));
+        show("512 B segments, 512 threads, 128 cols (U 8)", time_segv<512, 128, 512>(a, c, cols, col_bytes));
+    }
+    return 0;
+}
+
 static int strides() {
     const long cols = 16384, col_bytes = 65536;
     const long max_stride = 524288 + 64;
@@ -484,6 +551,7 @@ int main(int argc, char** argv) {
     if (argc > 1 && std::string(argv[1]) == "three") return three(argc > 2 ? std::atol(argv[2]) : 16384);
     if (argc > 1 && std::string(argv[1]) == "runs") return runs();
     if (argc > 1 && std::string(argv[1]) == "inflight") return inflight();
+    if (argc > 1 && std::string(argv[1]) == "segu") return segu();
     const long cols = 16384, col_bytes = 65536;  // 8192 fp64 rows per column, 1 GiB per side
     const long segs = col_bytes / 1024;
     const long max_stride = 131072 + 8192;
