@@ -123,11 +123,7 @@ def run_ranks(cmd, budget_s: float = RUN_BUDGET_S, n_gpus: int = 0) -> int:
                 sys.stderr.write(line)
                 sys.stderr.flush()
 
-    t = threading.Thread(target=relay, daemon=True)
-    t.start()
-    try:
-        rc = p.wait(timeout=budget_s)
-    except subprocess.TimeoutExpired:
+    def kill_group():
         for sig, grace in ((signal.SIGTERM, 10.0), (signal.SIGKILL, 5.0)):
             try:
                 os.killpg(p.pid, sig)
@@ -138,17 +134,42 @@ def run_ranks(cmd, budget_s: float = RUN_BUDGET_S, n_gpus: int = 0) -> int:
                 break
             except subprocess.TimeoutExpired:
                 continue
+
+    # the child group is its own session, so a signal meant for this process (the driver's
+    # timeout, Ctrl-C) does not reach the ranks: pass it on, then exit 128 + signal
+    def forward(signum, frame):
+        kill_group()
+        os._exit(128 + signum)
+
+    prev = {}
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        try:
+            prev[sig] = signal.signal(sig, forward)
+        except ValueError:  # not the main thread: the ranks' own watchdog stays the backstop
+            pass
+    t = threading.Thread(target=relay, daemon=True)
+    t.start()
+    try:
+        rc = p.wait(timeout=budget_s)
+    except subprocess.TimeoutExpired:
+        kill_group()
         t.join(timeout=5.0)
         print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": n_gpus,
                           "error": "timeout", "budget_s": budget_s,
                           "last_phase": {str(k): v for k, v in sorted(last.items())}}),
               flush=True)
         return 124
+    finally:
+        for sig, h in prev.items():
+            signal.signal(sig, h)
     t.join(timeout=5.0)
     return rc
 
 
 _last_phase = ["start"]
+# rank 0's result line as far as it is measured: the watchdog prints it (with the error) when a
+# later phase hangs, so a hang after the headline measurement still reports the headline
+_partial_line: dict = {}
 
 
 def phase(rank: int, msg: str):
@@ -169,9 +190,11 @@ def start_watchdog(rank: int, world: int, budget_s: float):
         msg = f"watchdog: {budget_s:.0f} s budget exceeded in phase '{_last_phase[0]}'"
         print(f"[bench rank {rank}] {msg}", file=sys.stderr, flush=True)
         if rank == 0:
-            print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world,
-                              "error": "timeout", "budget_s": budget_s,
-                              "last_phase": {"0": _last_phase[0]}}), flush=True)
+            line = {"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world}
+            line.update(_partial_line)
+            line.update({"error": "timeout", "budget_s": budget_s,
+                         "last_phase": {"0": _last_phase[0]}})
+            print(json.dumps(line), flush=True)
         os._exit(124)
 
     t = threading.Timer(budget_s, fire)
@@ -409,6 +432,48 @@ def cpu_baseline_reference(n=16384, b=256, target_s=10.0):
                      f"the host has {info['cpus_machine']}), verified C == A^T"}
     out.update(info)
     return out
+
+
+def host_layouts(costa, ha, hc, M: int, N: int, b: int, pm: int, pn: int, rank: int):
+    """the headline's layouts over host arrays: this rank's local A (M x N on pm x pn, ld = its
+    local rows) and C = A^T (N x M on the same grid), column-major"""
+    HA = costa.block_cyclic_layout(M, N, b, b, 1, 1, M, N, pm, pn, "R", 0, 0, ha, M // pm, "C", rank)
+    HC = costa.block_cyclic_layout(N, M, b, b, 1, 1, N, M, pm, pn, "R", 0, 0, hc, N // pm, "C", rank)
+    return HA, HC
+
+
+def host_c_check(hc, ha, M: int, N: int, b: int, pm: int, pn: int, rank: int, world: int, gen,
+                 sum_over_ranks) -> bool:
+    """correctness of an end-to-end leg: one rank compares every element (C == A^T); N ranks
+    compare the device legs' position samples of their host C, summed over the ranks"""
+    import numpy as np
+    import torch
+    if world == 1:
+        return bool(np.array_equal(hc.reshape(N, M), ha.reshape(N, M).T))
+    lr_c, lc_c = N // pm, M // pn
+    t = torch.from_numpy(hc)
+    if gen.device.type != "cpu":
+        t = t.to(gen.device)
+    bad = mismatch_bc(t, lr_c, lc_c, b, (pm, rank // pn, pn, rank % pn), lambda i, j: (j, i), gen)
+    return sum_over_ranks(bad) == 0
+
+
+def e2e_leg(call, hc, check, bytes_call: float, barrier, max_over_ranks, reps: int = 3,
+            before_timed=None):
+    """one host-resident leg of the headline (SURVEY §8d's end-to-end rate): C zeroed, a first
+    call (plan, staging allocation) whose result is checked, then `reps` timed calls; the time is
+    the max over the ranks -> (GBps_algorithmic, ms_per_call, verified)"""
+    hc[:] = 0
+    call()
+    ok = check()
+    if before_timed:
+        before_timed()
+    barrier()
+    t1 = time.perf_counter()
+    for _ in range(reps):
+        call()
+    te = max_over_ranks((time.perf_counter() - t1) / reps)
+    return round(bytes_call / te / 1e9, 2), round(te * 1e3, 2), ok
 
 
 def copy_ceiling(src, dst, col_bytes: int, reps: int = 20):
@@ -870,6 +935,16 @@ def main():
     pm, pn = grid_for(world)
     M, N = wmain.get("m", 0), wmain.get("n", 0)
 
+    if rank == 0:  # what the watchdog reports should a later phase hang
+        _partial_line.update({
+            "value": round(value, 2), "pct_hbm_peak": round(100 * value / (HBM_PEAK_GBPS * world), 2),
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "strong" if args.workload == "cfg5" else "weak", "vs_baseline": None,
+            "dtype": {"pxtran": "f64", "cfg3": "f64", "cfg4": "c128", "cfg5": "f32"}[args.workload],
+            "config": {"workload": wmain["wl"]}, "verified": res["verified"],
+            "partial": "the headline was measured; a later phase did not finish"})
+
     # dominant kernel: the launch list moving the most bytes on this rank
     kern = max([("local", st["local_bytes"], st["local_ms"], st["local_launches"]),
                 ("pack", st["pack_bytes"], st["pack_ms"], st["pack_launches"]),
@@ -906,69 +981,82 @@ def main():
         roof["copy_ceiling"] = cc
         roof["frac_of_ceiling"] = round(achieved / best, 4) if best > 0 else None
 
-    # end-to-end from host memory (H2D + kernels + D2H), reported, never `value`
+    # end-to-end from host memory (H2D + kernels [+ RCCL] + D2H), reported, never `value`: each
+    # rank's local A and C in host memory, the same algorithmic bytes as the device legs
     e2e = None
-    if not args.no_e2e and world == 1 and args.workload == "pxtran":
+    if not args.no_e2e and args.workload == "pxtran":
         import numpy as np
+        phase(rank, "end-to-end from host memory")
+        bytes_call = total_bytes / args.steps  # all ranks
         ha = A.cpu().numpy()
-        hc = np.zeros_like(ha)
-        HA = costa.block_cyclic_layout(M, N, b, b, 1, 1, M, N, pm, pn, "R", 0, 0, ha, M, "C", rank)
-        HC = costa.block_cyclic_layout(N, M, b, b, 1, 1, N, M, pm, pn, "R", 0, 0, hc, N, "C", rank)
-        res_e = {}
-        for mode in (1, 0):  # pipelined host staging (default), then the mirror scheme
-            costa.set_host_staging(mode)
-            hc[:] = 0
-            costa.transform(HA, HC, comm, "T", 1.0, 0.0)  # plan + staging allocation
-            ok = bool(np.array_equal(hc.reshape(N, M), ha.reshape(N, M).T)) if mode == 1 else None
-            costa.set_profiling(True)
-            costa.get_stats(reset=True)
-            reps, t1 = 3, time.perf_counter()
-            for _ in range(reps):
-                costa.transform(HA, HC, comm, "T", 1.0, 0.0)
-            te = (time.perf_counter() - t1) / reps
+        hc = np.zeros(Cm.numel())
+        HA, HC = host_layouts(costa, ha, hc, M, N, b, pm, pn, rank)
+
+        def leg(LA, LC, hcx, hax):
+            def start_stats():
+                costa.set_profiling(True)
+                costa.get_stats(reset=True)
+            gb, ms, ok = e2e_leg(lambda: costa.transform(LA, LC, comm, "T", 1.0, 0.0), hcx,
+                                 lambda: host_c_check(hcx, hax, M, N, b, pm, pn, rank, world, gen,
+                                                      sum_over_ranks),
+                                 bytes_call, barrier, max_over_ranks, before_timed=start_stats)
             sx = costa.get_stats(reset=True)
             costa.set_profiling(False)
-            res_e[mode] = {"GBps_algorithmic": round(2 * ha.nbytes / te / 1e9, 2),
-                           "ms_per_call": round(te * 1e3, 2),
-                           "h2d_ms": round(sx["h2d_ms"] / reps, 2),
-                           "d2h_ms": round(sx["d2h_ms"] / reps, 2),
-                           "kernel_ms": round(sx["local_ms"] / reps, 3)}
+            calls = max(1, sx["transforms"])  # the timed calls
+            return gb, ms, ok, sx, calls
+
+        res_e = {}
+        for mode in ((1, 0) if world == 1 else (1,)):  # pipelined (default), then the mirror
+            costa.set_host_staging(mode)
+            gb, ms, ok, sx, calls = leg(HA, HC, hc, ha)
+            res_e[mode] = {"GBps_algorithmic": gb, "ms_per_call": ms,
+                           "h2d_ms": round(sx["h2d_ms"] / calls, 2),
+                           "d2h_ms": round(sx["d2h_ms"] / calls, 2),
+                           "kernel_ms": round((sx["local_ms"] + sx["unpack_ms"]) / calls, 3)}
             if mode == 1:
-                res_e[mode].update({"groups": sx["host_groups"] // reps, "verified": ok})
+                res_e[mode].update({"groups": sx["host_groups"] // calls, "verified": ok})
+                if world > 1:
+                    res_e[mode]["exchange_ms"] = round(sx["exchange_ms"] / calls, 2)
+            if ok is False:
+                raise RuntimeError("bench.py: wrong end-to-end result (host staging mode %d)" % mode)
         costa.set_host_staging(1)
         # the same from page-locked host arrays (hipHostMalloc via torch's pinned allocator):
-        # every tile moves by strided DMA between the caller's memory and HBM, no host copies
+        # groups whose footprints are rectangles of the caller's arrays move by strided DMA
+        # between those arrays and HBM (pack / unpack groups included), no host copies
         tpa = torch.empty(ha.nbytes, dtype=torch.uint8, pin_memory=True)
         tpc = torch.empty(hc.nbytes, dtype=torch.uint8, pin_memory=True)
         pa, pc = tpa.numpy().view(ha.dtype), tpc.numpy().view(hc.dtype)
         pa[:] = ha
-        pc[:] = 0
-        PA = costa.block_cyclic_layout(M, N, b, b, 1, 1, M, N, pm, pn, "R", 0, 0, pa, M, "C", rank)
-        PC = costa.block_cyclic_layout(N, M, b, b, 1, 1, N, M, pm, pn, "R", 0, 0, pc, N, "C", rank)
-        costa.transform(PA, PC, comm, "T", 1.0, 0.0)
-        okp = bool(np.array_equal(pc.reshape(N, M), pa.reshape(N, M).T))
-        costa.set_profiling(True)
-        costa.get_stats(reset=True)
-        reps, t1 = 3, time.perf_counter()
-        for _ in range(reps):
-            costa.transform(PA, PC, comm, "T", 1.0, 0.0)
-        te = (time.perf_counter() - t1) / reps
-        sx = costa.get_stats(reset=True)
-        costa.set_profiling(False)
-        pinned = {"GBps_algorithmic": round(2 * pa.nbytes / te / 1e9, 2), "ms_per_call": round(te * 1e3, 2),
-                  "h2d_ms": round(sx["h2d_ms"] / reps, 2), "d2h_ms": round(sx["d2h_ms"] / reps, 2),
-                  "direct_dma": sx["host_direct"] == reps, "verified": okp}
+        PA, PC = host_layouts(costa, pa, pc, M, N, b, pm, pn, rank)
+        gb, ms, okp, sx, calls = leg(PA, PC, pc, pa)
+        pinned = {"GBps_algorithmic": gb, "ms_per_call": ms,
+                  "h2d_ms": round(sx["h2d_ms"] / calls, 2), "d2h_ms": round(sx["d2h_ms"] / calls, 2),
+                  "direct_dma": sx["host_direct"] == calls,
+                  "direct_groups": f"{sx['host_direct_groups'] // calls} of {sx['host_groups'] // calls}",
+                  "verified": okp}
+        if world > 1:
+            pinned["exchange_ms"] = round(sx["exchange_ms"] / calls, 2)
+        if okp is False:
+            raise RuntimeError("bench.py: wrong end-to-end result (page-locked host memory)")
         del PA, PC, tpa, tpc, pa, pc
         e2e = dict(res_e[1])
         e2e["pinned_host"] = pinned
-        e2e["mirror"] = res_e[0]
-        e2e["note"] = ("pageable host A and C (numpy), 2 x 2 GiB over PCIe. Pipelined (default): "
-                       "64 MiB tile groups, host gather -> H2D -> tile kernels -> D2H -> host "
-                       "scatter, both copy directions at once (h2d_ms/d2h_ms = span of each "
-                       "copy stream). pinned_host: the same matrices in page-locked host memory, "
-                       "tiles moved by strided DMA straight between the caller's arrays and HBM. "
-                       "mirror: H2D of A's range, kernel, D2H of C's range "
-                       "(C not uploaded: beta=0 and every byte of it is overwritten)")
+        if world == 1:
+            e2e["mirror"] = res_e[0]
+        e2e["note"] = ("each rank's local A and C in pageable host memory (numpy), "
+                       f"{2 * ha.nbytes / 2**30:.0f} GiB a rank over PCIe; the algorithmic bytes of "
+                       "the device legs over the max time of a blocking call over the ranks. "
+                       "Pipelined (default): 64 MiB tile groups, host gather -> H2D -> tile kernels "
+                       "-> D2H -> host scatter, both copy directions at once (h2d_ms / d2h_ms = span "
+                       "of each copy stream)"
+                       + (", pack groups gathered straight into the send buffer, RCCL exchange in "
+                          "rounds, unpack groups scattered back" if world > 1 else "")
+                       + ". pinned_host: the same matrices in page-locked host memory, groups moved "
+                         "by strided DMA straight between the caller's arrays and HBM where their "
+                         "footprints are rectangles (direct_groups)"
+                       + (". mirror: H2D of A's range, kernel, D2H of C's range (C not uploaded: "
+                          "beta=0 and every byte of it is overwritten)" if world == 1 else ""))
+        del ha, hc, HA, HC
 
     # fixed cost of one blocking transform call (plan-cache hit, one 16x16 tile)
     overhead_us = None

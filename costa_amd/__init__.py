@@ -97,7 +97,8 @@ class Stats(C.Structure):
                 ("local_bytes", C.c_int64), ("unpack_bytes", C.c_int64),
                 ("transforms", C.c_int64), ("plan_hits", C.c_int64),
                 ("plan_misses", C.c_int64), ("host_groups", C.c_int64),
-                ("device_plans", C.c_int64), ("plan_ms", C.c_double), ("host_direct", C.c_int64)]
+                ("device_plans", C.c_int64), ("plan_ms", C.c_double), ("host_direct", C.c_int64),
+                ("host_direct_groups", C.c_int64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -907,14 +907,23 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
             // (c64, on its 128 x 128 sub-tiles, ran 1 % slower with them: 4.36 against 4.31 ms)
             if (panel == 0)
                 panel = ld0 * E > (int64_t(128) << 10) && dtype != COSTA_CFLOAT ? (int64_t(128) << 10) / E : -1;
-            if (panel > 0 && one_ld && !key.empty()) {
-                uint64_t lo = ~uint64_t(0);
-                for (const auto& k : key) lo = std::min(lo, k.first);
-                const int64_t ld = ld0;
-                for (auto& k : key) {
-                    const uint64_t e = (k.first - lo) / uint64_t(E);
-                    const uint64_t row = e % uint64_t(ld), col = e / uint64_t(ld);
-                    k.first = ((row / uint64_t(panel)) << 48) | (col << 24) | (row % uint64_t(panel));
+            // key = panel (16 bits) | column (24) | row in the panel (24): a panel of 2^24 rows or
+            // more, a column index or a panel index past its field keeps the plain address order
+            if (panel >= (int64_t(1) << 24)) panel = -1;
+            if (panel > 0 && one_ld) {
+                uint64_t lo = ~uint64_t(0), hi = 0;
+                for (const auto& k : key) {
+                    lo = std::min(lo, k.first);
+                    hi = std::max(hi, k.first);
+                }
+                const uint64_t ld = uint64_t(ld0), last = (hi - lo) / uint64_t(E);
+                const bool fits = last / ld < (uint64_t(1) << 24) && ld / uint64_t(panel) < (uint64_t(1) << 16);
+                if (fits) {
+                    for (auto& k : key) {
+                        const uint64_t e = (k.first - lo) / uint64_t(E);
+                        const uint64_t row = e % ld, col = e / ld;
+                        k.first = ((row / uint64_t(panel)) << 48) | (col << 24) | (row % uint64_t(panel));
+                    }
                 }
             }
             std::sort(key.begin(), key.end());

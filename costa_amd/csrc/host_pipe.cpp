@@ -271,12 +271,15 @@ struct host_pipeline {
         size_t ord_first = 0, work_first = 0;
         bool any_tr = false;
         int64_t alg_bytes = 0;
-        // direct mode (page-locked caller memory): the group's source and target footprints as
-        // host rectangles, each moved by one strided DMA into / out of a dense device image,
-        // and the op list that reads / writes those images
+        // direct mode (page-locked caller memory): the group's host footprints -- the source of
+        // a PACK group, the target of an UNPACK group, both of a LOCAL one -- as rectangles of
+        // the caller's arrays, each moved by one strided DMA into / out of a dense device image,
+        // and the op list that reads / writes those images (build_direct)
+        bool direct = false;
         rect src_rect, dst_rect;
         work_split split_d;
         size_t ord_first_d = 0, work_first_d = 0;
+        bool any_tr_d = false;
     };
     costa_dtype_t dtype = COSTA_DOUBLE;
     size_t E = 8;
@@ -290,8 +293,10 @@ struct host_pipeline {
     std::vector<int> rounds_after;    // ... issued once group t is enqueued (cumulative)
     void* d_ops = nullptr;   // every group's ordered device ops (package offsets)
     void* d_work = nullptr;
-    bool direct_ok = false;  // every group LOCAL with rectangle footprints (direct mode possible)
-    void* d_ops_d = nullptr;  // ... and its device ops (image offsets)
+    // direct mode, built on the first call that finds the caller's memory page-locked
+    bool direct_built = false;
+    size_t n_direct = 0;      // groups whose footprints are rectangles
+    void* d_ops_d = nullptr;  // ... and their device ops (image offsets)
     void* d_work_d = nullptr;
     // the caller's host byte ranges the ops read or write (merged): when all of them are
     // page-locked the pipeline moves tiles by strided DMA instead of host copies
@@ -565,62 +570,6 @@ std::shared_ptr<host_pipeline> make_host_pipeline(costa_dtype_t dtype,
         all_ord.insert(all_ord.end(), ord.begin(), ord.end());
         all_work.insert(all_work.end(), work.begin(), work.end());
     }
-    // direct mode: every group LOCAL and both footprints rectangles of the caller's arrays
-    std::vector<costa_tile_op_t> all_ord_d;
-    std::vector<uint64_t> all_work_d;
-    hp->direct_ok = !hp->groups.empty();
-    for (auto& gr : hp->groups) {
-        if (!hp->direct_ok) break;
-        if (gr.kind != hpl::LOCAL) {
-            hp->direct_ok = false;
-            break;
-        }
-        std::vector<foot> fs, ft;
-        for (size_t i = gr.first; i < gr.first + gr.count; ++i) {
-            const auto& op = hp->hops[i].op;
-            int64_t run, runs;
-            target_shape(op, run, runs);
-            fs.push_back({uintptr_t(op.src), op.nf, op.ns, op.lds});
-            ft.push_back({uintptr_t(op.dst), run, runs, op.ldd});
-        }
-        std::vector<std::pair<int64_t, int64_t>> ps, pt;
-        if (!rectangle_of(fs, E, gr.src_rect, ps) || !rectangle_of(ft, E, gr.dst_rect, pt)) {
-            hp->direct_ok = false;
-            break;
-        }
-        std::vector<costa_tile_op_t> dev_ops;
-        for (size_t i = gr.first; i < gr.first + gr.count; ++i) {
-            const size_t j = i - gr.first;
-            costa_tile_op_t d = hp->hops[i].op;
-            d.src = uint64_t((ps[j].second * gr.src_rect.w + ps[j].first) * int64_t(E));
-            d.lds = int32_t(gr.src_rect.w);
-            d.dst = uint64_t((pt[j].second * gr.dst_rect.w + pt[j].first) * int64_t(E));
-            d.ldd = int32_t(gr.dst_rect.w);
-            d.flags &= ~uint32_t(COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST);
-            if (d.src % 16 == 0 && (int64_t(d.lds) * int64_t(E)) % 16 == 0) d.flags |= COSTA_TILE_VEC_SRC;
-            if (d.dst % 16 == 0 && (int64_t(d.ldd) * int64_t(E)) % 16 == 0) d.flags |= COSTA_TILE_VEC_DST;
-            dev_ops.push_back(d);
-        }
-        std::vector<costa_tile_op_t> ord;
-        std::vector<uint64_t> work;
-        gr.split_d = build_work(dtype, dev_ops, ord, work);
-        gr.ord_first_d = all_ord_d.size();
-        gr.work_first_d = all_work_d.size();
-        all_ord_d.insert(all_ord_d.end(), ord.begin(), ord.end());
-        all_work_d.insert(all_work_d.end(), work.begin(), work.end());
-    }
-    if (hp->direct_ok) {
-        if (!all_ord_d.empty()) {
-            HP_CHECK(hipMalloc(&hp->d_ops_d, all_ord_d.size() * sizeof(costa_tile_op_t)));
-            HP_CHECK(hipMemcpy(hp->d_ops_d, all_ord_d.data(), all_ord_d.size() * sizeof(costa_tile_op_t),
-                               hipMemcpyHostToDevice));
-        }
-        if (!all_work_d.empty()) {
-            HP_CHECK(hipMalloc(&hp->d_work_d, all_work_d.size() * sizeof(uint64_t)));
-            HP_CHECK(hipMemcpy(hp->d_work_d, all_work_d.data(), all_work_d.size() * sizeof(uint64_t),
-                               hipMemcpyHostToDevice));
-        }
-    }
     {  // host footprints: sources of PACK / LOCAL hops, targets of LOCAL / UNPACK hops
         auto& r = hp->host_ranges;
         for (const auto& gr : hp->groups)
@@ -636,10 +585,14 @@ std::shared_ptr<host_pipeline> make_host_pipeline(costa_dtype_t dtype,
                                  uintptr_t(op.dst + ((uint64_t(runs) - 1) * uint64_t(op.ldd) + uint64_t(run)) * E)});
                 }
             }
+        // merged where they overlap, not where they only touch: footprints lie inside their own
+        // arrays, so every merged range stays inside one allocation and its two ends tell whether
+        // that allocation is page-locked (a pageable array between two page-locked ones stays a
+        // range of its own)
         std::sort(r.begin(), r.end());
         size_t o = 0;
         for (size_t i = 0; i < r.size(); ++i) {
-            if (o && r[i].first <= r[o - 1].second)
+            if (o && r[i].first < r[o - 1].second)
                 r[o - 1].second = std::max(r[o - 1].second, r[i].second);
             else
                 r[o++] = r[i];
@@ -660,6 +613,86 @@ std::shared_ptr<host_pipeline> make_host_pipeline(costa_dtype_t dtype,
 }
 
 size_t host_pipeline_groups(const host_pipeline& hp) { return hp.groups.size(); }
+
+namespace {
+// Direct mode of a pipeline, built once, on its first call from page-locked memory (calls from
+// pageable memory never pay for it).  A group goes direct when the footprints it moves are
+// rectangles of the caller's arrays (rectangle_of): the source of a PACK group, the target of
+// an UNPACK group, both of a LOCAL group; its ops are rewritten against the dense device images
+// of those rectangles:
+//   PACK    image -> the send buffer at the package offsets (a pack kernel replaces the host
+//           gather; the reference's PACK, communication_data.cpp:191-217)
+//   LOCAL   source image -> target image
+//   UNPACK  the receive buffer -> target image (communication_data.cpp:219-244)
+// Other groups keep the host gather / scatter through the pinned slots, in the same call.
+void build_direct(host_pipeline& hp) {
+    using hpl = host_pipeline;
+    hp.direct_built = true;
+    const size_t E = hp.E;
+    std::vector<costa_tile_op_t> all_ord;
+    std::vector<uint64_t> all_work;
+    for (auto& gr : hp.groups) {
+        std::vector<foot> fs, ft;
+        for (size_t i = gr.first; i < gr.first + gr.count; ++i) {
+            const auto& op = hp.hops[i].op;
+            int64_t run, runs;
+            target_shape(op, run, runs);
+            if (gr.kind != hpl::UNPACK) fs.push_back({uintptr_t(op.src), op.nf, op.ns, op.lds});
+            if (gr.kind != hpl::PACK) ft.push_back({uintptr_t(op.dst), run, runs, op.ldd});
+        }
+        std::vector<std::pair<int64_t, int64_t>> ps, pt;
+        if ((gr.kind != hpl::UNPACK && !rectangle_of(fs, E, gr.src_rect, ps)) ||
+            (gr.kind != hpl::PACK && !rectangle_of(ft, E, gr.dst_rect, pt)))
+            continue;
+        // an image must fit its device slot half
+        const size_t S = hp.slot_bytes;
+        if (size_t(gr.src_rect.w * gr.src_rect.h) * E > S || size_t(gr.dst_rect.w * gr.dst_rect.h) * E > S)
+            continue;
+        std::vector<costa_tile_op_t> dev_ops;
+        for (size_t i = gr.first; i < gr.first + gr.count; ++i) {
+            const size_t j = i - gr.first;
+            costa_tile_op_t d = hp.hops[i].op;
+            if (gr.kind != hpl::UNPACK) {
+                d.src = uint64_t((ps[j].second * gr.src_rect.w + ps[j].first) * int64_t(E));
+                d.lds = int32_t(gr.src_rect.w);
+            }
+            if (gr.kind != hpl::PACK) {
+                d.dst = uint64_t((pt[j].second * gr.dst_rect.w + pt[j].first) * int64_t(E));
+                d.ldd = int32_t(gr.dst_rect.w);
+            }
+            d.flags &= ~uint32_t(COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST);
+            if (d.src % 16 == 0 && (int64_t(d.lds) * int64_t(E)) % 16 == 0) d.flags |= COSTA_TILE_VEC_SRC;
+            if (d.dst % 16 == 0 && (int64_t(d.ldd) * int64_t(E)) % 16 == 0) d.flags |= COSTA_TILE_VEC_DST;
+            dev_ops.push_back(d);
+        }
+        if (gr.kind == hpl::PACK) {
+            gr.alg_bytes = 0;
+            for (const auto& d : dev_ops) gr.alg_bytes += 2 * int64_t(E) * int64_t(d.nf) * d.ns;
+        }
+        gr.any_tr_d = any_transpose(dev_ops);
+        std::vector<costa_tile_op_t> ord;
+        std::vector<uint64_t> work;
+        gr.split_d = build_work(hp.dtype, dev_ops, ord, work,
+                                gr.kind == hpl::PACK ? list_pack : gr.kind == hpl::UNPACK ? list_unpack : list_local);
+        gr.ord_first_d = all_ord.size();
+        gr.work_first_d = all_work.size();
+        all_ord.insert(all_ord.end(), ord.begin(), ord.end());
+        all_work.insert(all_work.end(), work.begin(), work.end());
+        gr.direct = true;
+        ++hp.n_direct;
+    }
+    if (!all_ord.empty()) {
+        HP_CHECK(hipMalloc(&hp.d_ops_d, all_ord.size() * sizeof(costa_tile_op_t)));
+        HP_CHECK(hipMemcpy(hp.d_ops_d, all_ord.data(), all_ord.size() * sizeof(costa_tile_op_t),
+                           hipMemcpyHostToDevice));
+    }
+    if (!all_work.empty()) {
+        HP_CHECK(hipMalloc(&hp.d_work_d, all_work.size() * sizeof(uint64_t)));
+        HP_CHECK(hipMemcpy(hp.d_work_d, all_work.data(), all_work.size() * sizeof(uint64_t),
+                           hipMemcpyHostToDevice));
+    }
+}
+}  // namespace
 
 namespace {
 // every byte range page-locked host memory (hipHostMalloc / hipHostRegister), checked at both
@@ -695,7 +728,11 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
     // device slots (no host gather / scatter, no pinned slots); the host only issues, stream
     // events order everything.  pinned H2D + D2H of 1-16 KiB rows at once: 94-97 GB/s
     // (tools/pcie_probe.hip, profiles/r4h/)
-    const bool direct = hp.direct_ok && all_pinned(hp.host_ranges);
+    const bool pinned = all_pinned(hp.host_ranges);
+    if (pinned && !hp.direct_built) build_direct(hp);
+    const bool direct = pinned && hp.n_direct > 0;
+    auto is_direct = [&](const hpl::group* x) { return direct && x && x->direct; };
+    size_t n_direct_run = 0;
     // timing brackets (profiling only): per group kernel, the exchange, and the spans of both
     // copy streams
     std::vector<hipEvent_t> evs;
@@ -710,7 +747,7 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
         hipEvent_t a, b;
         bool unpack;
     };
-    std::vector<kbracket> kern_t;
+    std::vector<kbracket> kern_t, pack_t;
     hipEvent_t up0 = nullptr, up1 = nullptr, dn0 = nullptr, dn1 = nullptr, x0 = nullptr, x1 = nullptr;
     // every slot starts free: the ring's events are recorded on idle streams
     for (int k = 0; k < kRing; ++k) {
@@ -796,22 +833,47 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
         const hpl::group* g = t < G ? &hp.groups[t] : nullptr;
         const hpl::group* o = t >= size_t(kLag) ? &hp.groups[t - kLag] : nullptr;
         if (o && o->kind == hpl::PACK) o = nullptr;  // nothing comes back from a pack group
+        if (is_direct(o)) o = nullptr;               // ... nor to the host threads from a direct one
+        const bool gd = is_direct(g);
+        const hpl::group* gh = gd ? nullptr : g;     // group t's host gather
         const int ko = int((t + kRing - kLag) % kRing);  // slot of group t - kLag
         char* pin = R.pin_in + size_t(k) * 2 * S;
         char* dev = R.dev + size_t(k) * 2 * S;
         double t0 = now();
         // the pinned source slot is free once its previous upload has landed
-        if (g && !direct) HP_CHECK(hipEventSynchronize(R.up_done[k]));
+        if (gh) HP_CHECK(hipEventSynchronize(R.up_done[k]));
         double t1 = now();
         // group t - kLag's target package has landed in its pinned slot
-        if (o && !direct) HP_CHECK(hipEventSynchronize(R.down_done[ko]));
+        if (o) HP_CHECK(hipEventSynchronize(R.down_done[ko]));
         double t2 = now();
-        if (!direct) host_step(g, pin, o, R.pin_out + size_t(ko) * S);
+        if (gh || o) host_step(gh, pin, o, R.pin_out + size_t(ko) * S);
         double t3 = now();
         t_wait_up += t1 - t0;
         t_wait_down += t2 - t1;
         t_copy += t3 - t2;
         if (!g) continue;
+        n_direct_run += gd;
+        if (g->kind == hpl::PACK && gd) {
+            // direct: the source rectangle up into the device slot, then the pack kernel into the
+            // send buffer on the exchange stream, ahead of its round's RCCL group there
+            HP_CHECK(hipStreamWaitEvent(R.up, R.down_done[k], 0));  // the slot's previous user
+            if (prof && !up0) up0 = ev(R.up);
+            move_rect(g->src_rect, dev, true);
+            HP_CHECK(hipEventRecord(R.up_done[k], R.up));
+            if (prof) up1 = ev(R.up);
+            HP_CHECK(hipStreamWaitEvent(xs, R.up_done[k], 0));
+            hipEvent_t k0 = prof ? ev(xs) : nullptr;
+            launch_tiles(hp.dtype,
+                         make_launch(g->split_d, static_cast<const costa_tile_op_t*>(hp.d_ops_d) + g->ord_first_d,
+                                     static_cast<const uint64_t*>(hp.d_work_d) + g->work_first_d, dev, send_buf,
+                                     d_scalars, g->any_tr_d, false),
+                         xs);
+            if (prof) pack_t.push_back({k0, ev(xs), false});
+            HP_CHECK(hipEventRecord(R.down_done[k], xs));  // the device slot is free again
+            issue_rounds(hp.rounds_after[t]);
+            t_issue += now() - t3;
+            continue;
+        }
         if (g->kind == hpl::PACK) {  // the host gather is the pack: upload into the send buffer
             if (prof && !up0) up0 = ev(R.up);
             HP_CHECK(hipMemcpyAsync(send_buf + g->send_off, pin, g->in_bytes, hipMemcpyHostToDevice,
@@ -829,8 +891,8 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
         HP_CHECK(hipStreamWaitEvent(R.up, R.down_done[k], 0));
         if (g->in_bytes || g->reads_old) {
             if (prof && !up0) up0 = ev(R.up);
-            if (direct) {
-                move_rect(g->src_rect, dev, true);
+            if (gd) {
+                if (g->in_bytes) move_rect(g->src_rect, dev, true);
                 if (g->reads_old) move_rect(g->dst_rect, dev + S, true);
             } else {
                 if (g->in_bytes) HP_CHECK(hipMemcpyAsync(dev, pin, g->in_bytes, hipMemcpyHostToDevice, R.up));
@@ -844,11 +906,11 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
         HP_CHECK(hipStreamWaitEvent(comp, R.up_done[k], 0));
         if (unpack) HP_CHECK(hipStreamWaitEvent(comp, R.moved[g->round], 0));
         hipEvent_t k0 = prof ? ev(comp) : nullptr;
-        if (direct)
+        if (gd)
             launch_tiles(hp.dtype,
                          make_launch(g->split_d, static_cast<const costa_tile_op_t*>(hp.d_ops_d) + g->ord_first_d,
-                                     static_cast<const uint64_t*>(hp.d_work_d) + g->work_first_d, dev,
-                                     dev + S, d_scalars, g->any_tr, g->reads_old),
+                                     static_cast<const uint64_t*>(hp.d_work_d) + g->work_first_d,
+                                     unpack ? recv_buf : dev, dev + S, d_scalars, g->any_tr_d, g->reads_old),
                          comp);
         else
             launch_tiles(hp.dtype,
@@ -863,7 +925,7 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
         // t - kRing + kLag < t
         HP_CHECK(hipStreamWaitEvent(R.down, R.kern_done[k], 0));
         if (prof && !dn0) dn0 = ev(R.down);
-        if (direct)
+        if (gd)
             move_rect(g->dst_rect, dev + S, false);
         else
             HP_CHECK(hipMemcpyAsync(R.pin_out + size_t(k) * S, dev + S, g->out_bytes,
@@ -878,7 +940,8 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
         std::fprintf(stderr,
                      "[costa host pipe] groups %zu, %d exchange round(s), slot %zu MiB threads %d%s: "
                      "total %.2f ms, copies %.2f, wait-up %.2f, wait-down %.2f, issue %.2f\n",
-                     G, exchange ? hp.rounds : 0, S >> 20, host_threads(), direct ? " (direct DMA)" : "",
+                     G, exchange ? hp.rounds : 0, S >> 20, host_threads(),
+                     direct ? (n_direct_run == G ? " (direct DMA)" : " (direct DMA: some groups)") : "",
                      (now() - t_begin) * 1e3,
                      t_copy * 1e3, t_wait_up * 1e3, t_wait_down * 1e3, t_issue * 1e3);
     HP_CHECK(hipStreamSynchronize(R.up));
@@ -897,12 +960,23 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
         }
     }
     st.host_groups += int64_t(G);
-    if (direct) st.host_direct++;
+    if (n_direct_run) st.host_direct++;
+    st.host_direct_groups += int64_t(n_direct_run);
+    if (direct)
+        for (const auto& gr : hp.groups)
+            if (gr.kind == hpl::PACK && gr.direct) {
+                st.pack_bytes += gr.alg_bytes;
+                st.pack_launches++;
+            }
     if (prof) {
         float ms = 0.f;
         for (auto& x : kern_t) {
             HP_CHECK(hipEventElapsedTime(&ms, x.a, x.b));
             (x.unpack ? st.unpack_ms : st.local_ms) += ms;
+        }
+        for (auto& x : pack_t) {
+            HP_CHECK(hipEventElapsedTime(&ms, x.a, x.b));
+            st.pack_ms += ms;
         }
         if (up0 && up1 && hipEventElapsedTime(&ms, up0, up1) == hipSuccess) st.h2d_ms += ms;
         if (dn0 && dn1 && hipEventElapsedTime(&ms, dn0, dn1) == hipSuccess) st.d2h_ms += ms;

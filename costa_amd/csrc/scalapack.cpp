@@ -112,7 +112,23 @@ void free_at_finalize() {
     done = true;
 }
 
-MPI_Comm grid_comm(int ctxt, const grid_info& g) {
+// The communicator of one call: the cached one, or -- when some grid process lies outside this
+// process's MPI_COMM_WORLD (MPI_Comm_spawn / MPI_Comm_connect: its world rank translates to
+// MPI_UNDEFINED, and two different grids could then share a key) -- one made for the call and
+// freed after it, with the RCCL communicator cached on it.  Every member of such a grid sees an
+// undefined rank (the members share no world), so all of them take the uncached way together.
+struct call_comm {
+    MPI_Comm comm = MPI_COMM_NULL;
+    bool owned = false;
+    call_comm() = default;
+    call_comm(const call_comm&) = delete;
+    call_comm& operator=(const call_comm&) = delete;
+    ~call_comm() {
+        if (owned && comm != MPI_COMM_NULL) MPI_Comm_free(&comm);
+    }
+};
+
+void grid_comm(int ctxt, const grid_info& g, call_comm& cc) {
     comm_cache& cache = cached_comms();
     MPI_Comm sys = sys_comm(ctxt);
     MPI_Group all, grp, world;
@@ -124,18 +140,26 @@ MPI_Comm grid_comm(int ctxt, const grid_info& g) {
     MPI_Comm_group(MPI_COMM_WORLD, &world);
     MPI_Group_translate_ranks(grp, int(cells.size()), cells.data(), world, procs.data());
     MPI_Group_free(&world);
-    auto it = cache.by_procs.find(procs);
-    if (it != cache.by_procs.end()) {
-        MPI_Group_free(&grp);
-        return it->second;
+    const bool keyed = std::find(procs.begin(), procs.end(), MPI_UNDEFINED) == procs.end();
+    if (keyed) {
+        auto it = cache.by_procs.find(procs);
+        if (it != cache.by_procs.end()) {
+            MPI_Group_free(&grp);
+            cc.comm = it->second;
+            return;
+        }
     }
     MPI_Comm out = MPI_COMM_NULL;
     MPI_Comm_create_group(sys, grp, 0x6c0d, &out);
     MPI_Group_free(&grp);
     if (out == MPI_COMM_NULL) throw std::runtime_error("could not make the context's communicator");
+    cc.comm = out;
+    if (!keyed) {
+        cc.owned = true;
+        return;
+    }
     free_at_finalize();
     cache.by_procs.emplace(std::move(procs), out);
-    return out;
 }
 
 // One matrix's distribution as seen in `comm`: its grid, blocking and rank sources, and the
@@ -238,7 +262,9 @@ void pxgemr2d(int m, int n, const T* a, int ia, int ja, const int* desca, T* c, 
     try {
         const grid_info gi = grid_of(ictxt);
         if (!gi.member()) return;  // not a process of the call's context: nothing to do
-        MPI_Comm comm = grid_comm(ictxt, gi);
+        call_comm cc;
+        grid_comm(ictxt, gi, cc);
+        MPI_Comm comm = cc.comm;
         int P = 1;
         MPI_Comm_size(comm, &P);
         const auto d = distributions(comm, {desca, descc});
@@ -259,7 +285,9 @@ void pxtran(int m, int n, T alpha, const T* a, int ia, int ja, const int* desca,
             throw std::runtime_error("A and C must share one BLACS context");  // scalapack.cpp:18-23
         const grid_info g = grid_of(desca[1]);
         if (!g.member()) return;
-        MPI_Comm comm = grid_comm(desca[1], g);
+        call_comm cc;
+        grid_comm(desca[1], g, cc);
+        MPI_Comm comm = cc.comm;
         int P = 1;
         MPI_Comm_size(comm, &P);
         const auto d = distributions(comm, {desca, descc});

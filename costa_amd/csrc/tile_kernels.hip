@@ -470,6 +470,128 @@ template <> struct shapes<cpx<double>> {
     using small32_tr = shape<cpx<double>, 128, 32, 32>;
 };
 
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void glob_void;
+
+// Staging of full transposing sub-tiles (tuning builds; 0 = register staging, shipped):
+//   1  LDS-DMA (global_load_lds_dwordx4 nt): no VGPR holds staged data, no ds_write phase
+//   2  the same, the sub-tile's two halves of rows waited for and stored one after the other
+//   3  LDS-DMA, each wavefront's instructions on consecutive source columns
+//   4  register staging, two halves as in 2
+#ifndef COSTA_TR_STAGE
+#define COSTA_TR_STAGE 0
+#endif
+
+// A full transposing sub-tile staged by LDS-DMA.  The image has no pad: slot (s, q) (16 bytes,
+// V elements f = qV .. qV+V-1 of source column s) sits at s * Q + (q ^ (s % Q)), so the column-
+// wise slot reads of the store phase hit Q different bank groups.  An LDS-DMA instruction writes
+// 64 slots lane-linearly from a wave-uniform base; lane j of instruction i fills image slot
+// 64 i + j and loads whatever source vector belongs there.
+template <typename T, typename S, bool NT>
+__device__ __forceinline__ void tr_tile_glds(const costa_tile_op_t& op, int f0, int s0, const char* src_base,
+                                             char* dst_base, T alpha, T beta, T* tile) {
+    constexpr int V = S::V, BF = S::BF, BS = S::BS, Q = BF / V, NW = S::NW;
+    constexpr int NI = BS * Q / 64 / NW;  // LDS-DMA instructions per wavefront
+    static_assert(64 % Q == 0 && (BS * Q) % (64 * NW) == 0 && S::FW == 1, "glds mapping");
+    constexpr int MODE = COSTA_TR_STAGE;
+    const uint32_t flags = op.flags;
+    const uint32_t kind = (flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT;
+    const bool conj = flags & COSTA_TILE_CONJ;
+    const int64_t lds = op.lds, ldd = op.ldd;
+    const T* src = reinterpret_cast<const T*>(src_base + op.src) + int64_t(s0) * lds + f0;
+    const int lane = int(threadIdx.x) % 64;
+    const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / 64);
+    char* tb = reinterpret_cast<char*>(tile);
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+        const int i = MODE == 3 ? wave * NI + k : wave + NW * k;
+        const int slot = i * 64 + lane, s = slot / Q, q = (slot % Q) ^ (s % Q);
+        __builtin_amdgcn_global_load_lds((glob_void*)(src + int64_t(s) * lds + q * V), (lds_void*)(tb + i * 1024),
+                                         16, 0, NT ? 2 : 0);
+    }
+    T* dst = reinterpret_cast<T*>(dst_base + op.dst) + int64_t(f0) * ldd + s0;
+    constexpr int QG = Q;  // store units per s chunk (FW = 1)
+    auto unit = [&](int k, int& f, int& sb) {
+        const int u = wave + NW * k;
+        const int sc = u / QG, q = u % QG;
+        const int j = lane & (V - 1);
+        f = q * V + j;
+        sb = sc * 64 + (lane - j);
+    };
+    vec<T> old[S::PS];
+    if (kind == COSTA_SCALE_AXPBY) {
+#pragma unroll
+        for (int k = 0; k < S::PS; ++k) {
+            int f, sb;
+            unit(k, f, sb);
+            vload(old[k], dst + f * ldd + sb, V, true);
+        }
+    }
+    const raw16* img = reinterpret_cast<const raw16*>(tile);
+    auto store_units = [&](int k0, int k1) {
+        vec<T> y[S::PS];
+        if constexpr (MODE == 2) {
+            // the compiler waits for every LDS-DMA load before any LDS read it can see (vmcnt(0)):
+            // the reads of a half are issued as inline asm, ordered by the explicit waits
+            u32x4a r[S::PS];
+#pragma unroll
+            for (int k = k0; k < k1; ++k) {
+                const int u = wave + NW * k;
+                const int sc = u / QG, q = u % QG;
+                const int s = sc * 64 + lane;
+                const uint32_t a = uint32_t(reinterpret_cast<uintptr_t>(
+                    (__attribute__((address_space(3))) const raw16*)(img + s * Q + (q ^ (s % Q)))));
+                asm volatile("ds_read_b128 %0, %1" : "=v"(r[k]) : "v"(a) : "memory");
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int k = k0; k < k1; ++k) {
+                asm volatile("" : "+v"(r[k]));
+                __builtin_memcpy(&y[k], &r[k], 16);
+            }
+        } else {
+#pragma unroll
+            for (int k = k0; k < k1; ++k) {
+                const int u = wave + NW * k;
+                const int sc = u / QG, q = u % QG;
+                const int s = sc * 64 + lane;
+                raw16 r = img[s * Q + (q ^ (s % Q))];
+                __builtin_memcpy(&y[k], &r, 16);
+            }
+        }
+#pragma unroll
+        for (int k = k0; k < k1; ++k) {
+            vec<T> o = lane_transpose(y[k], lane);
+            int f, sb;
+            unit(k, f, sb);
+            if (kind != COSTA_SCALE_BITCOPY) {
+#pragma unroll
+                for (int e = 0; e < V; ++e)
+                    o.e[e] = scale(o.e[e], kind == COSTA_SCALE_AXPBY ? old[k].e[e] : e_zero<T>(), kind, conj,
+                                   alpha, beta);
+            }
+            vstore<T, NT>(dst + f * ldd + sb, o, V, true);
+        }
+    };
+    if constexpr (MODE == 2) {
+        if (kind != COSTA_SCALE_AXPBY) {
+            // the first NI / 2 instructions of every wavefront hold rows [0, BS / 2): store units
+            // 0 .. PS / 2 - 1 read only those (vector memory completes in issue order)
+            static_assert(NI % 2 == 0 && S::PS % 2 == 0, "halves");
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI / 2) : "memory");
+            __builtin_amdgcn_s_barrier();  // (no fence: the waits above order the LDS-DMA)
+            store_units(0, S::PS / 2);
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S::PS / 2) : "memory");
+            __builtin_amdgcn_s_barrier();  // (no fence: the waits above order the LDS-DMA)
+            store_units(S::PS / 2, S::PS);
+            return;
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // (no fence: the waits above order the LDS-DMA)
+    store_units(0, S::PS);
+}
+
 // One sub-tile.  FULL: the sub-tile is a whole BF x BS block with 16-byte aligned rows on
 // both sides, so every guard below folds away and each thread issues its loads and stores
 // back to back with no per-lane branches (the common case: block-cyclic tiles).
@@ -487,6 +609,12 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
     const bool vd = FULL || (flags & COSTA_TILE_VEC_DST);
     const int64_t lds = op.lds, ldd = op.ldd;
     const T* src = reinterpret_cast<const T*>(src_base + op.src) + int64_t(s0) * lds + f0;
+    if constexpr (FULL && COSTA_TR_STAGE >= 1 && COSTA_TR_STAGE <= 3 && !is_cpx<T>::value && S::FW == 1) {
+        if (flags & COSTA_TILE_TRANSPOSE) {
+            tr_tile_glds<T, S, NT>(op, f0, s0, src_base, dst_base, alpha, beta, tile);
+            return;
+        }
+    }
 
     // ---- load phase: lane -> (16-byte strip along f, column s); all loads issued first
     const int lf = (int(threadIdx.x) % S::LPC) * V;
@@ -570,6 +698,54 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
     };
     // beta != 0: the old destination values are requested now, overlapping the source loads
     // still in flight (not after the LDS exchange, one round trip per store unit)
+    if constexpr (FULL && COSTA_TR_STAGE == 4 && !is_cpx<T>::value && S::FW == 1 && S::PL % 2 == 0 &&
+                  S::PS % 2 == 0) {
+        if (kind != COSTA_SCALE_AXPBY) {
+            // two halves of rows: loads k < PL / 2 hold rows [0, BS / 2), store units k < PS / 2
+            // read only those
+            auto put = [&](int k0, int k1) {
+#pragma unroll
+                for (int k = k0; k < k1; ++k) {
+                    raw16 r;
+                    __builtin_memcpy(&r, &x[k], 16);
+                    *reinterpret_cast<raw16*>(tile + (c0 + k * S::CPP) * P + lf) = r;
+                }
+            };
+            vec<T> y[S::PS];
+            auto get = [&](int k0, int k1) {
+#pragma unroll
+                for (int k = k0; k < k1; ++k) {
+                    const int u = wave + S::NW * k;
+                    const int sc = u / QG, q = (u % QG) * FW + lane / SW;
+                    raw16 r = *reinterpret_cast<const raw16*>(tile + (sc * SW + lane % SW) * P + q * V);
+                    __builtin_memcpy(&y[k], &r, 16);
+                }
+            };
+            auto put_out = [&](int k0, int k1) {
+#pragma unroll
+                for (int k = k0; k < k1; ++k) {
+                    vec<T> o = lane_transpose(y[k], lane);
+                    int f, sb, n;
+                    unit(k, f, sb, n);
+                    if (kind != COSTA_SCALE_BITCOPY) {
+#pragma unroll
+                        for (int e = 0; e < V; ++e)
+                            o.e[e] = scale(o.e[e], e_zero<T>(), kind, conj, alpha, beta);
+                    }
+                    vstore<T, NT>(dst + f * ldd + sb, o, V, true);
+                }
+            };
+            put(0, S::PL / 2);
+            __syncthreads();
+            get(0, S::PS / 2);
+            put(S::PL / 2, S::PL);
+            put_out(0, S::PS / 2);
+            __syncthreads();
+            get(S::PS / 2, S::PS);
+            put_out(S::PS / 2, S::PS);
+            return;
+        }
+    }
     vec<T> old[S::PS];
     if (kind == COSTA_SCALE_AXPBY) {
 #pragma unroll
@@ -868,8 +1044,6 @@ struct lin {  // (f, s) of linear element index e = f + s*n, stepped by 64
 // (element (f, s) at s * pitch + f, pitch odd): an LDS-DMA instruction writes its 64 dwords
 // lane-linearly from a wave-uniform base, so lane j of instruction k takes dword 64 k + j of the
 // padded image and loads whatever source word belongs there (pad words: lane inactive).
-typedef __attribute__((address_space(3))) void lds_void;
-typedef const __attribute__((address_space(1))) void glob_void;
 template <typename T>
 __device__ __forceinline__ void tiny_stage(const T* src, int nf, int ns, int64_t lds, int pitch, int lane,
                                            T* t) {

@@ -225,8 +225,12 @@ typedef struct {
     int64_t host_groups; /* tile groups moved by the pipelined host staging */
     int64_t device_plans; /* plan-cache misses planned on the GPU (costa_hip_set_planner) */
     double plan_ms;       /* host wall time spent building plans (cache misses) */
-    int64_t host_direct;  /* host-resident calls whose buffers were page-locked: tiles moved by
-                             strided DMA between the caller's memory and HBM, no host copies */
+    int64_t host_direct;  /* host-resident calls whose buffers were page-locked and in which some
+                             tile groups moved by strided DMA between the caller's memory and
+                             HBM (no host copies for those groups) */
+    int64_t host_direct_groups; /* ... the tile groups that moved that way (PACK: a pack kernel
+                                   from the DMA'd source rectangle; LOCAL / UNPACK: kernels
+                                   writing the target rectangle's image, DMA'd back) */
 } costa_stats_t;
 int costa_hip_set_profiling(int on);
 int costa_hip_get_stats(costa_stats_t* out, int reset);

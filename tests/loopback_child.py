@@ -4,7 +4,9 @@ exchange rounds, merged tiles) go through PACK -> ncclSend/ncclRecv to self -> U
 (mode 2: half of the tiles, the rest through the concurrent LOCAL launch), then a loop of
 stream-ordered async transforms with A updated on torch's stream between them, then the golden
 cases and a 3000 x 2500 'T' alpha/beta case from host memory through both host staging schemes
-(pipelined: pack groups gathered into the send buffer, unpack groups scattered back).
+(pipelined: pack groups gathered into the send buffer, unpack groups scattered back), and again
+from page-locked memory (direct groups: source rectangles DMA'd up and packed on the GPU, unpack
+kernels writing target rectangles that are DMA'd back).  Prints 'DIRECT <groups>'.
 Prints one line per failure and a final 'OK <cases> <pack> <unpack> <local launches>'."""
 import os
 import sys
@@ -24,6 +26,16 @@ from golden_io import load, matches  # noqa: E402
 
 def dev(arr):
     return torch.from_numpy(np.ascontiguousarray(arr).view(np.uint8).copy()).cuda()
+
+
+def pinned(x, keep):
+    """a page-locked copy of numpy array x (torch's pinned allocator = hipHostMalloc); the
+    owning tensor is kept in `keep`"""
+    t = torch.empty(max(1, x.nbytes), dtype=torch.uint8, pin_memory=True)
+    a = t.numpy()[:x.nbytes].view(x.dtype)
+    a[:] = x
+    keep.append(t)
+    return a
 
 
 def main():
@@ -83,13 +95,18 @@ def main():
     # groups into the send buffer, exchanges with itself over RCCL and brings the unpack groups
     # back to host memory; the mirror scheme (mode 0) as a cross-check
     host_groups = 0
-    for hmode in (1, 0):
-        costa.set_host_staging(hmode)
+    direct_groups = 0
+    for hmode in (1, 0, "pinned"):
+        costa.set_host_staging(1 if hmode == "pinned" else hmode)
         g0 = costa.get_stats()["host_groups"]
+        d0 = costa.get_stats()["host_direct_groups"]
+        keep = []
         for case in all_cases():
             if case.P != 1:
                 continue
             bufs = [case.inputs(k, 0) for k in range(len(case.pairs))]
+            if hmode == "pinned":  # page-locked caller memory: groups move by strided DMA
+                bufs = [tuple(pinned(x, keep) for x in b) for b in bufs]
             As = [case.layout_A(k, 0, bufs[k][0].ctypes.data) for k in range(len(case.pairs))]
             Cs = [case.layout_C(k, 0, bufs[k][1].ctypes.data) for k in range(len(case.pairs))]
             eff = [case.effective(k) for k in range(len(case.pairs))]
@@ -104,6 +121,8 @@ def main():
         ha = rng.standard_normal(hm * hn)
         c0 = rng.standard_normal(hn * hm)
         hc = c0.copy()
+        if hmode == "pinned":
+            ha, hc = pinned(ha, keep), pinned(hc, keep)
         HA = costa.block_cyclic_layout(hm, hn, 512, 384, 1, 1, hm, hn, 1, 1, "R", 0, 0, ha, hm, "C", 0)
         HC = costa.block_cyclic_layout(hn, hm, 384, 512, 1, 1, hn, hm, 1, 1, "R", 0, 0, hc, hn, "C", 0)
         costa.transform(HA, HC, comm, "T", -0.75, 1.5)
@@ -111,11 +130,15 @@ def main():
         if not np.array_equal(hc.view(np.uint64), exp.view(np.uint64)):
             bad.append(f"host mode {hmode} {hm}x{hn} T axpby")
         groups = costa.get_stats()["host_groups"] - g0
-        if (groups > 0) != (hmode == 1):
+        if (groups > 0) != (hmode != 0):
             bad.append(f"host mode {hmode}: {groups} pipeline groups")
         host_groups += groups
+        if hmode == "pinned":
+            direct_groups = costa.get_stats()["host_direct_groups"] - d0
+        del keep
     costa.set_host_staging(1)
     print("HOST", host_groups)
+    print("DIRECT", direct_groups)
     st = costa.get_stats()
     for b in bad:
         print("FAIL", b)

@@ -73,6 +73,39 @@ def test_run_ranks_kills_a_hung_child_and_reports():
                                   "1": "ncclCommInitRank (RCCL 22606)"}
 
 
+def test_run_ranks_forwards_sigterm_to_the_ranks(tmp_path):
+    """SIGTERM to the parent (the driver's own timeout): the rank group, which runs in its own
+    session, is killed with it -- grandchildren included -- and the parent exits 128 + 15"""
+    import signal
+    import time
+    pidfile = tmp_path / "pids"
+    code = ("import os, sys, time, subprocess\n"
+            "g = subprocess.Popen([sys.executable, '-c', 'import time; time.sleep(600)'])\n"
+            f"open({str(pidfile)!r}, 'w').write(f'{{os.getpid()}} {{g.pid}}')\n"
+            "time.sleep(600)\n")
+    parent = subprocess.Popen([sys.executable, "-c",
+                               f"import bench; raise SystemExit(bench.run_ranks([{sys.executable!r}, '-c', "
+                               f"{code!r}], budget_s=300.0, n_gpus=2))"],
+                              cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    t0 = time.time()
+    while not pidfile.exists() or len(pidfile.read_text().split()) < 2:
+        assert time.time() - t0 < 60, "child did not start"
+        time.sleep(0.1)
+    pids = [int(x) for x in pidfile.read_text().split()]
+    parent.send_signal(signal.SIGTERM)
+    assert parent.wait(timeout=60) == 128 + signal.SIGTERM
+    for pid in pids:  # the rank and its grandchild are gone (reaped or zombie-free)
+        for _ in range(100):
+            try:
+                os.kill(pid, 0)
+            except ProcessLookupError:
+                break
+            time.sleep(0.1)
+        else:
+            os.kill(pid, signal.SIGKILL)
+            raise AssertionError(f"process {pid} outlived the parent's SIGTERM")
+
+
 def test_rank_watchdog_reports_phase_and_exits():
     """the in-rank watchdog (for ranks an outside launcher started): rank 0 prints the error line
     with its last phase and the process exits 124 while the main thread is blocked"""
@@ -87,6 +120,23 @@ def test_rank_watchdog_reports_phase_and_exits():
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["error"] == "timeout" and line["last_phase"] == {"0": "exchange"}
     assert "budget exceeded in phase 'exchange'" in r.stderr
+
+
+def test_watchdog_keeps_the_measured_headline():
+    """a hang after the headline was measured (an end-to-end or extra-config phase): the error
+    line still carries the headline value"""
+    code = ("import bench, time\n"
+            "bench._partial_line.update({'value': 123.5, 'ms_per_step': 0.7})\n"
+            "bench.phase(0, 'end-to-end from host memory')\n"
+            "bench.start_watchdog(0, 8, 1.0)\n"
+            "time.sleep(60)\n")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 124
+    import json
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["value"] == 123.5 and line["ms_per_step"] == 0.7 and line["n_gpus"] == 8
+    assert line["error"] == "timeout" and line["last_phase"] == {"0": "end-to-end from host memory"}
 
 
 def test_gpus_n_without_gpus_exits_nonzero():
@@ -231,3 +281,75 @@ def test_position_check_multirank(tmp_path, world, kind, corrupt):
         assert total == 0, f"{total} sampled positions differ on a correct transform"
     else:
         assert total > 0, f"the position check missed a {corrupt} error"
+
+
+def _e2e_worker(rank, world, port, corrupt, out_dir):
+    """bench.py's end-to-end leg at N ranks (host_layouts, e2e_leg, host_c_check) over host
+    arrays, the transform executed by the oracle with a gloo exchange at the product planner's
+    counts and displacements"""
+    sys.path.insert(0, ROOT)
+    import bench as B
+    import costa_amd as costa
+    import oracle
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n, b = 48, 8
+    pm, pn = B.grid_for(world)
+    pr, pc = rank // pn, rank % pn
+    M, N = n * pm, n * pn
+    ha = np.empty(n * n)
+    B.fill_bc(torch.from_numpy(ha), n, n, b, pm, pr, pn, pc, B.SEED_A, "f64", chunk_elems=500)
+    hc = np.zeros((N // pm) * (M // pn))
+    HA, HC = B.host_layouts(costa, ha, hc, M, N, b, pm, pn, rank)
+    calls = [0]
+
+    def call():  # one transform: pack -> all-to-all -> unpack, local
+        plan = costa.plan_export([HA], [HC], rank, world, ["T"], [1.0], [0.0])
+        send = np.zeros(max(1, plan.send_elems))
+        recv = np.zeros(max(1, plan.recv_elems))
+        oracle.exec_tile_ops(costa.DOUBLE, plan.pack_ops, plan.scalars, 0, send.ctypes.data)
+        st, rt = torch.from_numpy(send.view(np.uint8)), torch.from_numpy(recv.view(np.uint8))
+        sc = [int(x) * 8 for x in plan.send_counts]
+        rc = [int(x) * 8 for x in plan.recv_counts]
+        dist.all_to_all_single(rt[:sum(rc)], st[:sum(sc)], rc, sc)
+        if not (corrupt == "drop" and rank == 1):
+            oracle.exec_tile_ops(costa.DOUBLE, plan.unpack_ops, plan.scalars, recv.ctypes.data, 0)
+        oracle.exec_tile_ops(costa.DOUBLE, plan.local_ops, plan.scalars, 0, 0)
+        calls[0] += 1
+
+    def sum_over_ranks(x):
+        t = torch.tensor([x], dtype=torch.int64)
+        dist.all_reduce(t)
+        return int(t.item())
+
+    def max_over_ranks(x):
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    g = torch.Generator()
+    g.manual_seed(rank)
+    bytes_call = 2.0 * 8 * n * n * world
+    gb, ms, ok = B.e2e_leg(call, hc, lambda: B.host_c_check(hc, ha, M, N, b, pm, pn, rank, world, g,
+                                                              sum_over_ranks),
+                           bytes_call, dist.barrier, max_over_ranks, reps=2)
+    with open(os.path.join(out_dir, f"r{rank}.txt"), "w") as f:
+        f.write(f"{int(ok)} {calls[0]} {gb} {ms}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("corrupt", [None, "drop"])
+def test_e2e_host_leg_multirank(tmp_path, world, corrupt):
+    """the N-rank end-to-end code path of bench.py: per-rank host A / C, the transform, the
+    position check of the host C summed over ranks, the timed calls' max over ranks"""
+    mp.spawn(_e2e_worker, args=(world, _free_port(), corrupt, str(tmp_path)), nprocs=world, join=True)
+    res = [(tmp_path / f"r{r}.txt").read_text().split() for r in range(world)]
+    oks = {int(x[0]) for x in res}
+    assert len(oks) == 1  # every rank reports the same verdict
+    assert oks.pop() == (0 if corrupt else 1)
+    assert all(int(x[1]) == 3 for x in res)  # checked call + 2 timed
+    assert len({(x[2], x[3]) for x in res}) == 1 and float(res[0][2]) > 0  # max over ranks

@@ -6,6 +6,9 @@ rank's host buffers) through both host staging modes of engine.cpp / host_pipe.c
 Both must match the reference bit for bit (0 ulp: contraction is off), leave every
 byte of C the transform does not write untouched, and mode 1 must actually run the pipeline
 (costa_stats_t::host_groups)."""
+import json
+import os
+
 import numpy as np
 import pytest
 
@@ -38,6 +41,8 @@ def _with_mode(costa, mode, fn):
 
 
 SINGLE = [c for c in all_cases() if c.P == 1]
+_DX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "host_direct.json")
+DIRECT_EXPECTED = json.load(open(_DX)) if os.path.exists(_DX) else {}
 
 
 @pytest.mark.parametrize("mode", [1, 0])
@@ -160,9 +165,21 @@ def test_golden_host_pinned(gpu, case):
         key = f"C{k}_r0"
         got = keep[k][2]
         assert matches(fx, key, got), f"{case.name} {key}: " + first_mismatch(fx, key, got)
-    # (direct DMA only where every group's footprints are rectangles of the caller's arrays;
-    # the rest of these cases run the copying pipeline from page-locked memory)
-    assert st["host_direct"] <= st["transforms"]
+    # direct DMA for the groups whose footprints are rectangles of the caller's arrays, the
+    # copying pipeline for the rest, in the same call.  How many groups go direct is fixed by the
+    # plan (deterministic): recorded per case in tests/golden/host_direct.json on the GPU
+    # (COSTA_RECORD_HOST_DIRECT=<file> writes the counts instead of checking them)
+    d = st["host_direct_groups"]
+    assert d <= st["host_groups"] and (st["host_direct"] > 0) == (d > 0)
+    rec = os.environ.get("COSTA_RECORD_HOST_DIRECT")
+    if rec:
+        with open(rec, "a") as f:
+            f.write(json.dumps({case.name: [int(d), int(st["host_groups"])]}) + "\n")
+        return
+    assert case.name in DIRECT_EXPECTED, f"{case.name}: no recorded direct-group count"
+    assert [d, st["host_groups"]] == DIRECT_EXPECTED[case.name], case.name
+    if case.name == "block_cyclic":  # whole block-cyclic matrices: every group is a rectangle
+        assert d == st["host_groups"] >= 1
 
 
 @pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))

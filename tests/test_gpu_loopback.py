@@ -35,6 +35,9 @@ def test_loopback_exchange_matches_golden(mode, slot, planner):
     assert r.returncode == 0 and out and out[-1].startswith("OK"), r.stdout + r.stderr
     host = [l for l in out if l.startswith("HOST")]
     assert host and int(host[-1].split()[1]) > 0, "pipelined host staging did not run"
+    direct = [l for l in out if l.startswith("DIRECT")]
+    # page-locked host cases: pack / unpack groups moved by strided DMA (one rectangle per group)
+    assert direct and int(direct[-1].split()[1]) > 0, "no direct (DMA) group ran from page-locked memory"
     _, n, packs, unpacks, locals_ = out[-1].split()
     assert int(packs) >= int(n) and int(unpacks) >= int(n), out[-1]  # every case exchanged
     if mode == "1":

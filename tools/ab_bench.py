@@ -40,7 +40,8 @@ def main():
             d = json.loads(lines[-1])
             ro = d.get("roofline") or {}
             msg = (f"{label:24s} rep {r}: kernel {ro.get('avg_launch_ms')} ms  value {d.get('value')} GB/s  "
-                   f"frac {ro.get('frac')}  verified {d.get('verified')}")
+                   f"frac {ro.get('frac')}  of_ceiling {ro.get('frac_of_ceiling')}  "
+                   f"ceiling {(ro.get('copy_ceiling') or {}).get('best_GBps')}  verified {d.get('verified')}")
             print(msg, flush=True)
             log.write(msg + "\n")
             log.flush()
