@@ -476,6 +476,24 @@ def e2e_leg(call, hc, check, bytes_call: float, barrier, max_over_ranks, reps: i
     return round(bytes_call / te / 1e9, 2), round(te * 1e3, 2), ok
 
 
+def pass_fracs(bytes_per_launch: float, launches_per_step: float, avg_launch_ms: float,
+               ms_per_step: float, events_ms_per_step: float) -> dict:
+    """The roofline fraction of each timing pass, so that no figure mixes passes: `frac` (the
+    line's roofline.frac) = bytes per launch over the kernel's own average duration, from the
+    events pass, beside that pass's step time (the kernels of a step fit inside it);
+    `frac_value_pass` = the same step's bytes over ms_per_step, the events-off pass `value` comes
+    from (its step time bounds its kernel time from above, so this frac is the lower one)."""
+    return {
+        "events_pass_ms_per_step": round(events_ms_per_step, 4),
+        "frac_value_pass": (round(bytes_per_launch * launches_per_step / (ms_per_step * 1e-3) / 1e9
+                                  / HBM_PEAK_GBPS, 4) if ms_per_step > 0 else None),
+        "avg_launch_ms_note": (
+            "frac and avg_launch_ms: the events pass (events_pass_ms_per_step, the same K steps with "
+            "a HIP event pair around every phase; kernel time per step <= that step time); "
+            "frac_value_pass: the bytes of a step over ms_per_step, the events-off pass of `value`"),
+    }
+
+
 def copy_ceiling(src, dst, col_bytes: int, reps: int = 20):
     """SURVEY §8(d)'s measured ceiling: what plain device copies of the headline's bytes reach on
     this box, in this process, after the timed region (src -> dst, both device buffers of the
@@ -507,14 +525,10 @@ def copy_ceiling(src, dst, col_bytes: int, reps: int = 20):
     return out
 
 
-def cfg5_workload(costa, torch, rank, world, op):
-    """BASELINE configs[4] (SURVEY §8d): fp32 16384^2 custom_layout; A tile edges uniform in
-    [8, 96] (seeds 0xC5A1 rows / 0xC5A2 cols), C edges uniform in [16, 160] (0xC5A3 / 0xC5A4),
-    owners uniform over the ranks (0xC5A5 for A, 0xC5A6 for C); every owned block is its own
-    column-major buffer (ld = rows) in a 256-byte-aligned arena.  numpy PCG64 streams are used
-    for the draws.  op 'N' alpha=1 beta=0, or the 'T' variant alpha=-0.5 beta=2."""
+def cfg5_splits(n: int = 16384):
+    """BASELINE configs[4]'s block edges: A rows / cols uniform in [8, 96] (seeds 0xC5A1 /
+    0xC5A2), C rows / cols uniform in [16, 160] (0xC5A3 / 0xC5A4), numpy PCG64 streams"""
     import numpy as np
-    n = 16384
 
     def splits(seed, lo, hi):
         r = np.random.default_rng(seed)
@@ -522,9 +536,75 @@ def cfg5_workload(costa, torch, rank, world, op):
         while s[-1] < n:
             s.append(min(n, s[-1] + int(r.integers(lo, hi + 1))))
         return s
+    return (splits(0xC5A1, 8, 96), splits(0xC5A2, 8, 96), splits(0xC5A3, 16, 160),
+            splits(0xC5A4, 16, 160))
 
-    ars, acs = splits(0xC5A1, 8, 96), splits(0xC5A2, 8, 96)
-    crs, ccs = splits(0xC5A3, 16, 160), splits(0xC5A4, 16, 160)
+
+def cpu_baseline_configs(items, target_s: float = 8.0):
+    """The REFERENCE's own OpenMP path beside each BASELINE config the run measures
+    (baseline_configs): oracle/_ref/ref_harness bench_cfg3 / bench_c128 / bench_custom on one rank
+    with every CPU this job may use -- cfg 3 a 16384^2 fp64 'N' copy slice (128^2 blocks), cfg 4 a
+    16384^2 complex<double> 'T' alpha, beta slice (128^2 blocks), cfg 5 the full 16384^2 custom
+    layouts ('N' or 'T').  Child processes, started before this process touches the GPU.
+    -> {entry key: cpu_baseline dict}; configs the binary cannot run are left out (warning)."""
+    import subprocess
+    import tempfile
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(exe):
+        print("bench.py: WARNING oracle/_ref/ref_harness is absent: no CPU baseline beside the "
+              "extra configs", file=sys.stderr)
+        return {}
+    threads, info = host_cpus()
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+    out = {}
+    for key, kind, edge in items:
+        spec = None
+        if kind == "cfg3":
+            args = ["bench_cfg3", "16384", "128"]
+            sample = "a 16384x16384 fp64 slice of configs[2], 128x128 blocks, op N (no-scale copy)"
+        elif kind == "cfg4":
+            args = ["bench_c128", "16384", "128"]
+            sample = ("a 16384x16384 complex<double> slice of configs[3], 128x128 blocks, op T, "
+                      "alpha=(0.75,-0.5) beta=(1.25,0.25); the first call checked every 97th element")
+        elif kind == "cfg5":
+            op = edge if edge in ("N", "T") else "N"
+            fd, spec = tempfile.mkstemp(suffix=".txt")
+            with os.fdopen(fd, "w") as f:
+                for v in cfg5_splits():
+                    f.write(f"{len(v)} " + " ".join(map(str, v)) + "\n")
+            args = ["bench_custom", spec, op]
+            sample = (f"configs[4]'s full 16384x16384 fp32 custom layouts on one rank, op {op}; the "
+                      f"first call checked against the definition on every 7th column")
+        else:
+            continue
+        try:
+            r = subprocess.run([exe] + args + [str(target_s)], capture_output=True, text=True,
+                               timeout=6 * target_s + 240, env=env)
+            d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+            if r.returncode != 0 or not d.get("verified"):
+                raise RuntimeError(f"rc {r.returncode}, verified {d.get('verified')}")
+        except Exception as e:
+            print(f"bench.py: WARNING reference CPU baseline of {key} failed ({e})", file=sys.stderr)
+            continue
+        finally:
+            if spec:
+                os.unlink(spec)
+        out[key] = {"value": round(d["GBps"], 3), "unit": "GB/s", "cores": d["threads"],
+                    "kind": "reference",
+                    "sample": f"{sample}: the reference's costa::transform (planning included, as "
+                              f"every reference call re-plans), {d['reps']} calls in "
+                              f"{d['seconds']:.1f} s, OpenMP {d['threads']} threads, verified"}
+    return out
+
+
+def cfg5_workload(costa, torch, rank, world, op):
+    """BASELINE configs[4] (SURVEY §8d): fp32 16384^2 custom_layout; A tile edges uniform in
+    [8, 96] (seeds 0xC5A1 rows / 0xC5A2 cols), C edges uniform in [16, 160] (0xC5A3 / 0xC5A4),
+    owners uniform over the ranks (0xC5A5 for A, 0xC5A6 for C); every owned block is its own
+    column-major buffer (ld = rows) in a 256-byte-aligned arena.  numpy PCG64 streams are used
+    for the draws.  op 'N' alpha=1 beta=0, or the 'T' variant alpha=-0.5 beta=2."""
+    import numpy as np
+    ars, acs, crs, ccs = cfg5_splits()
     aown = np.random.default_rng(0xC5A5).integers(0, world, (len(ars) - 1, len(acs) - 1))
     cown = np.random.default_rng(0xC5A6).integers(0, world, (len(crs) - 1, len(ccs) - 1))
 
@@ -646,8 +726,26 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "pxtran"
-    # the reference's own CPU path, as a child process before anything touches the GPU
+    # BASELINE's other configurations, measured after the headline in the same processes: at
+    # the GPU counts they are quoted on (cfg 3 at 4 GPUs, cfg 4 and cfg 5 at 8), and at one GPU
+    # their single-GPU slices, each beside the reference's own CPU rate
+    extra_plan = {1: [("cfg3", None), ("cfg4", 32768), ("cfg5", "N"), ("cfg5", "T")],
+                  4: [("cfg3", None)], 8: [("cfg4", 32768), ("cfg5", "N")]}
+    plan_x = extra_plan.get(world, [])
+    if args.extra:
+        plan_x = []
+        for item in args.extra.split(","):
+            k, _, e = item.partition(":")
+            plan_x.append((k, (int(e) if e.isdigit() else e) if e else None))
+    if args.workload != "pxtran" or args.no_extra:
+        plan_x = []
+    keys_x = []  # (entry key, config, edge / op)
+    for kind, edge in plan_x:
+        used = {k for k, _, _ in keys_x}
+        keys_x.append((kind if kind not in used else f"{kind}_{edge}", kind, edge))
+    # the reference's own CPU path, as child processes before anything touches the GPU
     cpu_ref = cpu_baseline_reference(n=args.edge, b=args.block) if want_cpu else None
+    cpu_x = cpu_baseline_configs(keys_x) if want_cpu and keys_x else {}
     import torch
     import torch.distributed as dist
     import costa_amd as costa
@@ -964,10 +1062,8 @@ def main():
             "bytes_per_launch": int(per_launch),
             "avg_launch_ms": round(avg_ms, 4)}
 
-    roof["events_pass_ms_per_step"] = round(el_ev / args.steps * 1e3, 4)
-    roof["avg_launch_ms_note"] = (
-        "avg_launch_ms comes from the events pass (events_pass_ms_per_step, the same K steps "
-        "with a HIP event pair around every phase); ms_per_step / value from the events-off pass")
+    roof.update(pass_fracs(per_launch, kl / args.steps, avg_ms, el / args.steps * 1e3,
+                           el_ev / args.steps * 1e3))
     # the copy ceiling of the same bytes on this box, measured after the timed
     # region (it overwrites C, whose checks have run)
     if world == 1 and args.workload == "pxtran":
@@ -1076,20 +1172,12 @@ def main():
             costa.transform(SA, SC, comm, "T", 1.0, 0.0)
         overhead_us = round((time.perf_counter() - t1) / 200 * 1e6, 1)
 
-    # BASELINE's multi-GPU configurations at the GPU counts they are quoted on (the driver runs
-    # only `bench.py --gpus N`): cfg 3 at 4 GPUs, cfg 4 and cfg 5 at 8 GPUs
+    # BASELINE's other configurations (plan_x above; the driver runs only `bench.py --gpus N`)
     extra = {}
-    extra_plan = {4: [("cfg3", None)], 8: [("cfg4", 32768), ("cfg5", "N")]}
-    plan_x = extra_plan.get(world, [])
-    if args.extra:
-        plan_x = []
-        for item in args.extra.split(","):
-            k, _, e = item.partition(":")
-            plan_x.append((k, (int(e) if e.isdigit() else e) if e else None))
-    if args.workload == "pxtran" and not args.no_extra and plan_x:
+    if keys_x:
         for key in ("LA", "LC", "check"):
             wmain.pop(key, None)
-        for kind, edge in plan_x:
+        for key, kind, edge in keys_x:
             costa.release_caches()
             torch.cuda.empty_cache()
             phase(rank, f"extra config {kind}:{edge}: build")
@@ -1097,11 +1185,17 @@ def main():
             phase(rank, f"extra config {kind}:{edge}: measure")
             ksteps = max(1, min(args.steps, 5 if kind != "cfg5" else 10))
             rx = measure(wx, ksteps, 1)
-            key = kind if kind not in extra else f"{kind}_{edge}"
             extra[key] = summary(wx, rx, ksteps)
+            if key in cpu_x:
+                extra[key]["cpu_baseline"] = cpu_x[key]
+            elif world > 1:
+                extra[key]["cpu_baseline"] = ("measured at N = 1 only (rank 0's host cores): the "
+                                              "one-GPU line's baseline_configs entry of this config")
             del wx, rx
             costa.release_caches()
             torch.cuda.empty_cache()
+            if rank == 0:
+                _partial_line.setdefault("baseline_configs", {})[key] = extra[key]
 
     phase(rank, "report")
     cpu = None

@@ -588,6 +588,129 @@ void host_parallel(size_t n, F fn) {
 }  // namespace
 
 namespace {
+// Destination-block groups (r5, tile_kernels.hip cblock_kernel).  Among the ops bound for the
+// wavefront path, those whose destination footprints (same leading dimension R) overlap or touch
+// form components; a component whose ops tile R x K elements exactly -- whole columns of a
+// buffer whose leading dimension is R: a custom layout's own block buffer (cfg 5), or several of
+// them back to back -- is one contiguous destination range, written by one workgroup in 16-byte
+// vectors instead of one element a lane per wavefront piece.  Components above the workgroup's
+// budget (cblock_max_elems) are cut into column bands, their ops cut at the band edges (a
+// sub-rectangle of a tile op is a tile op).  Ops of a component must share one transform (flags
+// apart from the vector bits).  Emitted into `ordered` as [header, ops...] per group (header: src
+// = number of ops, dst = the range, nf = R, ns = K, flags = the transform); `work` gets the
+// header indices in destination order; the grouped ops leave `wave_ops`.  COSTA_CBLOCK=0
+// (tuning): off.
+int64_t cblock_groups(costa_dtype_t dtype, std::vector<const costa_tile_op_t*>& wave_ops, list_kind kind,
+                      std::vector<costa_tile_op_t>& ordered, std::vector<uint64_t>& work, int64_t& lds) {
+    static const int on = [] {
+        const char* s = tuning_env("COSTA_CBLOCK");
+        return s ? std::atoi(s) : 1;
+    }();
+    lds = 0;
+    // real types (complex elements are on the large shapes wherever it matters: cfg 4)
+    const bool real = dtype == COSTA_FLOAT || dtype == COSTA_DOUBLE || dtype == COSTA_INT32;
+    if (!on || !real || kind == list_pack || wave_ops.size() < 2) return 0;
+    const int64_t E = int64_t(dtype_size(dtype));
+    const uint32_t vec_bits = COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST;
+    const int64_t budget = cblock_max_elems(E);
+    struct cand {
+        uint64_t lo, hi;
+        int32_t ldd;
+        uint32_t i;
+    };
+    std::vector<cand> cs;
+    cs.reserve(wave_ops.size());
+    for (uint32_t i = 0; i < wave_ops.size(); ++i) {
+        const costa_tile_op_t& op = *wave_ops[i];
+        if (op.nf <= 0 || op.ns <= 0 || op.ldd <= 0 || op.dst % uint64_t(E) != 0) continue;
+        const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
+        const int64_t run = tr ? op.ns : op.nf, runs = tr ? op.nf : op.ns;
+        if (run > op.ldd || op.ldd > budget) continue;
+        cs.push_back({op.dst, op.dst + uint64_t(((runs - 1) * int64_t(op.ldd) + run) * E), op.ldd, i});
+    }
+    std::sort(cs.begin(), cs.end(), [](const cand& a, const cand& b) {
+        return a.ldd != b.ldd ? a.ldd < b.ldd : a.lo < b.lo;
+    });
+    std::vector<char> taken(wave_ops.size(), 0);
+    struct group {
+        uint64_t dst;
+        std::vector<costa_tile_op_t> ops;
+        int32_t R, K;
+        uint32_t flags;
+    };
+    std::vector<group> out;
+    for (size_t a = 0; a < cs.size();) {
+        size_t b = a + 1;
+        uint64_t hi = cs[a].hi;
+        while (b < cs.size() && cs[b].ldd == cs[a].ldd && cs[b].lo <= hi) hi = std::max(hi, cs[b].hi), ++b;
+        const size_t a0 = a;
+        a = b;
+        if (b - a0 < 2) continue;
+        const int64_t R = cs[a0].ldd;
+        const uint64_t base = cs[a0].lo;
+        const costa_tile_op_t& first = *wave_ops[cs[a0].i];
+        const uint32_t fl = first.flags & ~vec_bits;
+        int64_t area = 0, K = 0;
+        bool ok = true;
+        for (size_t k = a0; k < b && ok; ++k) {
+            const costa_tile_op_t& op = *wave_ops[cs[k].i];
+            const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
+            const int64_t run = tr ? op.ns : op.nf, runs = tr ? op.nf : op.ns;
+            const int64_t e = int64_t(op.dst - base) / E;
+            ok = (op.flags & ~vec_bits) == fl && e % R + run <= R;
+            area += run * runs;
+            K = std::max(K, e / R + runs);
+        }
+        if (!ok || area != R * K || K > INT32_MAX) continue;
+        // column bands of at most `budget` elements
+        const int64_t KB = std::max<int64_t>(1, budget / R);
+        for (int64_t cb0 = 0; cb0 < K; cb0 += KB) {
+            const int64_t cb1 = std::min(K, cb0 + KB);
+            group g{base + uint64_t(cb0 * R * E), {}, int32_t(R), int32_t(cb1 - cb0), fl};
+            for (size_t k = a0; k < b; ++k) {
+                costa_tile_op_t op = *wave_ops[cs[k].i];
+                const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
+                const int64_t c0 = int64_t(op.dst - base) / E / R;
+                const int64_t runs = tr ? op.nf : op.ns;
+                const int64_t lo = std::max(cb0, c0), up = std::min(cb1, c0 + runs);
+                if (lo >= up) continue;
+                const int64_t d0 = lo - c0, dn = up - lo;  // destination columns of the op kept
+                op.dst += uint64_t(d0 * R * E);
+                if (tr) {  // destination columns = source f
+                    op.src += uint64_t(d0 * E);
+                    op.nf = int32_t(dn);
+                } else {  // destination columns = source s
+                    op.src += uint64_t(d0 * int64_t(op.lds) * E);
+                    op.ns = int32_t(dn);
+                }
+                g.ops.push_back(op);
+            }
+            out.push_back(std::move(g));
+        }
+        for (size_t k = a0; k < b; ++k) taken[cs[k].i] = 1;
+    }
+    if (out.empty()) return 0;
+    std::sort(out.begin(), out.end(), [](const group& x, const group& y) { return x.dst < y.dst; });
+    for (auto& g : out) {
+        costa_tile_op_t h{};
+        h.src = g.ops.size();
+        h.dst = g.dst;
+        h.nf = g.R;
+        h.ns = g.K;
+        h.ldd = g.R;
+        h.flags = g.flags;
+        work.push_back(uint64_t(ordered.size()));
+        ordered.push_back(h);
+        ordered.insert(ordered.end(), g.ops.begin(), g.ops.end());
+        lds = std::max(lds, int64_t(g.R | 1) * g.K);
+    }
+    size_t o = 0;
+    for (size_t i = 0; i < wave_ops.size(); ++i)
+        if (!taken[i]) wave_ops[o++] = wave_ops[i];
+    wave_ops.resize(o);
+    return int64_t(out.size());
+}
+
 struct wave_knobs {  // defaults, overridable for tuning runs
     int policy = 2;  // COSTA_WAVE_POLICY 1: every op below the large threshold takes the wave
                      // path; 2: also large ops that are not 16-byte aligned on both sides, up to
@@ -955,6 +1078,9 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         }
         n_work[c] = int64_t(work.size() - w0);
     }
+    // destination-block groups out of the wavefront ops (after the skew items in `work`)
+    int64_t cblock_lds = 0;
+    const int64_t n_cblock = cblock_groups(dtype, wave_ops, kind, ordered, work, cblock_lds);
     // ops are independent (disjoint destinations), so any order is valid; neighbours in
     // memory run at the same time and share the partially used cache lines at their edges.
     // The wavefront ops are ordered first, then cut into their pieces straight into the ordered
@@ -1041,6 +1167,8 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     w.n_medium = n_work[1];
     w.n_skew = n_work[2];
     w.skew_wide = skew_wide && n_work[2] > 0;
+    w.n_cblock = n_cblock;
+    w.cblock_lds = cblock_lds;
 
     w.tiny_first = int64_t(ordered.size());
     w.n_tiny = int64_t(at_piece[nw]);
@@ -1062,6 +1190,8 @@ launch_args make_launch(const work_split& w, const void* d_ordered, const void* 
     a.n_large = w.n_large;
     a.n_medium = w.n_medium;
     a.n_skew = w.n_skew;
+    a.n_cblock = w.n_cblock;
+    a.cblock_lds = w.cblock_lds;
     a.tiny_first = w.tiny_first;
     a.n_tiny = w.n_tiny;
     a.src_base = src_base;

@@ -189,6 +189,8 @@ struct launch_args {
     int64_t n_large;        // work items using the large sub-tile shape
     int64_t n_medium;       // then work[n_large, n_large + n_medium): the medium shape
     int64_t n_skew = 0;     // then n_skew items of the skew shape (unaligned destinations)
+    int64_t n_cblock = 0;   // then n_cblock destination-block groups: index of the group's header op
+    int64_t cblock_lds = 0; // LDS image of the largest group (elements)
     int64_t tiny_first;     // ops[tiny_first, tiny_first + n_tiny) run one per wavefront
     int64_t n_tiny;
     const char* src_base;
@@ -206,6 +208,11 @@ struct launch_args {
 bool any_transpose(const std::vector<costa_tile_op_t>& ops);
 bool any_axpby(const std::vector<costa_tile_op_t>& ops);
 void launch_tiles(costa_dtype_t dtype, const launch_args& a, void* stream /* hipStream_t */);
+// destination-block groups (tile_kernels.hip cblock_kernel): threads per workgroup and 16-byte
+// destination vectors per thread; a group holds at most kCblockThreads * kCblockChunks vectors
+constexpr int kCblockThreads = 256;
+constexpr int kCblockChunks = 8;
+inline int64_t cblock_max_elems(int64_t E) { return int64_t(kCblockThreads) * kCblockChunks * (16 / E); }
 // sub-tile shapes (elements along the source's fast dim, along its slow dim) of a copy-only list
 // or of a list with transposing ops: the large shape, the medium one (bf_m = bs_m = 0: none) and
 // the large shape's square variant for lists whose large ops all fit it (bf_q = bs_q = 0: none),
@@ -223,6 +230,8 @@ void tile_shapes(costa_dtype_t dtype, bool transposing_list, shape_dims* out);
 struct work_split {
     int64_t n_large = 0, n_medium = 0, tiny_first = 0, n_tiny = 0;
     int64_t n_skew = 0;     // skew-shape work items, after the medium ones
+    int64_t n_cblock = 0;   // destination-block groups, after the skew items (cblock_groups)
+    int64_t cblock_lds = 0; // elements of the largest group's LDS image
     bool tr_shape = false;  // sub-tiles cut with tile_shapes(dtype, true, ...)
     bool sq = false;        // ... the large ops with its square variant (bf_q x bs_q)
     bool full = false;      // every large op of a transposing list is aligned and a whole number
@@ -230,7 +239,7 @@ struct work_split {
     bool med_full = false;  // the same for the medium ops and the medium sub-tile
     bool med_sq = false;    // the medium class runs on 32 x 32 sub-tiles (bf_s x bs_s)
     bool skew_wide = false; // the skew items are sub-tiles of its wide variant (bf_kw x bs_kw)
-    int64_t n_items() const { return n_large + n_medium + n_skew + n_tiny; }
+    int64_t n_items() const { return n_large + n_medium + n_skew + n_cblock + n_tiny; }
 };
 // list_pack: the ops write the dense send package (their destinations are contiguous whatever
 // their order), which changes the wavefront ops' order (wave_knobs::sort); local lists (both

@@ -1179,6 +1179,160 @@ __device__ __forceinline__ void tiny_op(const costa_tile_op_t& op, int lane, T* 
     tiny_transpose_glds<T, AX>(src, dst, nf, ns, lds, ldd, kind, conj, alpha, beta, lane, t);
 }
 
+// ---------------------------------------------------------------- destination blocks (r5)
+// A group = the ops of a list that together write one contiguous destination range: R rows x K
+// columns of a column-major buffer whose leading dimension is R (a custom layout's own block
+// buffer, or a column band of it; engine.cpp cblock_groups).  One workgroup per group:
+//   load   every wavefront walks its share of the group's ops in source order (lanes along the
+//          source's contiguous dimension, U elements a lane in flight) and writes each element
+//          to its destination position in an LDS image of the range (column pitch R | 1: the
+//          transposed writes are conflict-free)
+//   store  the range in 16-byte vectors at 16-byte aligned addresses, old values (beta != 0)
+//          requested before the barrier, element-wise only at the two ends
+// Every destination granule inside the range is written by this workgroup alone, in whole
+// 16-byte vectors: the wavefront path writes cfg 5's destination columns one element a lane,
+// each granule shared by the tiles of two source blocks (cfg 5).
+// Header op (work item): src = number of ops that follow it, dst = the range, nf = R, ns = K,
+// flags = the transform of every op of the group.
+constexpr int CB_NT = kCblockThreads;              // threads per workgroup
+constexpr int CB_CHUNKS = kCblockChunks;           // 16-byte destination vectors per thread
+constexpr int CB_U = 16;                           // source elements a lane has in flight
+
+template <typename T, bool TR, bool AX>
+__global__ __launch_bounds__(CB_NT) void cblock_kernel(const costa_tile_op_t* __restrict__ ops,
+                                                       const uint64_t* __restrict__ work,
+                                                       const char* src_base, char* dst_base,
+                                                       const T* __restrict__ scalars) {
+    constexpr int V = 16 / int(sizeof(T)), NW = CB_NT / 64;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    T* img = reinterpret_cast<T*>(smem);
+    const uint64_t h = work[blockIdx.x];
+    const costa_tile_op_t hd = ops[h];
+    const int n_ops = int(hd.src), R = hd.nf, K = hd.ns, P = R | 1;
+    const uint32_t flags = hd.flags;
+    const uint32_t kind = (flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT;
+    const bool conj = flags & COSTA_TILE_CONJ;
+    const bool tr = TR && (flags & COSTA_TILE_TRANSPOSE);
+    const uint32_t slot = flags >> COSTA_SLOT_SHIFT;
+    T alpha = e_zero<T>(), beta = e_zero<T>();
+    if (kind >= COSTA_SCALE_ALPHA) {
+        alpha = scalars[2 * slot];
+        beta = scalars[2 * slot + 1];
+    }
+    const int lane = int(threadIdx.x) % 64;
+    const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / 64);
+    T* dst = reinterpret_cast<T*>(dst_base + hd.dst);
+    const int total = R * K;
+    // 16-byte vectors of the range: vector c holds elements [V c - mis, V c - mis + V)
+    const int mis = int((reinterpret_cast<uintptr_t>(dst) / sizeof(T)) & uintptr_t(V - 1));
+    const int nvec = (total + mis + V - 1) / V;
+    vec<T> old[CB_CHUNKS];
+    if (AX && kind == COSTA_SCALE_AXPBY) {  // old values, in flight with the source loads
+#pragma unroll
+        for (int k = 0; k < CB_CHUNKS; ++k) {
+            const int c = int(threadIdx.x) + CB_NT * k;
+            const int e0 = V * c - mis;
+            if (c >= nvec) break;
+            if (e0 >= 0 && e0 + V <= total) {
+                raw16 r = *reinterpret_cast<const raw16*>(dst + e0);
+                __builtin_memcpy(&old[k], &r, 16);
+            } else {
+#pragma unroll
+                for (int e = 0; e < V; ++e)
+                    if (e0 + e >= 0 && e0 + e < total) old[k].e[e] = dst[e0 + e];
+            }
+        }
+    }
+    // ---- sources -> image (element (r, c) of the range at c * P + r)
+    for (int i = wave; i < n_ops; i += NW) {
+        const costa_tile_op_t op = ops[h + 1 + uint64_t(i)];
+        const T* src = reinterpret_cast<const T*>(src_base + op.src);
+        const int64_t e0 = int64_t(op.dst - hd.dst) / int64_t(sizeof(T));
+        const int r0 = int(e0 % R), c0 = int(e0 / R);
+        const int nf = op.nf, n = op.nf * op.ns;
+        const int64_t lds = op.lds;
+        // image position of source element (f, s): transpose (r0 + s, c0 + f), copy (r0 + f, c0 + s)
+        const int di_f = tr ? P : 1, di_s = tr ? 1 : P;
+        const int ibase = c0 * P + r0;
+        lin<T> p(lane, nf);
+        for (int b = 0; b < n; b += 64 * CB_U) {
+            T x[CB_U];
+            int at[CB_U];
+#pragma unroll
+            for (int u = 0; u < CB_U; ++u) {
+                if (b + u * 64 >= n) break;
+                at[u] = -1;
+                if (b + u * 64 + lane < n) {
+                    x[u] = src[p.s * lds + p.f];
+                    at[u] = ibase + p.f * di_f + p.s * di_s;
+                }
+                p.step();
+            }
+#pragma unroll
+            for (int u = 0; u < CB_U; ++u) {
+                if (b + u * 64 >= n) break;
+                if (at[u] >= 0) img[at[u]] = x[u];
+            }
+        }
+    }
+    __syncthreads();
+    // ---- image -> the range, 16-byte vectors
+#pragma unroll
+    for (int k = 0; k < CB_CHUNKS; ++k) {
+        const int c = int(threadIdx.x) + CB_NT * k;
+        if (c >= nvec) break;
+        const int e0 = V * c - mis;
+        const int first = e0 < 0 ? -e0 : 0;  // elements of the vector inside the range
+        int r = (e0 + first) % R, col = (e0 + first) / R;
+        vec<T> o;
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+            if (e < first || e0 + e >= total) continue;
+            T v = img[col * P + r];
+            if (kind != COSTA_SCALE_BITCOPY)
+                v = scale(v, AX && kind == COSTA_SCALE_AXPBY ? old[k].e[e] : e_zero<T>(), kind, conj,
+                          alpha, beta);
+            o.e[e] = v;
+            if (++r == R) {
+                r = 0;
+                ++col;
+            }
+        }
+        if (e0 >= 0 && e0 + V <= total) {
+            raw16 w;
+            __builtin_memcpy(&w, &o, 16);
+            st16<true>(dst + e0, w);
+        } else {
+#pragma unroll
+            for (int e = 0; e < V; ++e)
+                if (e0 + e >= 0 && e0 + e < total) dst[e0 + e] = o.e[e];
+        }
+    }
+}
+
+template <typename T, bool TR, bool AX>
+void launch_cblock_v(const launch_args& a, const uint64_t* work, int64_t n, hipStream_t stream) {
+    const size_t lds = size_t(a.cblock_lds) * sizeof(T);
+    const int64_t max_grid = 1LL << 30;
+    for (int64_t off = 0; off < n; off += max_grid) {
+        const int64_t m = std::min(max_grid, n - off);
+        hipLaunchKernelGGL((cblock_kernel<T, TR, AX>), dim3(unsigned(m)), dim3(CB_NT), lds, stream, a.ops,
+                           work + off, a.src_base, a.dst_base, static_cast<const T*>(a.scalars));
+    }
+}
+template <typename T>
+void launch_cblock(const launch_args& a, const uint64_t* work, int64_t n, hipStream_t stream) {
+    if (n <= 0) return;
+    if constexpr (is_cpx<T>::value) {  // real types only (engine.cpp cblock_groups)
+        throw error(COSTA_ERR_INTERNAL, "costa: destination-block groups of a complex type");
+    } else if (a.any_transpose)
+        a.any_axpby ? launch_cblock_v<T, true, true>(a, work, n, stream)
+                    : launch_cblock_v<T, true, false>(a, work, n, stream);
+    else
+        a.any_axpby ? launch_cblock_v<T, false, true>(a, work, n, stream)
+                    : launch_cblock_v<T, false, false>(a, work, n, stream);
+}
+
 // One op per wavefront.  Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md,
 // workgroup dispatch); they are renumbered so that each XCD walks one contiguous slice of the
 // locality-ordered list, and neighbouring ops (which share partially written cache lines) meet
@@ -1266,6 +1420,7 @@ void launch_t(const launch_args& a, hipStream_t stream) {
             launch_shape<T, typename shapes<T>::medium_tr>(a, a.work + a.n_large, a.n_medium, stream);
     }
     if (a.n_skew > 0) launch_skew<T>(a, a.work + a.n_large + a.n_medium, a.n_skew, stream);
+    launch_cblock<T>(a, a.work + a.n_large + a.n_medium + a.n_skew, a.n_cblock, stream);
     launch_tiny<T>(a, stream);
 }
 
@@ -1307,6 +1462,13 @@ void set_lds_limits() {
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
                                   int(skew_shape<T, true>::lds_bytes));
     }
+    if constexpr (!is_cpx<T>::value)
+        for (void* f : {reinterpret_cast<void*>(&cblock_kernel<T, true, true>),
+                        reinterpret_cast<void*>(&cblock_kernel<T, true, false>),
+                        reinterpret_cast<void*>(&cblock_kernel<T, false, true>),
+                        reinterpret_cast<void*>(&cblock_kernel<T, false, false>)})
+            (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      int((cblock_max_elems(int64_t(sizeof(T))) + 4096) * int64_t(sizeof(T))));
     set_lds_limit<T, typename shapes<T>::large>();
     set_lds_limit<T, typename shapes<T>::large_tr>();
     set_lds_limit<T, typename shapes<T>::medium_tr>();
@@ -1331,7 +1493,7 @@ void tile_shapes(costa_dtype_t dtype, bool transposing_list, shape_dims* d) {
 }
 
 void launch_tiles(costa_dtype_t dtype, const launch_args& a, void* stream) {
-    if (a.n_large + a.n_medium + a.n_skew + a.n_tiny <= 0) return;
+    if (a.n_large + a.n_medium + a.n_skew + a.n_cblock + a.n_tiny <= 0) return;
     static bool once = [] {
         set_lds_limits<float>();
         set_lds_limits<double>();

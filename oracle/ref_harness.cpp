@@ -13,6 +13,8 @@
 //                                        threads: OMP_NUM_THREADS); prints one JSON line.
 //                                        Run by bench.py (cpu_baseline, rank 0, N = 1) on the
 //                                        GPU box as a child process, as the timed baseline.
+//   ref_harness bench_cfg3 <n> <nb> <s> | bench_c128 <n> <nb> <s> | bench_custom <spec> <N|T> <s>
+//                                        the same for BASELINE cfg 3 / 4 / 5 (run_bench_cfg3 ...)
 //   ref_harness relabel <spec>           rank relabelling of two grids (spec: P, trans, then
 //                                        per grid its row splits, col splits, owners): prints
 //                                        the communication volume, the reference's proposed
@@ -36,6 +38,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
+#include <functional>
 #include <iostream>
 #include <limits>
 #include <memory>
@@ -325,6 +328,139 @@ int run_bench(int m, int n, int nb, double seconds) {
     return ok ? 0 : 1;
 }
 
+// CPU baselines of BASELINE cfg 3 / 4 / 5 (bench.py cpu_baseline of each baseline_configs
+// entry; one rank, the reference's own OpenMP transform, timed like run_bench):
+//   cfg3  pxgemr2d slice: fp64 'N' no-scale copy of an n x n matrix, nb x nb blocks, 1 x 1 grid
+//   c128  pztranu slice: complex<double> 'T', alpha = (0.75, -0.5), beta = (1.25, 0.25), n x n,
+//         nb x nb blocks (C changes every call; the first call's result is checked)
+//   spec  custom layouts (cfg 5): `spec` holds A's row and column splits, then C's (each: count,
+//         values); every block its own column-major buffer; op N (alpha 1, beta 0) or T
+//         (alpha -0.5, beta 2)
+// Each prints one JSON line {GBps (algorithmic bytes: read + write of every element, + read of C
+// when beta != 0), reps, seconds, threads, verified}.
+template <typename T>
+double bench_loop(const std::function<void()>& call, double seconds, int& reps) {
+    call();  // warm-up: first touch (the checked call where C changes)
+    reps = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    double el = 0;
+    do {
+        call();
+        ++reps;
+        el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    } while (el < seconds && reps < 100000);
+    return el;
+}
+
+void print_bench(double bytes, int reps, double el, bool ok) {
+    std::printf("{\"GBps\": %.3f, \"reps\": %d, \"seconds\": %.3f, \"threads\": %d, \"verified\": %s}\n",
+                bytes * reps / el / 1e9, reps, el, omp_get_max_threads(), ok ? "true" : "false");
+}
+
+int run_bench_cfg3(int n, int nb, double seconds) {
+    std::vector<double> a(size_t(n) * n), c(size_t(n) * n, 0.0);
+    for (size_t k = 0; k < a.size(); ++k) a[k] = gen<double>(0xC057A0, 0, k);
+    auto A = costa::block_cyclic_layout<double>(n, n, nb, nb, 1, 1, n, n, 1, 1, 'R', 0, 0, a.data(), n, 'C', 0);
+    auto C = costa::block_cyclic_layout<double>(n, n, nb, nb, 1, 1, n, n, 1, 1, 'R', 0, 0, c.data(), n, 'C', 0);
+    int reps = 0;
+    const double el = bench_loop<double>([&] { costa::transform<double>(A, C, MPI_COMM_WORLD); }, seconds, reps);
+    const bool ok = a == c;
+    print_bench(2.0 * sizeof(double) * double(n) * n, reps, el, ok);
+    return ok ? 0 : 1;
+}
+
+int run_bench_c128(int n, int nb, double seconds) {
+    using z = std::complex<double>;
+    std::vector<z> a(size_t(n) * n), c(size_t(n) * n);
+    for (size_t k = 0; k < a.size(); ++k) {
+        a[k] = gen<z>(0xC057A0, 0, k);
+        c[k] = gen<z>(0xC057C0, 0, k);
+    }
+    const std::vector<z> c0 = c;
+    const z alpha(0.75, -0.5), beta(1.25, 0.25);
+    auto A = costa::block_cyclic_layout<z>(n, n, nb, nb, 1, 1, n, n, 1, 1, 'R', 0, 0, a.data(), n, 'C', 0);
+    auto C = costa::block_cyclic_layout<z>(n, n, nb, nb, 1, 1, n, n, 1, 1, 'R', 0, 0, c.data(), n, 'C', 0);
+    costa::transform<z>(A, C, 'T', alpha, beta, MPI_COMM_WORLD);
+    bool ok = true;  // the first call: C(i, j) = beta C0(i, j) + alpha A(j, i), every 97th element
+    for (size_t k = 0; k < c.size() && ok; k += 97) {
+        const size_t i = k % size_t(n), j = k / size_t(n);
+        ok = c[k] == beta * c0[k] + alpha * a[i * size_t(n) + j];
+    }
+    int reps = 0;
+    const double el = bench_loop<z>([&] { costa::transform<z>(A, C, 'T', alpha, beta, MPI_COMM_WORLD); },
+                                    seconds, reps);
+    print_bench(3.0 * sizeof(z) * double(n) * n, reps, el, ok);
+    return ok ? 0 : 1;
+}
+
+int run_bench_custom(const char* spec, char op, double seconds) {
+    std::ifstream in(spec);
+    auto vec = [&]() {
+        int k;
+        in >> k;
+        std::vector<int> v(static_cast<size_t>(k));
+        for (auto& x : v) in >> x;
+        return v;
+    };
+    const std::vector<int> ars = vec(), acs = vec(), crs = vec(), ccs = vec();
+    struct arena {
+        std::vector<float> buf;
+        std::vector<costa::block_t> blocks;
+        std::vector<size_t> off;
+        std::vector<int> owners;
+    };
+    // every block its own column-major buffer (ld = rows), 256-byte aligned offsets
+    auto make = [](const std::vector<int>& rs, const std::vector<int>& cs, uint64_t seed) {
+        arena r;
+        size_t off = 0;
+        for (size_t i = 0; i + 1 < rs.size(); ++i)
+            for (size_t j = 0; j + 1 < cs.size(); ++j) {
+                r.off.push_back(off);
+                off += (size_t(rs[i + 1] - rs[i]) * size_t(cs[j + 1] - cs[j]) + 63) / 64 * 64;
+            }
+        r.buf.assign(std::max<size_t>(off, 64), 0.f);
+        for (size_t k = 0; k < r.buf.size(); ++k) r.buf[k] = gen<float>(seed, 0, k);
+        size_t b = 0;
+        for (size_t i = 0; i + 1 < rs.size(); ++i)
+            for (size_t j = 0; j + 1 < cs.size(); ++j, ++b)
+                r.blocks.push_back({r.buf.data() + r.off[b], rs[i + 1] - rs[i], int(i), int(j)});
+        r.owners.assign(r.blocks.size(), 0);
+        return r;
+    };
+    arena a = make(ars, acs, 0xC057A0), c = make(crs, ccs, 0xC057C0);
+    const std::vector<float> c0 = c.buf;
+    auto A = costa::custom_layout<float>(int(ars.size()) - 1, int(acs.size()) - 1, ars.data(), acs.data(),
+                                         a.owners.data(), int(a.blocks.size()), a.blocks.data(), 'C');
+    auto C = costa::custom_layout<float>(int(crs.size()) - 1, int(ccs.size()) - 1, crs.data(), ccs.data(),
+                                         c.owners.data(), int(c.blocks.size()), c.blocks.data(), 'C');
+    const float alpha = op == 'N' ? 1.f : -0.5f, beta = op == 'N' ? 0.f : 2.f;
+    costa::transform<float>(A, C, op, alpha, beta, MPI_COMM_WORLD);
+    // the first call against the definition, element by element: C(i, j) = beta C0 + alpha op(A)
+    auto at = [](const arena& r, const std::vector<int>& rs, const std::vector<int>& cs, int i, int j) {
+        const size_t bi = size_t(std::upper_bound(rs.begin(), rs.end(), i) - rs.begin()) - 1;
+        const size_t bj = size_t(std::upper_bound(cs.begin(), cs.end(), j) - cs.begin()) - 1;
+        const size_t b = bi * (cs.size() - 1) + bj;
+        return r.off[b] + size_t(j - cs[bj]) * size_t(rs[bi + 1] - rs[bi]) + size_t(i - rs[bi]);
+    };
+    bool ok = true;
+    const int M = crs.back(), N = ccs.back();
+    for (int j = 0; j < N && ok; j += 7)
+        for (int i = 0; i < M; ++i) {
+            const size_t kc = at(c, crs, ccs, i, j);
+            const float x = op == 'N' ? a.buf[at(a, ars, acs, i, j)] : a.buf[at(a, ars, acs, j, i)];
+            const float want = op == 'N' ? x : beta * c0[kc] + alpha * x;
+            if (c.buf[kc] != want) {
+                ok = false;
+                break;
+            }
+        }
+    int reps = 0;
+    const double el = bench_loop<float>([&] { costa::transform<float>(A, C, op, alpha, beta, MPI_COMM_WORLD); },
+                                        seconds, reps);
+    print_bench((op == 'N' ? 2.0 : 3.0) * sizeof(float) * double(M) * N, reps, el, ok);
+    return ok ? 0 : 1;
+}
+
 // spec: P trans / per grid: n_rs rs... n_cs cs... owners (row-major)
 costa::assigned_grid2D read_grid(std::istream& in, int P) {
     auto vec = [&]() {
@@ -400,6 +536,12 @@ int main(int argc, char** argv) {
         rc = rank == 0 ? run_bench(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]),
                                    std::atof(argv[5]))
                        : 0;
+    } else if (argc >= 5 && std::string(argv[1]) == "bench_cfg3") {
+        rc = rank == 0 ? run_bench_cfg3(std::atoi(argv[2]), std::atoi(argv[3]), std::atof(argv[4])) : 0;
+    } else if (argc >= 5 && std::string(argv[1]) == "bench_c128") {
+        rc = rank == 0 ? run_bench_c128(std::atoi(argv[2]), std::atoi(argv[3]), std::atof(argv[4])) : 0;
+    } else if (argc >= 5 && std::string(argv[1]) == "bench_custom") {
+        rc = rank == 0 ? run_bench_custom(argv[2], argv[3][0], std::atof(argv[4])) : 0;
     } else if (argc >= 3 && std::string(argv[1]) == "relabel") {
         rc = rank == 0 ? run_relabel(argv[2]) : 0;
     } else {

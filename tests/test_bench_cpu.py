@@ -139,6 +139,21 @@ def test_watchdog_keeps_the_measured_headline():
     assert line["error"] == "timeout" and line["last_phase"] == {"0": "end-to-end from host memory"}
 
 
+def test_roofline_fracs_per_pass():
+    """kernel time <= step time must hold within each pass.  The line carries the
+    events pass's frac (kernel duration) beside that pass's own step time, and the value pass's
+    frac (step bytes over ms_per_step); r4's driver numbers: kernel 0.6989 ms in a 0.7097 ms
+    events-pass step, value pass 0.6971 ms"""
+    b = 4 * 2 ** 30
+    r = bench.pass_fracs(b, 1, 0.6989, 0.6971, 0.7097)
+    assert r["events_pass_ms_per_step"] == 0.7097
+    assert 0.6989 <= r["events_pass_ms_per_step"]  # kernels of a step inside that pass's step
+    assert r["frac_value_pass"] == round(b / 0.6971e-3 / 1e9 / 8000.0, 4)
+    # the value pass's frac never exceeds what its own step time allows
+    assert r["frac_value_pass"] * 8000.0 * 1e9 * 0.6971e-3 <= b * 1.0001
+    assert bench.pass_fracs(b, 1, 0.7, 0.0, 0.7)["frac_value_pass"] is None
+
+
 def test_gpus_n_without_gpus_exits_nonzero():
     """no GPU here: the parent counts devices (no GPU initialisation) and refuses"""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}

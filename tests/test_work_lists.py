@@ -31,7 +31,7 @@ def test_work_lists_cfg5(tmp_path):
                         "COSTA_SKEW_XCD", "COSTA_TINY_LDS", "COSTA_TINY_COPY", "COSTA_MISALIGNED_VEC", "COSTA_SKEW",
                         "COSTA_MERGE", "COSTA_TR_SIDE", "COSTA_FORCE_SQ", "COSTA_BAND_H", "COSTA_TUNING")}
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300,
-                       env=dict(env, COSTA_MERGE="0", COSTA_TUNING="1"))
+                       env=dict(env, COSTA_MERGE="0", COSTA_CBLOCK="0", COSTA_TUNING="1"))
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
     # merging of ops that continue each other (on by default)
     r = subprocess.run([str(exe), "merge"], capture_output=True, text=True, timeout=300, env=env)
@@ -42,14 +42,18 @@ def test_work_lists_cfg5(tmp_path):
     clean = {k: v for k, v in os.environ.items() if not k.startswith("COSTA_")}
     for extra in ({}, {"COSTA_MERGE": "0", "COSTA_TUNING": "1"}):
         r = subprocess.run([str(exe), "cover"], capture_output=True, text=True, timeout=300,
-                           env=dict(clean, **extra))
+                           env=dict(clean, COSTA_CBLOCK="0", COSTA_TUNING="1", **extra))
         assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
+    # destination-block groups (default on): each group's ops tile its range exactly once, and
+    # with the pieces cover every op of cfg 5's lists; column bands of blocks over the budget
+    r = subprocess.run([str(exe), "cblock"], capture_output=True, text=True, timeout=300, env=clean)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
 
 
 TUNING = {"COSTA_TINY_SORT": "0", "COSTA_FORCE_SQ": "1", "COSTA_LARGE_SORT": "0", "COSTA_XCD_BANDS": "0",
           "COSTA_WAVE_POLICY": "1", "COSTA_MERGE": "0", "COSTA_SKEW": "0", "COSTA_TINY_LDS": "1024",
           "COSTA_TINY_COPY": "512", "COSTA_TR_SIDE": "4", "COSTA_MISALIGNED_VEC": "3",
-          "COSTA_SKEW_XCD": "2"}
+          "COSTA_SKEW_XCD": "2", "COSTA_CBLOCK": "0"}
 
 
 @pytest.mark.skipif(shutil.which("g++") is None, reason="no g++")

@@ -258,6 +258,7 @@ static bool check_cover(const std::string& name, costa_dtype_t dt, const std::ve
     shape_dims sh;
     tile_shapes(dt, w.tr_shape, &sh);
     const int64_t E = int64_t(dtype_size(dt));
+    CHECK(w.n_cblock == 0, "%lld destination-block groups (run with COSTA_CBLOCK=0)", (long long)w.n_cblock);
     CHECK(int64_t(work.size()) == w.n_large + w.n_medium + w.n_skew, "%zu work items, split %lld + %lld + %lld",
           work.size(), (long long)w.n_large, (long long)w.n_medium, (long long)w.n_skew);
     const int bfs[3][2] = {{w.sq ? sh.bf_q : sh.bf, w.sq ? sh.bs_q : sh.bs},
@@ -301,6 +302,92 @@ static bool check_cover(const std::string& name, costa_dtype_t dt, const std::ve
     std::printf("cover %s: %lld shaped ops -> %zu items (%lld large, %lld medium, %lld skew)%s\n", name.c_str(),
                 (long long)w.tiny_first, work.size(), (long long)w.n_large, (long long)w.n_medium,
                 (long long)w.n_skew, expect_panels ? ", panels" : "");
+    return true;
+}
+
+// destination-block groups (engine.cpp cblock_groups): every group's ops tile its R x K range
+// exactly once (ldd = R, inside the range, no element twice, one transform), and together with
+// the shaped ops and the wavefront pieces every op of the list is covered exactly (by its hint)
+static bool check_cblock(const std::string& name, costa_dtype_t dt, const std::vector<costa_tile_op_t>& ops,
+                         list_kind kind, bool expect_groups) {
+    std::vector<costa_tile_op_t> ord;
+    std::vector<uint64_t> work;
+    const work_split w = build_work(dt, ops, ord, work, kind);
+    const int64_t E = int64_t(dtype_size(dt));
+    const uint32_t vec_bits = COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST;
+    CHECK(int64_t(work.size()) == w.n_large + w.n_medium + w.n_skew + w.n_cblock, "%zu work items", work.size());
+    CHECK(!expect_groups || w.n_cblock > 0, "no destination-block group");
+    std::map<uint32_t, int64_t> area;
+    int64_t lds = 0, grouped = 0, first = INT64_MAX;
+    uint64_t last = 0;
+    for (int64_t x = w.n_large + w.n_medium + w.n_skew; x < int64_t(work.size()); ++x) {
+        const uint64_t h = work[size_t(x)];
+        CHECK(h < uint64_t(w.tiny_first), "group header %llu past the groups", (unsigned long long)h);
+        first = std::min(first, int64_t(h));
+        const costa_tile_op_t& hd = ord[size_t(h)];
+        const int64_t R = hd.nf, K = hd.ns, n = int64_t(hd.src);
+        CHECK(R > 0 && K > 0 && n >= 1 && hd.ldd == R && R * K <= cblock_max_elems(E), "group %lld shape", (long long)x);
+        CHECK(hd.dst >= last, "group %lld out of destination order", (long long)x);
+        last = hd.dst;
+        lds = std::max(lds, (R | 1) * K);
+        std::vector<char> cov(size_t(R * K), 0);
+        for (int64_t i = 0; i < n; ++i) {
+            const costa_tile_op_t& op = ord[size_t(h) + 1 + size_t(i)];
+            const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
+            const int64_t run = tr ? op.ns : op.nf, runs = tr ? op.nf : op.ns;
+            CHECK(op.ldd == R && (op.flags & ~vec_bits) == hd.flags && op.dst >= hd.dst, "group %lld op %lld", (long long)x,
+                  (long long)i);
+            const int64_t e = int64_t(op.dst - hd.dst) / E, r0 = e % R, c0 = e / R;
+            CHECK(r0 + run <= R && c0 + runs <= K, "group %lld op %lld outside the range", (long long)x, (long long)i);
+            for (int64_t c = c0; c < c0 + runs; ++c)
+                for (int64_t r = r0; r < r0 + run; ++r) {
+                    CHECK(!cov[size_t(c * R + r)], "group %lld: element (%lld, %lld) twice", (long long)x, (long long)r,
+                          (long long)c);
+                    cov[size_t(c * R + r)] = 1;
+                }
+            area[op.order] += int64_t(op.nf) * op.ns;
+            grouped += int64_t(op.nf) * op.ns;
+        }
+        for (char v : cov) CHECK(v, "group %lld not covered", (long long)x);
+    }
+    CHECK(lds == w.cblock_lds, "LDS image %lld, split says %lld", (long long)lds, (long long)w.cblock_lds);
+    for (int64_t i = 0; i < std::min<int64_t>(first, w.tiny_first); ++i) area[ord[size_t(i)].order] += int64_t(ord[size_t(i)].nf) * ord[size_t(i)].ns;
+    for (int64_t i = w.tiny_first; i < w.tiny_first + w.n_tiny; ++i) area[ord[size_t(i)].order] += int64_t(ord[size_t(i)].nf) * ord[size_t(i)].ns;
+    for (const auto& o : ops)
+        CHECK(area[o.order] == int64_t(o.nf) * o.ns, "op %u covered %lld of %lld", o.order, (long long)area[o.order],
+              (long long)(int64_t(o.nf) * o.ns));
+    std::printf("cblock %s: %zu ops -> %lld groups holding %lld elements, %lld pieces, LDS %lld elements\n", name.c_str(),
+                ops.size(), (long long)w.n_cblock, (long long)grouped, (long long)w.n_tiny, (long long)lds);
+    return true;
+}
+
+static bool check_cblocks() {
+    const int n = 16384;
+    auto LA = layout(splits(0xC5A1, 8, 96, n), splits(0xC5A2, 8, 96, n), uint64_t(1) << 40);
+    auto LC = layout(splits(0xC5A3, 16, 160, n), splits(0xC5A4, 16, 160, n), uint64_t(1) << 41);
+    elayout a = erase(LA), c = erase(LC);
+    for (char op : {'N', 'T'}) {
+        auto p = plan_of(a, c, op, op == 'N' ? 1.f : -0.5f, op == 'N' ? 0.f : 2.f);
+        if (!check_cblock(std::string("cfg5 ") + op, p->dtype, p->local_ops, list_local, true)) return false;
+        if (!check_cblock(std::string("cfg5 unpack-list ") + op, p->dtype, p->local_ops, list_unpack, true)) return false;
+        // every 8th op: the ranges are no longer covered, so no group forms
+        std::vector<costa_tile_op_t> sub;
+        for (size_t i = 0; i < p->local_ops.size(); i += 8) sub.push_back(p->local_ops[i]);
+        if (!check_cblock(std::string("cfg5 sub-list ") + op, p->dtype, sub, list_local, false)) return false;
+    }
+    // C blocks of 200 x 200 fp64 (over the budget: cut into column bands) and blocks separated by
+    // gaps, fed by 24 x 24 A blocks
+    auto LA2 = layout<double>(splits(7, 20, 28, 2000), splits(8, 20, 28, 2000), uint64_t(1) << 40);
+    auto LC2 = layout<double>(splits(9, 150, 250, 2000), splits(10, 150, 250, 2000), uint64_t(1) << 41, 3);
+    elayout a2 = erase(LA2), c2 = erase(LC2);
+    for (char op : {'N', 'T'}) {
+        job j{&a2, &c2, op, {}};
+        const double one = 1.0, zero = 0.0;
+        std::memcpy(j.s.alpha.data(), &one, 8);
+        std::memcpy(j.s.beta.data(), &zero, 8);
+        auto p = make_plan({j}, 0, 1);
+        if (!check_cblock(std::string("fp64 bands ") + op, p->dtype, p->local_ops, list_local, true)) return false;
+    }
     return true;
 }
 
@@ -447,6 +534,11 @@ int main(int argc, char** argv) {
     }
     if (argc > 1 && std::string(argv[1]) == "cover") {
         if (!check_covers()) return 1;
+        std::printf("ok\n");
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "cblock") {
+        if (!check_cblocks()) return 1;
         std::printf("ok\n");
         return 0;
     }
