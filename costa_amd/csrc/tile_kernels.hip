@@ -478,6 +478,7 @@ typedef const __attribute__((address_space(1))) void glob_void;
 //   2  the same, the sub-tile's two halves of rows waited for and stored one after the other
 //   3  LDS-DMA, each wavefront's instructions on consecutive source columns
 //   4  register staging, two halves as in 2
+//   5  register staging, each wavefront's loads on consecutive source columns
 #ifndef COSTA_TR_STAGE
 #define COSTA_TR_STAGE 0
 #endif
@@ -619,11 +620,19 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
     // ---- load phase: lane -> (16-byte strip along f, column s); all loads issued first
     const int lf = (int(threadIdx.x) % S::LPC) * V;
     const int c0 = int(threadIdx.x) / S::LPC;
+    // source column of load k (COSTA_TR_STAGE 5, tuning: each wavefront's loads on consecutive
+    // columns instead of columns NW apart)
+    auto col_of = [&](int k) {
+        if constexpr (FULL && COSTA_TR_STAGE == 5 && 64 % S::LPC == 0 && (S::PL * S::CPP) % S::NW == 0)
+            return int(threadIdx.x) / 64 * (S::PL * S::CPP / S::NW) + k * (64 / S::LPC) +
+                   int(threadIdx.x) % 64 / S::LPC;
+        return c0 + k * S::CPP;
+    };
     const int nf_lane = FULL ? V : tf - lf;  // elements of this lane's strip inside the tile
     vec<T> x[S::PL];
 #pragma unroll
     for (int k = 0; k < S::PL; ++k) {
-        const int s = c0 + k * S::CPP;
+        const int s = col_of(k);
         if (FULL || (nf_lane > 0 && s < ts)) vload(x[k], src + s * lds + lf, nf_lane, vs);
     }
 
@@ -636,14 +645,14 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
         if (kind == COSTA_SCALE_AXPBY) {
 #pragma unroll
             for (int k = 0; k < S::PL; ++k) {
-                const int s = c0 + k * S::CPP;
+                const int s = col_of(k);
                 if (FULL || (nf_lane > 0 && s < ts)) vload(y[k], dst + s * ldd + lf, nf_lane, vd);
             }
         }
         uint32_t redo = 0;  // complex vectors left for the Annex G path (bit k: strip k)
 #pragma unroll
         for (int k = 0; k < S::PL; ++k) {
-            const int s = c0 + k * S::CPP;
+            const int s = col_of(k);
             if (!FULL && (nf_lane <= 0 || s >= ts)) continue;
             T* d = dst + s * ldd + lf;
             if (kind != COSTA_SCALE_BITCOPY) {
@@ -667,7 +676,7 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
 #pragma unroll 1
                 for (int k = 0; k < S::PL; ++k) {
                     if (!((redo >> k) & 1u)) continue;
-                    const int s = c0 + k * S::CPP;
+                    const int s = col_of(k);
                     const T* a = src + s * lds + lf;
                     T* d = dst + s * ldd + lf;
                     const int n = FULL ? V : min(V, nf_lane);
@@ -708,7 +717,7 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
                 for (int k = k0; k < k1; ++k) {
                     raw16 r;
                     __builtin_memcpy(&r, &x[k], 16);
-                    *reinterpret_cast<raw16*>(tile + (c0 + k * S::CPP) * P + lf) = r;
+                    *reinterpret_cast<raw16*>(tile + col_of(k) * P + lf) = r;
                 }
             };
             vec<T> y[S::PS];
@@ -756,7 +765,7 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
     }
 #pragma unroll
     for (int k = 0; k < S::PL; ++k) {
-        const int s = c0 + k * S::CPP;
+        const int s = col_of(k);
         if (FULL || (nf_lane > 0 && s < ts)) {  // partial strips: the tail is junk, never stored
             raw16 r;
             __builtin_memcpy(&r, &x[k], 16);

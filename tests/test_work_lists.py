@@ -42,7 +42,7 @@ def test_work_lists_cfg5(tmp_path):
     clean = {k: v for k, v in os.environ.items() if not k.startswith("COSTA_")}
     for extra in ({}, {"COSTA_MERGE": "0", "COSTA_TUNING": "1"}):
         r = subprocess.run([str(exe), "cover"], capture_output=True, text=True, timeout=300,
-                           env=dict(clean, COSTA_CBLOCK="0", COSTA_TUNING="1", **extra))
+                           env=dict(clean, **{"COSTA_CBLOCK": "0", "COSTA_TUNING": "1", **extra}))
         assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
     # destination-block groups (default on): each group's ops tile its range exactly once, and
     # with the pieces cover every op of cfg 5's lists; column bands of blocks over the budget

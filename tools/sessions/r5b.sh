@@ -14,3 +14,11 @@ for op in T N; do
   timeout -k 10 300 python3 tools/ab_bench.py $O/c5$op 2 cblock: wave:COSTA_TUNING=1,COSTA_CBLOCK=0 \
     -- --workload cfg5 --cfg5-op $op --steps 20 --warmup 3 --no-cpu-baseline --no-e2e --no-extra || exit 1
 done
+# the host pipeline's two-team mode (COSTA_HOST_TEAMS=1): host tests, then the end-to-end legs
+COSTA_TUNING=1 COSTA_HOST_TEAMS=1 timeout -k 10 300 $PT tests/test_gpu_host_pipeline.py -k "not golden_host_pinned" > $O/pytest_host_teams.txt 2>&1 || exit 1
+for r in 0 1; do
+  for v in "one" "teams"; do
+    if [ $v = teams ]; then E="COSTA_TUNING=1 COSTA_HOST_TEAMS=1"; else E=""; fi
+    env $E COSTA_HOST_PIPE_TRACE=1 timeout -k 10 200 python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-extra > $O/e2e_${v}_$r.json 2> $O/e2e_${v}_$r.err || exit 1
+  done
+done
