@@ -612,7 +612,9 @@ int64_t cblock_groups(costa_dtype_t dtype, std::vector<const costa_tile_op_t*>& 
     if (!on || !real || kind == list_pack || wave_ops.size() < 2) return 0;
     const int64_t E = int64_t(dtype_size(dtype));
     const uint32_t vec_bits = COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST;
-    const int64_t budget = cblock_max_elems(E);
+    // a range of n elements starting off the 16-byte grid spans up to n + V - 1 elements of
+    // whole vectors: the workgroup's kCblockChunks vectors a thread must cover that
+    const int64_t budget = cblock_max_elems(E) - (16 / E - 1);
     struct cand {
         uint64_t lo, hi;
         int32_t ldd;

@@ -211,7 +211,7 @@ void launch_tiles(costa_dtype_t dtype, const launch_args& a, void* stream /* hip
 // destination-block groups (tile_kernels.hip cblock_kernel): threads per workgroup and 16-byte
 // destination vectors per thread; a group holds at most kCblockThreads * kCblockChunks vectors
 constexpr int kCblockThreads = 256;
-constexpr int kCblockChunks = 8;
+constexpr int kCblockChunks = 4;
 inline int64_t cblock_max_elems(int64_t E) { return int64_t(kCblockThreads) * kCblockChunks * (16 / E); }
 // sub-tile shapes (elements along the source's fast dim, along its slow dim) of a copy-only list
 // or of a list with transposing ops: the large shape, the medium one (bf_m = bs_m = 0: none) and

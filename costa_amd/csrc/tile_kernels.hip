@@ -479,6 +479,8 @@ typedef const __attribute__((address_space(1))) void glob_void;
 //   3  LDS-DMA, each wavefront's instructions on consecutive source columns
 //   4  register staging, two halves as in 2
 //   5  register staging, each wavefront's loads on consecutive source columns
+//   6  LDS-DMA, one destination column per store instruction (fp64 64 x 128)
+//   7  register staging, a wavefront's stores walk each column pair's s chunks back to back
 #ifndef COSTA_TR_STAGE
 #define COSTA_TR_STAGE 0
 #endif
@@ -503,10 +505,13 @@ __device__ __forceinline__ void tr_tile_glds(const costa_tile_op_t& op, int f0, 
     const int lane = int(threadIdx.x) % 64;
     const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / 64);
     char* tb = reinterpret_cast<char*>(tile);
+    // slot swizzle of row s: conflict-free 16-byte slot reads down a slot column (modes 1-3);
+    // mode 6 reads 8-byte halves of rows 2l and 2l + 1 in lane l: rows in pairs
+    auto swz = [](int s) { return MODE == 6 ? (s / 2) % Q : s % Q; };
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
         const int i = MODE == 3 ? wave * NI + k : wave + NW * k;
-        const int slot = i * 64 + lane, s = slot / Q, q = (slot % Q) ^ (s % Q);
+        const int slot = i * 64 + lane, s = slot / Q, q = (slot % Q) ^ swz(s);
         __builtin_amdgcn_global_load_lds((glob_void*)(src + int64_t(s) * lds + q * V), (lds_void*)(tb + i * 1024),
                                          16, 0, NT ? 2 : 0);
     }
@@ -541,7 +546,7 @@ __device__ __forceinline__ void tr_tile_glds(const costa_tile_op_t& op, int f0, 
                 const int sc = u / QG, q = u % QG;
                 const int s = sc * 64 + lane;
                 const uint32_t a = uint32_t(reinterpret_cast<uintptr_t>(
-                    (__attribute__((address_space(3))) const raw16*)(img + s * Q + (q ^ (s % Q)))));
+                    (__attribute__((address_space(3))) const raw16*)(img + s * Q + (q ^ swz(s)))));
                 asm volatile("ds_read_b128 %0, %1" : "=v"(r[k]) : "v"(a) : "memory");
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -556,7 +561,7 @@ __device__ __forceinline__ void tr_tile_glds(const costa_tile_op_t& op, int f0, 
                 const int u = wave + NW * k;
                 const int sc = u / QG, q = u % QG;
                 const int s = sc * 64 + lane;
-                raw16 r = img[s * Q + (q ^ (s % Q))];
+                raw16 r = img[s * Q + (q ^ swz(s))];
                 __builtin_memcpy(&y[k], &r, 16);
             }
         }
@@ -574,6 +579,36 @@ __device__ __forceinline__ void tr_tile_glds(const costa_tile_op_t& op, int f0, 
             vstore<T, NT>(dst + f * ldd + sb, o, V, true);
         }
     };
+    if constexpr (MODE == 6 && V == 2 && BS == 128) {
+        // one destination column per store instruction: unit k of wave w is column f =
+        // w + NW k, lane l holds its rows 2l, 2l + 1 (two 8-byte LDS reads, no lane exchange):
+        // 1 KiB of one column instead of 512 B of two
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // (no fence: the wait above orders the LDS-DMA)
+        constexpr int NU = BF / NW;
+        const T* img8 = tile;
+#pragma unroll
+        for (int k = 0; k < NU; ++k) {
+            const int f = wave + NW * k, q = f / V, h = f % V;
+            vec<T> o;
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int sr = 2 * lane + e;
+                o.e[e] = img8[(sr * Q + (q ^ swz(sr))) * V + h];
+            }
+            T* d = dst + int64_t(f) * ldd + 2 * lane;
+            if (kind != COSTA_SCALE_BITCOPY) {
+#pragma unroll
+                for (int e = 0; e < V; ++e) {
+                    T y = e_zero<T>();
+                    if (kind == COSTA_SCALE_AXPBY) y = d[e];
+                    o.e[e] = scale(o.e[e], y, kind, conj, alpha, beta);
+                }
+            }
+            vstore<T, NT>(d, o, V, true);
+        }
+        return;
+    }
     if constexpr (MODE == 2) {
         if (kind != COSTA_SCALE_AXPBY) {
             // the first NI / 2 instructions of every wavefront hold rows [0, BS / 2): store units
@@ -610,7 +645,8 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
     const bool vd = FULL || (flags & COSTA_TILE_VEC_DST);
     const int64_t lds = op.lds, ldd = op.ldd;
     const T* src = reinterpret_cast<const T*>(src_base + op.src) + int64_t(s0) * lds + f0;
-    if constexpr (FULL && COSTA_TR_STAGE >= 1 && COSTA_TR_STAGE <= 3 && !is_cpx<T>::value && S::FW == 1) {
+    if constexpr (FULL && ((COSTA_TR_STAGE >= 1 && COSTA_TR_STAGE <= 3) || COSTA_TR_STAGE == 6) &&
+                  !is_cpx<T>::value && S::FW == 1) {
         if (flags & COSTA_TILE_TRANSPOSE) {
             tr_tile_glds<T, S, NT>(op, f0, s0, src_base, dst_base, alpha, beta, tile);
             return;
@@ -694,11 +730,22 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
     T* dst = reinterpret_cast<T*>(dst_base + op.dst) + int64_t(f0) * ldd + s0;
     const int lane = int(threadIdx.x) % 64, wave = int(threadIdx.x) / 64;
     constexpr int SW = S::SW, FW = S::FW, QG = BF / V / FW;  // QG: f-slot groups per s chunk
+    // store unit u -> (s chunk, f-slot group): s chunk slowest; COSTA_TR_STAGE 7 (tuning): s chunk
+    // fastest, so a wavefront writes a column pair's chunks one after the other
+    constexpr int NSC = S::BS / SW;
+    auto unit_sc = [&](int u) {
+        if constexpr (FULL && COSTA_TR_STAGE == 7) return u % NSC;
+        return u / QG;
+    };
+    auto unit_q = [&](int u) {
+        if constexpr (FULL && COSTA_TR_STAGE == 7) return u / NSC;
+        return u % QG;
+    };
     // store unit k of this lane: SW s values x FW f slots (64 x 1 for BS >= 64); after the lane
     // exchange lane (base + j) stores f = q*V + j for s = sc*SW + base .. +V-1
     auto unit = [&](int k, int& f, int& sb, int& n) {
         const int u = wave + S::NW * k;
-        const int sc = u / QG, q = (u % QG) * FW + lane / SW;
+        const int sc = unit_sc(u), q = unit_q(u) * FW + lane / SW;
         const int j = lane & (V - 1);
         f = q * V + j;
         sb = sc * SW + (lane % SW - j);
@@ -725,7 +772,7 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
 #pragma unroll
                 for (int k = k0; k < k1; ++k) {
                     const int u = wave + S::NW * k;
-                    const int sc = u / QG, q = (u % QG) * FW + lane / SW;
+                    const int sc = unit_sc(u), q = unit_q(u) * FW + lane / SW;
                     raw16 r = *reinterpret_cast<const raw16*>(tile + (sc * SW + lane % SW) * P + q * V);
                     __builtin_memcpy(&y[k], &r, 16);
                 }
@@ -778,7 +825,7 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
 #pragma unroll
     for (int k = 0; k < S::PS; ++k) {
         const int u = wave + S::NW * k;                         // store unit
-        const int sc = u / QG, q = (u % QG) * FW + lane / SW;   // s chunk, f slot
+        const int sc = unit_sc(u), q = unit_q(u) * FW + lane / SW;   // s chunk, f slot
         const int s = sc * SW + lane % SW;
         if (FULL || (s < ts && q * V < tf)) {
             raw16 r = *reinterpret_cast<const raw16*>(tile + s * P + q * V);

@@ -1,0 +1,82 @@
+"""Tuning probe (not product): several builds of libcosta_amd.so loaded side by side in ONE
+process (RTLD_LOCAL, raw C ABI), timed on the SAME buffers -- the headline's rate depends on where
+the destination buffer lies physically (r5, tools/pairs_probe.py), so builds compared in separate
+processes see different placements.  K pairs of 2 GiB buffers; per pair and build the kernel time
+of 10 stream-ordered transforms (the library's own events), C checked against A^T once.
+    python tools/libs_probe.py <pairs> <label=path.so> [<label=path.so> ...]"""
+import ctypes as C
+import os
+import sys
+
+import torch
+
+N, B = 16384, 256
+
+
+class Stats(C.Structure):  # costa_stats_t (include/costa_hip.h)
+    _fields_ = [(k, C.c_double) for k in ("pack_ms", "local_ms", "unpack_ms", "exchange_ms", "h2d_ms", "d2h_ms")] + \
+               [(k, C.c_int64) for k in ("pack_launches", "local_launches", "unpack_launches", "pack_bytes",
+                                         "local_bytes", "unpack_bytes", "transforms", "plan_hits", "plan_misses",
+                                         "host_groups", "device_plans")] + \
+               [("plan_ms", C.c_double), ("host_direct", C.c_int64), ("host_direct_groups", C.c_int64)]
+
+
+class Lib:
+    def __init__(self, path):
+        self.L = C.CDLL(path, mode=C.RTLD_LOCAL)
+        vp, i, c = C.c_void_p, C.c_int, C.c_char
+        self.L.costa_hip_block_cyclic_layout.argtypes = [i, i, i, i, i, i, i, i, i, i, i, c, i, i, vp, i, c, i,
+                                                         C.POINTER(vp)]
+        self.L.costa_hip_comm_self.argtypes = [i, C.POINTER(vp)]
+        self.L.costa_hip_transform_async.argtypes = [vp, vp, c, vp, vp, vp, vp]
+        self.L.costa_hip_synchronize.argtypes = [vp]
+        self.L.costa_hip_get_stats.argtypes = [C.POINTER(Stats), i]
+        self.comm = vp()
+        assert self.L.costa_hip_comm_self(0, C.byref(self.comm)) == 0
+        self.one, self.zero = C.c_double(1.0), C.c_double(0.0)
+
+    def layout(self, ptr):
+        h = C.c_void_p()
+        rc = self.L.costa_hip_block_cyclic_layout(1, N, N, B, B, 1, 1, N, N, 1, 1, b"R", 0, 0, C.c_void_p(ptr), N,
+                                                  b"C", 0, C.byref(h))
+        assert rc == 0
+        return h
+
+    def ms(self, LA, LC, steps=10):
+        def run(k):
+            for _ in range(k):
+                assert self.L.costa_hip_transform_async(LA, LC, b"T", C.byref(self.one), C.byref(self.zero),
+                                                        self.comm, None) == 0
+            assert self.L.costa_hip_synchronize(self.comm) == 0
+        run(2)
+        st = Stats()
+        self.L.costa_hip_set_profiling(1)
+        self.L.costa_hip_get_stats(C.byref(st), 1)
+        run(steps)
+        self.L.costa_hip_get_stats(C.byref(st), 1)
+        self.L.costa_hip_set_profiling(0)
+        return st.local_ms / steps
+
+
+def main():
+    pairs = int(sys.argv[1])
+    libs = []
+    for a in sys.argv[2:]:
+        lab, _, path = a.partition("=")
+        libs.append((lab, Lib(path)))
+    bufs = [(torch.rand(N * N, dtype=torch.float64, device="cuda"), torch.empty(N * N, dtype=torch.float64, device="cuda"))
+            for _ in range(pairs)]
+    print("pair  " + "  ".join(f"{lab:>10s}" for lab, _ in libs), flush=True)
+    for k, (a, c) in enumerate(bufs):
+        row = []
+        for lab, lib in libs:
+            LA, LC = lib.layout(a.data_ptr()), lib.layout(c.data_ptr())
+            row.append(lib.ms(LA, LC))
+            torch.cuda.synchronize()
+            assert torch.equal(c.view(N, N), a.view(N, N).t()), f"{lab}: wrong result"
+            c.zero_()
+        print(f"{k:4d}  " + "  ".join(f"{x:10.4f}" for x in row), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -326,7 +326,9 @@ static bool check_cblock(const std::string& name, costa_dtype_t dt, const std::v
         first = std::min(first, int64_t(h));
         const costa_tile_op_t& hd = ord[size_t(h)];
         const int64_t R = hd.nf, K = hd.ns, n = int64_t(hd.src);
-        CHECK(R > 0 && K > 0 && n >= 1 && hd.ldd == R && R * K <= cblock_max_elems(E), "group %lld shape", (long long)x);
+        // (a range off the 16-byte grid needs up to V - 1 more elements of whole vectors)
+        CHECK(R > 0 && K > 0 && n >= 1 && hd.ldd == R && R * K + 16 / E - 1 <= cblock_max_elems(E),
+              "group %lld shape", (long long)x);
         CHECK(hd.dst >= last, "group %lld out of destination order", (long long)x);
         last = hd.dst;
         lds = std::max(lds, (R | 1) * K);
@@ -377,6 +379,7 @@ static bool check_cblocks() {
     }
     // C blocks of 200 x 200 fp64 (over the budget: cut into column bands) and blocks separated by
     // gaps, fed by 24 x 24 A blocks
+    // (gap 3: every block after the first starts off the 16-byte grid, as in test_gpu_cblock.py)
     auto LA2 = layout<double>(splits(7, 20, 28, 2000), splits(8, 20, 28, 2000), uint64_t(1) << 40);
     auto LC2 = layout<double>(splits(9, 150, 250, 2000), splits(10, 150, 250, 2000), uint64_t(1) << 41, 3);
     elayout a2 = erase(LA2), c2 = erase(LC2);
