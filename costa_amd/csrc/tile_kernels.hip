@@ -480,7 +480,10 @@ typedef const __attribute__((address_space(1))) void glob_void;
 //   4  register staging, two halves as in 2
 //   5  register staging, each wavefront's loads on consecutive source columns
 //   6  LDS-DMA, one destination column per store instruction (fp64 64 x 128)
-//   7  register staging, a wavefront's stores walk each column pair's s chunks back to back
+//   7  register staging, the two s chunks of a column pair stored at once (by two wavefronts)
+//   8  LDS-DMA with the store order of 7
+//   9  register staging, a wavefront's stores on its own column pairs, both chunks back to back
+//   10 LDS-DMA with the store order of 9
 #ifndef COSTA_TR_STAGE
 #define COSTA_TR_STAGE 0
 #endif
@@ -517,9 +520,12 @@ __device__ __forceinline__ void tr_tile_glds(const costa_tile_op_t& op, int f0, 
     }
     T* dst = reinterpret_cast<T*>(dst_base + op.dst) + int64_t(f0) * ldd + s0;
     constexpr int QG = Q;  // store units per s chunk (FW = 1)
+    // mode 10 (tuning): the store order of register mode 9 (wave-contiguous units, a column
+    // pair's chunks back to back)
+    auto unit_u = [&](int k) { return MODE == 10 ? wave * S::PS + k : wave + NW * k; };
     auto unit = [&](int k, int& f, int& sb) {
-        const int u = wave + NW * k;
-        const int sc = u / QG, q = u % QG;
+        const int u = unit_u(k);
+        const int sc = MODE >= 8 ? u % (BS / 64) : u / QG, q = MODE >= 8 ? u / (BS / 64) : u % QG;
         const int j = lane & (V - 1);
         f = q * V + j;
         sb = sc * 64 + (lane - j);
@@ -542,8 +548,8 @@ __device__ __forceinline__ void tr_tile_glds(const costa_tile_op_t& op, int f0, 
             u32x4a r[S::PS];
 #pragma unroll
             for (int k = k0; k < k1; ++k) {
-                const int u = wave + NW * k;
-                const int sc = u / QG, q = u % QG;
+                const int u = unit_u(k);
+                const int sc = MODE >= 8 ? u % (BS / 64) : u / QG, q = MODE >= 8 ? u / (BS / 64) : u % QG;
                 const int s = sc * 64 + lane;
                 const uint32_t a = uint32_t(reinterpret_cast<uintptr_t>(
                     (__attribute__((address_space(3))) const raw16*)(img + s * Q + (q ^ swz(s)))));
@@ -558,8 +564,8 @@ __device__ __forceinline__ void tr_tile_glds(const costa_tile_op_t& op, int f0, 
         } else {
 #pragma unroll
             for (int k = k0; k < k1; ++k) {
-                const int u = wave + NW * k;
-                const int sc = u / QG, q = u % QG;
+                const int u = unit_u(k);
+                const int sc = MODE >= 8 ? u % (BS / 64) : u / QG, q = MODE >= 8 ? u / (BS / 64) : u % QG;
                 const int s = sc * 64 + lane;
                 raw16 r = img[s * Q + (q ^ swz(s))];
                 __builtin_memcpy(&y[k], &r, 16);
@@ -645,7 +651,8 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
     const bool vd = FULL || (flags & COSTA_TILE_VEC_DST);
     const int64_t lds = op.lds, ldd = op.ldd;
     const T* src = reinterpret_cast<const T*>(src_base + op.src) + int64_t(s0) * lds + f0;
-    if constexpr (FULL && ((COSTA_TR_STAGE >= 1 && COSTA_TR_STAGE <= 3) || COSTA_TR_STAGE == 6) &&
+    if constexpr (FULL && ((COSTA_TR_STAGE >= 1 && COSTA_TR_STAGE <= 3) || COSTA_TR_STAGE == 6 || COSTA_TR_STAGE == 8 ||
+                         COSTA_TR_STAGE == 10) &&
                   !is_cpx<T>::value && S::FW == 1) {
         if (flags & COSTA_TILE_TRANSPOSE) {
             tr_tile_glds<T, S, NT>(op, f0, s0, src_base, dst_base, alpha, beta, tile);
@@ -733,18 +740,30 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
     // store unit u -> (s chunk, f-slot group): s chunk slowest; COSTA_TR_STAGE 7 (tuning): s chunk
     // fastest, so a wavefront writes a column pair's chunks one after the other
     constexpr int NSC = S::BS / SW;
+    // PAIR (r5, the fp64 64 x 128 shape -- BASELINE cfg 2 -- as shipped; COSTA_TR_STAGE 9 for
+    // every shape in tuning builds): a wavefront stores its own column pairs, the two s chunks of
+    // a pair back to back, so each destination column's 1 KiB segment is written in one go.
+    // Side by side on the same buffers (tools/libs_probe.py, profiles/r5l/): fp64 0.6990 ->
+    // 0.6934 ms; fp32 128 x 128 +2 %, c128 64 x 64 +4.5 %: those keep the strided order
+    constexpr bool PAIR = FULL && (COSTA_TR_STAGE == 9 ||
+                                   (COSTA_TR_STAGE == 0 && std::is_same<T, double>::value && S::BF == 64 &&
+                                    S::BS == 128 && S::NT == 512));
+    auto unit_u = [&](int k) {
+        if constexpr (PAIR) return wave * S::PS + k;
+        return wave + S::NW * k;
+    };
     auto unit_sc = [&](int u) {
-        if constexpr (FULL && COSTA_TR_STAGE == 7) return u % NSC;
+        if constexpr (PAIR || (FULL && COSTA_TR_STAGE == 7)) return u % NSC;
         return u / QG;
     };
     auto unit_q = [&](int u) {
-        if constexpr (FULL && COSTA_TR_STAGE == 7) return u / NSC;
+        if constexpr (PAIR || (FULL && COSTA_TR_STAGE == 7)) return u / NSC;
         return u % QG;
     };
     // store unit k of this lane: SW s values x FW f slots (64 x 1 for BS >= 64); after the lane
     // exchange lane (base + j) stores f = q*V + j for s = sc*SW + base .. +V-1
     auto unit = [&](int k, int& f, int& sb, int& n) {
-        const int u = wave + S::NW * k;
+        const int u = unit_u(k);
         const int sc = unit_sc(u), q = unit_q(u) * FW + lane / SW;
         const int j = lane & (V - 1);
         f = q * V + j;
@@ -771,7 +790,7 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
             auto get = [&](int k0, int k1) {
 #pragma unroll
                 for (int k = k0; k < k1; ++k) {
-                    const int u = wave + S::NW * k;
+                    const int u = unit_u(k);
                     const int sc = unit_sc(u), q = unit_q(u) * FW + lane / SW;
                     raw16 r = *reinterpret_cast<const raw16*>(tile + (sc * SW + lane % SW) * P + q * V);
                     __builtin_memcpy(&y[k], &r, 16);
@@ -824,7 +843,7 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
     vec<T> y[S::PS];
 #pragma unroll
     for (int k = 0; k < S::PS; ++k) {
-        const int u = wave + S::NW * k;                         // store unit
+        const int u = unit_u(k);                         // store unit
         const int sc = unit_sc(u), q = unit_q(u) * FW + lane / SW;   // s chunk, f slot
         const int s = sc * SW + lane % SW;
         if (FULL || (s < ts && q * V < tf)) {

@@ -3,14 +3,20 @@ process (RTLD_LOCAL, raw C ABI), timed on the SAME buffers -- the headline's rat
 the destination buffer lies physically (r5, tools/pairs_probe.py), so builds compared in separate
 processes see different placements.  K pairs of 2 GiB buffers; per pair and build the kernel time
 of 10 stream-ordered transforms (the library's own events), C checked against A^T once.
-    python tools/libs_probe.py <pairs> <label=path.so> [<label=path.so> ...]"""
+    python tools/libs_probe.py <pairs> <label=path.so> [<label=path.so> ...]
+(beta != 0 runs are timed only: C changes every call)"""
 import ctypes as C
 import os
 import sys
 
 import torch
 
-N, B = 16384, 256
+# PROBE_DT (f64 | f32 | c64 | c128), PROBE_N, PROBE_B, PROBE_BETA: other headline-like geometries
+DT = os.environ.get("PROBE_DT", "f64")
+N, B = int(os.environ.get("PROBE_N", "16384")), int(os.environ.get("PROBE_B", "256"))
+BETA = float(os.environ.get("PROBE_BETA", "0"))
+CODE, TDT = {"f32": (0, torch.float32), "f64": (1, torch.float64), "c64": (2, torch.complex64),
+             "c128": (3, torch.complex128)}[DT]
 
 
 class Stats(C.Structure):  # costa_stats_t (include/costa_hip.h)
@@ -33,11 +39,19 @@ class Lib:
         self.L.costa_hip_get_stats.argtypes = [C.POINTER(Stats), i]
         self.comm = vp()
         assert self.L.costa_hip_comm_self(0, C.byref(self.comm)) == 0
-        self.one, self.zero = C.c_double(1.0), C.c_double(0.0)
+        E = {0: 4, 1: 8, 2: 8, 3: 16}[CODE]
+        self.alpha = (C.c_char * E)()
+        self.beta = (C.c_char * E)()
+        import struct
+        fmt = {0: "f", 1: "d", 2: "ff", 3: "dd"}[CODE]
+        av = (1.0 if BETA == 0 else 0.5,) + ((0.0,) if CODE >= 2 else ())
+        bv = (BETA,) + ((0.0,) if CODE >= 2 else ())
+        C.memmove(self.alpha, struct.pack(fmt, *av), E)
+        C.memmove(self.beta, struct.pack(fmt, *bv), E)
 
     def layout(self, ptr):
         h = C.c_void_p()
-        rc = self.L.costa_hip_block_cyclic_layout(1, N, N, B, B, 1, 1, N, N, 1, 1, b"R", 0, 0, C.c_void_p(ptr), N,
+        rc = self.L.costa_hip_block_cyclic_layout(CODE, N, N, B, B, 1, 1, N, N, 1, 1, b"R", 0, 0, C.c_void_p(ptr), N,
                                                   b"C", 0, C.byref(h))
         assert rc == 0
         return h
@@ -45,7 +59,7 @@ class Lib:
     def ms(self, LA, LC, steps=10):
         def run(k):
             for _ in range(k):
-                assert self.L.costa_hip_transform_async(LA, LC, b"T", C.byref(self.one), C.byref(self.zero),
+                assert self.L.costa_hip_transform_async(LA, LC, b"T", self.alpha, self.beta,
                                                         self.comm, None) == 0
             assert self.L.costa_hip_synchronize(self.comm) == 0
         run(2)
@@ -64,7 +78,7 @@ def main():
     for a in sys.argv[2:]:
         lab, _, path = a.partition("=")
         libs.append((lab, Lib(path)))
-    bufs = [(torch.rand(N * N, dtype=torch.float64, device="cuda"), torch.empty(N * N, dtype=torch.float64, device="cuda"))
+    bufs = [(torch.rand(N * N, dtype=TDT, device="cuda"), torch.zeros(N * N, dtype=TDT, device="cuda"))
             for _ in range(pairs)]
     print("pair  " + "  ".join(f"{lab:>10s}" for lab, _ in libs), flush=True)
     for k, (a, c) in enumerate(bufs):
@@ -73,7 +87,8 @@ def main():
             LA, LC = lib.layout(a.data_ptr()), lib.layout(c.data_ptr())
             row.append(lib.ms(LA, LC))
             torch.cuda.synchronize()
-            assert torch.equal(c.view(N, N), a.view(N, N).t()), f"{lab}: wrong result"
+            if BETA == 0:
+                assert torch.equal(c.view(N, N), a.view(N, N).t()), f"{lab}: wrong result"
             c.zero_()
         print(f"{k:4d}  " + "  ".join(f"{x:10.4f}" for x in row), flush=True)
 
