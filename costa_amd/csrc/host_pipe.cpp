@@ -179,52 +179,6 @@ pool& thread_pool() {  // never destroyed: its threads outlive static destructio
     return *p;
 }
 
-// Two teams (COSTA_HOST_TEAMS=1, tuning): the gathers and the scatters run on disjoint halves of
-// the host threads, each team at its own pace, instead of one pass per step that first waits for
-// both the upload slot and the download
-bool host_teams() {
-    static const bool on = [] {
-        const char* s = tuning_env("COSTA_HOST_TEAMS");
-        return s && std::atoi(s) != 0;
-    }();
-    return on;
-}
-pool& gather_pool() {
-    static pool* p = new pool(std::max(1, host_threads() / 2));
-    return *p;
-}
-pool& scatter_pool() {
-    static pool* p = new pool(std::max(1, host_threads() - host_threads() / 2));
-    return *p;
-}
-
-// in-order progress of one team (the last finished step), with failure propagation
-struct progress {
-    std::mutex m;
-    std::condition_variable cv;
-    int64_t upto = -1;
-    bool failed = false;
-    void set(int64_t t) {
-        {
-            std::lock_guard<std::mutex> lk(m);
-            upto = t;
-        }
-        cv.notify_all();
-    }
-    void fail() {
-        {
-            std::lock_guard<std::mutex> lk(m);
-            failed = true;
-        }
-        cv.notify_all();
-    }
-    void wait(int64_t t) {
-        std::unique_lock<std::mutex> lk(m);
-        cv.wait(lk, [&] { return upto >= t || failed; });
-        if (upto < t) throw error(COSTA_ERR_INTERNAL, "costa: host pipeline step failed");
-    }
-};
-
 // ---------------------------------------------------------------- per-device ring
 struct ring {
     int device = 0;
@@ -870,7 +824,7 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
 
     // COSTA_HOST_PIPE_TRACE=1: host-side time split (copies / waits / issue) on stderr
     static const bool trace = std::getenv("COSTA_HOST_PIPE_TRACE") != nullptr;
-    double t_copy = 0, t_scatter = 0, t_wait_up = 0, t_wait_down = 0, t_wait_issue = 0, t_issue = 0;
+    double t_copy = 0, t_wait_up = 0, t_wait_down = 0, t_issue = 0;
     auto now = [] {
         return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
     };
@@ -967,114 +921,39 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
         t_issue += now() - t3;
     };
 
-    const bool teams = host_teams();
-    if (!teams) {
-        // one pass per step t: the gather of group t and the scatter of group t - kLag together
-        for (size_t t = 0; t < G + kLag; ++t) {
-            const int k = int(t % kRing);
-            const hpl::group* g = t < G ? &hp.groups[t] : nullptr;
-            const hpl::group* o = t >= size_t(kLag) ? &hp.groups[t - kLag] : nullptr;
-            if (o && o->kind == hpl::PACK) o = nullptr;  // nothing comes back from a pack group
-            if (is_direct(o)) o = nullptr;               // ... nor to the host threads from a direct one
-            const hpl::group* gh = is_direct(g) ? nullptr : g;  // group t's host gather
-            const int ko = int((t + kRing - kLag) % kRing);     // slot of group t - kLag
-            double t0 = now();
-            // the pinned source slot is free once its previous upload has landed
-            if (gh) HP_CHECK(hipEventSynchronize(R.up_done[k]));
-            double t1 = now();
-            // group t - kLag's target package has landed in its pinned slot
-            if (o) HP_CHECK(hipEventSynchronize(R.down_done[ko]));
-            double t2 = now();
-            if (gh || o) host_step(gh, R.pin_in + size_t(k) * 2 * S, o, R.pin_out + size_t(ko) * S, P);
-            t_wait_up += t1 - t0;
-            t_wait_down += t2 - t1;
-            t_copy += now() - t2;
-            if (g) issue(t);  // (the target slot of group t - kRing was scattered at step t - 1)
-        }
-    } else {
-        // two teams: a gather thread (group t into pinned slot t % kRing once the upload of group
-        // t - kRing has landed), a scatter thread (group t out of its pinned slot once its download
-        // has landed), and this thread issuing group t once it is gathered and group t - kRing
-        // (same slots) scattered
-        progress gathered, scattered, issued_p;
-        std::exception_ptr err[3];
-        auto fail_all = [&] {
-            gathered.fail();
-            scattered.fail();
-            issued_p.fail();
-        };
-        std::thread gth([&] {
-            try {
-                HP_CHECK(hipSetDevice(device));
-                for (size_t t = 0; t < G; ++t) {
-                    const hpl::group* g = &hp.groups[t];
-                    const int k = int(t % kRing);
-                    if (!is_direct(g) && (!g->gather.empty() || g->reads_old)) {
-                        if (t >= size_t(kRing)) issued_p.wait(int64_t(t) - kRing);
-                        const double a = now();
-                        HP_CHECK(hipEventSynchronize(R.up_done[k]));
-                        const double b = now();
-                        host_step(g, R.pin_in + size_t(k) * 2 * S, nullptr, nullptr, gather_pool());
-                        t_wait_up += b - a;
-                        t_copy += now() - b;
-                    }
-                    gathered.set(int64_t(t));
-                }
-            } catch (...) {
-                err[1] = std::current_exception();
-                fail_all();
-            }
-        });
-        std::thread sth([&] {
-            try {
-                HP_CHECK(hipSetDevice(device));
-                for (size_t t = 0; t < G; ++t) {
-                    const hpl::group* o = &hp.groups[t];
-                    const int k = int(t % kRing);
-                    if (o->kind != hpl::PACK && !is_direct(o)) {
-                        issued_p.wait(int64_t(t));
-                        const double a = now();
-                        HP_CHECK(hipEventSynchronize(R.down_done[k]));
-                        const double b = now();
-                        host_step(nullptr, nullptr, o, R.pin_out + size_t(k) * S, scatter_pool());
-                        t_wait_down += b - a;
-                        t_scatter += now() - b;
-                    }
-                    scattered.set(int64_t(t));
-                }
-            } catch (...) {
-                err[2] = std::current_exception();
-                fail_all();
-            }
-        });
-        try {
-            for (size_t t = 0; t < G; ++t) {
-                const double a = now();
-                gathered.wait(int64_t(t));
-                if (t >= size_t(kRing)) scattered.wait(int64_t(t) - kRing);
-                t_wait_issue += now() - a;
-                issue(t);
-                issued_p.set(int64_t(t));
-            }
-        } catch (...) {
-            err[0] = std::current_exception();
-            fail_all();
-        }
-        gth.join();
-        sth.join();
-        for (auto& e : err)
-            if (e) std::rethrow_exception(e);
+    // one pass per step t: the gather of group t and the scatter of group t - kLag together, on
+    // every host thread (r5: gathers and scatters on two halves of the threads, each at its own
+    // pace, ran 56-58 against 83 GB/s -- the gather on 8 threads became the bound;
+    // profiles/r5d/)
+    for (size_t t = 0; t < G + kLag; ++t) {
+        const int k = int(t % kRing);
+        const hpl::group* g = t < G ? &hp.groups[t] : nullptr;
+        const hpl::group* o = t >= size_t(kLag) ? &hp.groups[t - kLag] : nullptr;
+        if (o && o->kind == hpl::PACK) o = nullptr;  // nothing comes back from a pack group
+        if (is_direct(o)) o = nullptr;               // ... nor to the host threads from a direct one
+        const hpl::group* gh = is_direct(g) ? nullptr : g;  // group t's host gather
+        const int ko = int((t + kRing - kLag) % kRing);     // slot of group t - kLag
+        double t0 = now();
+        // the pinned source slot is free once its previous upload has landed
+        if (gh) HP_CHECK(hipEventSynchronize(R.up_done[k]));
+        double t1 = now();
+        // group t - kLag's target package has landed in its pinned slot
+        if (o) HP_CHECK(hipEventSynchronize(R.down_done[ko]));
+        double t2 = now();
+        if (gh || o) host_step(gh, R.pin_in + size_t(k) * 2 * S, o, R.pin_out + size_t(ko) * S, P);
+        t_wait_up += t1 - t0;
+        t_wait_down += t2 - t1;
+        t_copy += now() - t2;
+        if (g) issue(t);  // (the target slot of group t - kRing was scattered at step t - 1)
     }
     issue_rounds(hp.rounds);  // a rank with nothing to upload still takes part in the exchange
     if (trace)
         std::fprintf(stderr,
-                     "[costa host pipe] groups %zu, %d exchange round(s), slot %zu MiB threads %d%s%s: "
-                     "total %.2f ms, copies %.2f (scatter team %.2f), wait-up %.2f, wait-down %.2f, "
-                     "issuer waits %.2f, issue %.2f\n",
-                     G, exchange ? hp.rounds : 0, S >> 20, host_threads(), teams ? " (two teams)" : "",
+                     "[costa host pipe] groups %zu, %d exchange round(s), slot %zu MiB threads %d%s: "
+                     "total %.2f ms, copies %.2f, wait-up %.2f, wait-down %.2f, issue %.2f\n",
+                     G, exchange ? hp.rounds : 0, S >> 20, host_threads(),
                      direct ? (n_direct_run == G ? " (direct DMA)" : " (direct DMA: some groups)") : "",
-                     (now() - t_begin) * 1e3, t_copy * 1e3, t_scatter * 1e3, t_wait_up * 1e3,
-                     t_wait_down * 1e3, t_wait_issue * 1e3, t_issue * 1e3);
+                     (now() - t_begin) * 1e3, t_copy * 1e3, t_wait_up * 1e3, t_wait_down * 1e3, t_issue * 1e3);
     HP_CHECK(hipStreamSynchronize(R.up));
     HP_CHECK(hipStreamSynchronize(xs));
     HP_CHECK(hipStreamSynchronize(comp));
