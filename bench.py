@@ -90,7 +90,7 @@ def launch_decision(gpus: int, env, argv, port=None):
 
 
 RUN_BUDGET_S = 540.0  # wall-clock budget of an N-rank child (below the driver's own limit)
-_PHASE = re.compile(r"^\[bench rank (\d+)\] phase: (.*)$")
+_PHASE = re.compile(r"^\[bench rank (\d+)\] phase: (.*?)(?: \(t=[0-9.]+ s\))?$")
 
 
 def run_ranks(cmd, budget_s: float = RUN_BUDGET_S, n_gpus: int = 0) -> int:
@@ -172,10 +172,14 @@ _last_phase = ["start"]
 _partial_line: dict = {}
 
 
+_T0 = time.time()
+
+
 def phase(rank: int, msg: str):
-    """progress line of one rank (stderr), parsed by run_ranks and kept for the watchdog"""
+    """progress line of one rank (stderr, with the seconds since start), parsed by run_ranks and
+    kept for the watchdog"""
     _last_phase[0] = msg
-    print(f"[bench rank {rank}] phase: {msg}", file=sys.stderr, flush=True)
+    print(f"[bench rank {rank}] phase: {msg} (t={time.time() - _T0:.1f} s)", file=sys.stderr, flush=True)
 
 
 def start_watchdog(rank: int, world: int, budget_s: float):
@@ -744,6 +748,8 @@ def main():
         used = {k for k, _, _ in keys_x}
         keys_x.append((kind if kind not in used else f"{kind}_{edge}", kind, edge))
     # the reference's own CPU path, as child processes before anything touches the GPU
+    if want_cpu:
+        phase(rank, "CPU baselines (the reference on the host cores)")
     cpu_ref = cpu_baseline_reference(n=args.edge, b=args.block) if want_cpu else None
     cpu_x = cpu_baseline_configs(keys_x) if want_cpu and keys_x else {}
     import torch

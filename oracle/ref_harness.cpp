@@ -300,6 +300,7 @@ int run_kat(const std::string& out) {
 
 int run_bench(int m, int n, int nb, double seconds) {
     std::vector<double> a(size_t(m) * n), c(size_t(n) * m, 0.0);
+#pragma omp parallel for schedule(static)
     for (size_t k = 0; k < a.size(); ++k) a[k] = gen<double>(0xC057A0, 0, k);
     auto A = costa::block_cyclic_layout<double>(m, n, nb, nb, 1, 1, m, n, 1, 1, 'R', 0, 0,
                                                 a.data(), m, 'C', 0);
@@ -359,6 +360,7 @@ void print_bench(double bytes, int reps, double el, bool ok) {
 
 int run_bench_cfg3(int n, int nb, double seconds) {
     std::vector<double> a(size_t(n) * n), c(size_t(n) * n, 0.0);
+#pragma omp parallel for schedule(static)
     for (size_t k = 0; k < a.size(); ++k) a[k] = gen<double>(0xC057A0, 0, k);
     auto A = costa::block_cyclic_layout<double>(n, n, nb, nb, 1, 1, n, n, 1, 1, 'R', 0, 0, a.data(), n, 'C', 0);
     auto C = costa::block_cyclic_layout<double>(n, n, nb, nb, 1, 1, n, n, 1, 1, 'R', 0, 0, c.data(), n, 'C', 0);
@@ -372,6 +374,7 @@ int run_bench_cfg3(int n, int nb, double seconds) {
 int run_bench_c128(int n, int nb, double seconds) {
     using z = std::complex<double>;
     std::vector<z> a(size_t(n) * n), c(size_t(n) * n);
+#pragma omp parallel for schedule(static)
     for (size_t k = 0; k < a.size(); ++k) {
         a[k] = gen<z>(0xC057A0, 0, k);
         c[k] = gen<z>(0xC057C0, 0, k);
@@ -419,6 +422,7 @@ int run_bench_custom(const char* spec, char op, double seconds) {
                 off += (size_t(rs[i + 1] - rs[i]) * size_t(cs[j + 1] - cs[j]) + 63) / 64 * 64;
             }
         r.buf.assign(std::max<size_t>(off, 64), 0.f);
+#pragma omp parallel for schedule(static)
         for (size_t k = 0; k < r.buf.size(); ++k) r.buf[k] = gen<float>(seed, 0, k);
         size_t b = 0;
         for (size_t i = 0; i + 1 < rs.size(); ++i)
@@ -442,18 +446,17 @@ int run_bench_custom(const char* spec, char op, double seconds) {
         const size_t b = bi * (cs.size() - 1) + bj;
         return r.off[b] + size_t(j - cs[bj]) * size_t(rs[bi + 1] - rs[bi]) + size_t(i - rs[bi]);
     };
-    bool ok = true;
     const int M = crs.back(), N = ccs.back();
-    for (int j = 0; j < N && ok; j += 7)
+    long bad = 0;
+#pragma omp parallel for schedule(dynamic, 16) reduction(+ : bad)
+    for (int j = 0; j < N; j += 7)
         for (int i = 0; i < M; ++i) {
             const size_t kc = at(c, crs, ccs, i, j);
             const float x = op == 'N' ? a.buf[at(a, ars, acs, i, j)] : a.buf[at(a, ars, acs, j, i)];
             const float want = op == 'N' ? x : beta * c0[kc] + alpha * x;
-            if (c.buf[kc] != want) {
-                ok = false;
-                break;
-            }
+            bad += c.buf[kc] != want;
         }
+    const bool ok = bad == 0;
     int reps = 0;
     const double el = bench_loop<float>([&] { costa::transform<float>(A, C, op, alpha, beta, MPI_COMM_WORLD); },
                                         seconds, reps);
