@@ -208,6 +208,9 @@ struct launch_args {
 bool any_transpose(const std::vector<costa_tile_op_t>& ops);
 bool any_axpby(const std::vector<costa_tile_op_t>& ops);
 void launch_tiles(costa_dtype_t dtype, const launch_args& a, void* stream /* hipStream_t */);
+// walk of the destination bands in destination-address order (tuning builds: 1 boustrophedon,
+// 2 band pairs interleaved, 3 skewed band starts, 4 band quads; 0 = plain address order)
+constexpr int kDstOrderVariant = 0;
 // destination-block groups (tile_kernels.hip cblock_kernel): threads per workgroup and 16-byte
 // destination vectors per thread; a group holds at most kCblockThreads * kCblockChunks vectors
 constexpr int kCblockThreads = 256;
