@@ -1031,7 +1031,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
             for (size_t i = op0; i < ordered.size() && one_ld; ++i) one_ld = ordered[i].ldd == ld0;
             // (c64, on its 128 x 128 sub-tiles, ran 1 % slower with them: 4.36 against 4.31 ms)
             if (panel == 0)
-                panel = ld0 * E > (int64_t(128) << 10) && dtype != COSTA_CFLOAT ? (int64_t(128) << 10) / E : -1;
+                panel = ld0 * E > kPanelBytes && dtype != COSTA_CFLOAT ? kPanelBytes / E : -1;
             // key = panel (16 bits) | column (24) | row in the panel (24): a panel of 2^24 rows or
             // more, a column index or a panel index past its field keeps the plain address order
             if (panel >= (int64_t(1) << 24)) panel = -1;

@@ -211,6 +211,9 @@ void launch_tiles(costa_dtype_t dtype, const launch_args& a, void* stream /* hip
 // walk of the destination bands in destination-address order (tuning builds: 1 boustrophedon,
 // 2 band pairs interleaved, 3 skewed band starts, 4 band quads; 0 = plain address order)
 constexpr int kDstOrderVariant = 0;
+// destination columns taller than this are walked in panels of this many bytes of rows (engine.cpp
+// build_work)
+constexpr int64_t kPanelBytes = int64_t(128) << 10;
 // destination-block groups (tile_kernels.hip cblock_kernel): threads per workgroup and 16-byte
 // destination vectors per thread; a group holds at most kCblockThreads * kCblockChunks vectors
 constexpr int kCblockThreads = 256;
