@@ -473,167 +473,6 @@ template <> struct shapes<cpx<double>> {
 typedef __attribute__((address_space(3))) void lds_void;
 typedef const __attribute__((address_space(1))) void glob_void;
 
-// Staging of full transposing sub-tiles (tuning builds; 0 = register staging, shipped):
-//   1  LDS-DMA (global_load_lds_dwordx4 nt): no VGPR holds staged data, no ds_write phase
-//   2  the same, the sub-tile's two halves of rows waited for and stored one after the other
-//   3  LDS-DMA, each wavefront's instructions on consecutive source columns
-//   4  register staging, two halves as in 2
-//   5  register staging, each wavefront's loads on consecutive source columns
-//   6  LDS-DMA, one destination column per store instruction (fp64 64 x 128)
-//   7  register staging, the two s chunks of a column pair stored at once (by two wavefronts)
-//   8  LDS-DMA with the store order of 7
-//   9  register staging, a wavefront's stores on its own column pairs, both chunks back to back
-//   10 LDS-DMA with the store order of 9
-#ifndef COSTA_TR_STAGE
-#define COSTA_TR_STAGE 0
-#endif
-
-// A full transposing sub-tile staged by LDS-DMA.  The image has no pad: slot (s, q) (16 bytes,
-// V elements f = qV .. qV+V-1 of source column s) sits at s * Q + (q ^ (s % Q)), so the column-
-// wise slot reads of the store phase hit Q different bank groups.  An LDS-DMA instruction writes
-// 64 slots lane-linearly from a wave-uniform base; lane j of instruction i fills image slot
-// 64 i + j and loads whatever source vector belongs there.
-template <typename T, typename S, bool NT>
-__device__ __forceinline__ void tr_tile_glds(const costa_tile_op_t& op, int f0, int s0, const char* src_base,
-                                             char* dst_base, T alpha, T beta, T* tile) {
-    constexpr int V = S::V, BF = S::BF, BS = S::BS, Q = BF / V, NW = S::NW;
-    constexpr int NI = BS * Q / 64 / NW;  // LDS-DMA instructions per wavefront
-    static_assert(64 % Q == 0 && (BS * Q) % (64 * NW) == 0 && S::FW == 1, "glds mapping");
-    constexpr int MODE = COSTA_TR_STAGE;
-    const uint32_t flags = op.flags;
-    const uint32_t kind = (flags & COSTA_SCALE_MASK) >> COSTA_SCALE_SHIFT;
-    const bool conj = flags & COSTA_TILE_CONJ;
-    const int64_t lds = op.lds, ldd = op.ldd;
-    const T* src = reinterpret_cast<const T*>(src_base + op.src) + int64_t(s0) * lds + f0;
-    const int lane = int(threadIdx.x) % 64;
-    const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / 64);
-    char* tb = reinterpret_cast<char*>(tile);
-    // slot swizzle of row s: conflict-free 16-byte slot reads down a slot column (modes 1-3);
-    // mode 6 reads 8-byte halves of rows 2l and 2l + 1 in lane l: rows in pairs
-    auto swz = [](int s) { return MODE == 6 ? (s / 2) % Q : s % Q; };
-#pragma unroll
-    for (int k = 0; k < NI; ++k) {
-        const int i = MODE == 3 ? wave * NI + k : wave + NW * k;
-        const int slot = i * 64 + lane, s = slot / Q, q = (slot % Q) ^ swz(s);
-        __builtin_amdgcn_global_load_lds((glob_void*)(src + int64_t(s) * lds + q * V), (lds_void*)(tb + i * 1024),
-                                         16, 0, NT ? 2 : 0);
-    }
-    T* dst = reinterpret_cast<T*>(dst_base + op.dst) + int64_t(f0) * ldd + s0;
-    constexpr int QG = Q;  // store units per s chunk (FW = 1)
-    // mode 10 (tuning): the store order of register mode 9 (wave-contiguous units, a column
-    // pair's chunks back to back)
-    auto unit_u = [&](int k) { return MODE == 10 ? wave * S::PS + k : wave + NW * k; };
-    auto unit = [&](int k, int& f, int& sb) {
-        const int u = unit_u(k);
-        const int sc = MODE >= 8 ? u % (BS / 64) : u / QG, q = MODE >= 8 ? u / (BS / 64) : u % QG;
-        const int j = lane & (V - 1);
-        f = q * V + j;
-        sb = sc * 64 + (lane - j);
-    };
-    vec<T> old[S::PS];
-    if (kind == COSTA_SCALE_AXPBY) {
-#pragma unroll
-        for (int k = 0; k < S::PS; ++k) {
-            int f, sb;
-            unit(k, f, sb);
-            vload(old[k], dst + f * ldd + sb, V, true);
-        }
-    }
-    const raw16* img = reinterpret_cast<const raw16*>(tile);
-    auto store_units = [&](int k0, int k1) {
-        vec<T> y[S::PS];
-        if constexpr (MODE == 2) {
-            // the compiler waits for every LDS-DMA load before any LDS read it can see (vmcnt(0)):
-            // the reads of a half are issued as inline asm, ordered by the explicit waits
-            u32x4a r[S::PS];
-#pragma unroll
-            for (int k = k0; k < k1; ++k) {
-                const int u = unit_u(k);
-                const int sc = MODE >= 8 ? u % (BS / 64) : u / QG, q = MODE >= 8 ? u / (BS / 64) : u % QG;
-                const int s = sc * 64 + lane;
-                const uint32_t a = uint32_t(reinterpret_cast<uintptr_t>(
-                    (__attribute__((address_space(3))) const raw16*)(img + s * Q + (q ^ swz(s)))));
-                asm volatile("ds_read_b128 %0, %1" : "=v"(r[k]) : "v"(a) : "memory");
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-            for (int k = k0; k < k1; ++k) {
-                asm volatile("" : "+v"(r[k]));
-                __builtin_memcpy(&y[k], &r[k], 16);
-            }
-        } else {
-#pragma unroll
-            for (int k = k0; k < k1; ++k) {
-                const int u = unit_u(k);
-                const int sc = MODE >= 8 ? u % (BS / 64) : u / QG, q = MODE >= 8 ? u / (BS / 64) : u % QG;
-                const int s = sc * 64 + lane;
-                raw16 r = img[s * Q + (q ^ swz(s))];
-                __builtin_memcpy(&y[k], &r, 16);
-            }
-        }
-#pragma unroll
-        for (int k = k0; k < k1; ++k) {
-            vec<T> o = lane_transpose(y[k], lane);
-            int f, sb;
-            unit(k, f, sb);
-            if (kind != COSTA_SCALE_BITCOPY) {
-#pragma unroll
-                for (int e = 0; e < V; ++e)
-                    o.e[e] = scale(o.e[e], kind == COSTA_SCALE_AXPBY ? old[k].e[e] : e_zero<T>(), kind, conj,
-                                   alpha, beta);
-            }
-            vstore<T, NT>(dst + f * ldd + sb, o, V, true);
-        }
-    };
-    if constexpr (MODE == 6 && V == 2 && BS == 128) {
-        // one destination column per store instruction: unit k of wave w is column f =
-        // w + NW k, lane l holds its rows 2l, 2l + 1 (two 8-byte LDS reads, no lane exchange):
-        // 1 KiB of one column instead of 512 B of two
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();  // (no fence: the wait above orders the LDS-DMA)
-        constexpr int NU = BF / NW;
-        const T* img8 = tile;
-#pragma unroll
-        for (int k = 0; k < NU; ++k) {
-            const int f = wave + NW * k, q = f / V, h = f % V;
-            vec<T> o;
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                const int sr = 2 * lane + e;
-                o.e[e] = img8[(sr * Q + (q ^ swz(sr))) * V + h];
-            }
-            T* d = dst + int64_t(f) * ldd + 2 * lane;
-            if (kind != COSTA_SCALE_BITCOPY) {
-#pragma unroll
-                for (int e = 0; e < V; ++e) {
-                    T y = e_zero<T>();
-                    if (kind == COSTA_SCALE_AXPBY) y = d[e];
-                    o.e[e] = scale(o.e[e], y, kind, conj, alpha, beta);
-                }
-            }
-            vstore<T, NT>(d, o, V, true);
-        }
-        return;
-    }
-    if constexpr (MODE == 2) {
-        if (kind != COSTA_SCALE_AXPBY) {
-            // the first NI / 2 instructions of every wavefront hold rows [0, BS / 2): store units
-            // 0 .. PS / 2 - 1 read only those (vector memory completes in issue order)
-            static_assert(NI % 2 == 0 && S::PS % 2 == 0, "halves");
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI / 2) : "memory");
-            __builtin_amdgcn_s_barrier();  // (no fence: the waits above order the LDS-DMA)
-            store_units(0, S::PS / 2);
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S::PS / 2) : "memory");
-            __builtin_amdgcn_s_barrier();  // (no fence: the waits above order the LDS-DMA)
-            store_units(S::PS / 2, S::PS);
-            return;
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // (no fence: the waits above order the LDS-DMA)
-    store_units(0, S::PS);
-}
-
 // One sub-tile.  FULL: the sub-tile is a whole BF x BS block with 16-byte aligned rows on
 // both sides, so every guard below folds away and each thread issues its loads and stores
 // back to back with no per-lane branches (the common case: block-cyclic tiles).
@@ -651,26 +490,11 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
     const bool vd = FULL || (flags & COSTA_TILE_VEC_DST);
     const int64_t lds = op.lds, ldd = op.ldd;
     const T* src = reinterpret_cast<const T*>(src_base + op.src) + int64_t(s0) * lds + f0;
-    if constexpr (FULL && ((COSTA_TR_STAGE >= 1 && COSTA_TR_STAGE <= 3) || COSTA_TR_STAGE == 6 || COSTA_TR_STAGE == 8 ||
-                         COSTA_TR_STAGE == 10) &&
-                  !is_cpx<T>::value && S::FW == 1) {
-        if (flags & COSTA_TILE_TRANSPOSE) {
-            tr_tile_glds<T, S, NT>(op, f0, s0, src_base, dst_base, alpha, beta, tile);
-            return;
-        }
-    }
 
     // ---- load phase: lane -> (16-byte strip along f, column s); all loads issued first
     const int lf = (int(threadIdx.x) % S::LPC) * V;
     const int c0 = int(threadIdx.x) / S::LPC;
-    // source column of load k (COSTA_TR_STAGE 5, tuning: each wavefront's loads on consecutive
-    // columns instead of columns NW apart)
-    auto col_of = [&](int k) {
-        if constexpr (FULL && COSTA_TR_STAGE == 5 && 64 % S::LPC == 0 && (S::PL * S::CPP) % S::NW == 0)
-            return int(threadIdx.x) / 64 * (S::PL * S::CPP / S::NW) + k * (64 / S::LPC) +
-                   int(threadIdx.x) % 64 / S::LPC;
-        return c0 + k * S::CPP;
-    };
+    auto col_of = [&](int k) { return c0 + k * S::CPP; };  // source column of load k
     const int nf_lane = FULL ? V : tf - lf;  // elements of this lane's strip inside the tile
     vec<T> x[S::PL];
 #pragma unroll
@@ -737,27 +561,24 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
     T* dst = reinterpret_cast<T*>(dst_base + op.dst) + int64_t(f0) * ldd + s0;
     const int lane = int(threadIdx.x) % 64, wave = int(threadIdx.x) / 64;
     constexpr int SW = S::SW, FW = S::FW, QG = BF / V / FW;  // QG: f-slot groups per s chunk
-    // store unit u -> (s chunk, f-slot group): s chunk slowest; COSTA_TR_STAGE 7 (tuning): s chunk
-    // fastest, so a wavefront writes a column pair's chunks one after the other
+    // store unit u -> (s chunk, f-slot group): s chunk slowest, units NW apart per wavefront.
+    // PAIR (r5, the fp64 64 x 128 shape of BASELINE cfg 2): a wavefront stores its own column
+    // pairs, the two s chunks of a pair back to back, so each destination column's 1 KiB segment
+    // is written in one go.  Side by side on the same buffers (tools/libs_probe.py,
+    // profiles/r5l/): fp64 0.6990 -> 0.6934 ms; fp32 128 x 128 +2 %, c128 64 x 64 +4.5 %: those
+    // keep the strided order
     constexpr int NSC = S::BS / SW;
-    // PAIR (r5, the fp64 64 x 128 shape -- BASELINE cfg 2 -- as shipped; COSTA_TR_STAGE 9 for
-    // every shape in tuning builds): a wavefront stores its own column pairs, the two s chunks of
-    // a pair back to back, so each destination column's 1 KiB segment is written in one go.
-    // Side by side on the same buffers (tools/libs_probe.py, profiles/r5l/): fp64 0.6990 ->
-    // 0.6934 ms; fp32 128 x 128 +2 %, c128 64 x 64 +4.5 %: those keep the strided order
-    constexpr bool PAIR = FULL && (COSTA_TR_STAGE == 9 ||
-                                   (COSTA_TR_STAGE == 0 && std::is_same<T, double>::value && S::BF == 64 &&
-                                    S::BS == 128 && S::NT == 512));
+    constexpr bool PAIR = FULL && std::is_same<T, double>::value && S::BF == 64 && S::BS == 128 && S::NT == 512;
     auto unit_u = [&](int k) {
         if constexpr (PAIR) return wave * S::PS + k;
         return wave + S::NW * k;
     };
     auto unit_sc = [&](int u) {
-        if constexpr (PAIR || (FULL && COSTA_TR_STAGE == 7)) return u % NSC;
+        if constexpr (PAIR) return u % NSC;
         return u / QG;
     };
     auto unit_q = [&](int u) {
-        if constexpr (PAIR || (FULL && COSTA_TR_STAGE == 7)) return u / NSC;
+        if constexpr (PAIR) return u / NSC;
         return u % QG;
     };
     // store unit k of this lane: SW s values x FW f slots (64 x 1 for BS >= 64); after the lane
@@ -773,54 +594,6 @@ __device__ __forceinline__ void run_tile(const costa_tile_op_t& op, int f0, int 
     };
     // beta != 0: the old destination values are requested now, overlapping the source loads
     // still in flight (not after the LDS exchange, one round trip per store unit)
-    if constexpr (FULL && COSTA_TR_STAGE == 4 && !is_cpx<T>::value && S::FW == 1 && S::PL % 2 == 0 &&
-                  S::PS % 2 == 0) {
-        if (kind != COSTA_SCALE_AXPBY) {
-            // two halves of rows: loads k < PL / 2 hold rows [0, BS / 2), store units k < PS / 2
-            // read only those
-            auto put = [&](int k0, int k1) {
-#pragma unroll
-                for (int k = k0; k < k1; ++k) {
-                    raw16 r;
-                    __builtin_memcpy(&r, &x[k], 16);
-                    *reinterpret_cast<raw16*>(tile + col_of(k) * P + lf) = r;
-                }
-            };
-            vec<T> y[S::PS];
-            auto get = [&](int k0, int k1) {
-#pragma unroll
-                for (int k = k0; k < k1; ++k) {
-                    const int u = unit_u(k);
-                    const int sc = unit_sc(u), q = unit_q(u) * FW + lane / SW;
-                    raw16 r = *reinterpret_cast<const raw16*>(tile + (sc * SW + lane % SW) * P + q * V);
-                    __builtin_memcpy(&y[k], &r, 16);
-                }
-            };
-            auto put_out = [&](int k0, int k1) {
-#pragma unroll
-                for (int k = k0; k < k1; ++k) {
-                    vec<T> o = lane_transpose(y[k], lane);
-                    int f, sb, n;
-                    unit(k, f, sb, n);
-                    if (kind != COSTA_SCALE_BITCOPY) {
-#pragma unroll
-                        for (int e = 0; e < V; ++e)
-                            o.e[e] = scale(o.e[e], e_zero<T>(), kind, conj, alpha, beta);
-                    }
-                    vstore<T, NT>(dst + f * ldd + sb, o, V, true);
-                }
-            };
-            put(0, S::PL / 2);
-            __syncthreads();
-            get(0, S::PS / 2);
-            put(S::PL / 2, S::PL);
-            put_out(0, S::PS / 2);
-            __syncthreads();
-            get(S::PS / 2, S::PS);
-            put_out(S::PS / 2, S::PS);
-            return;
-        }
-    }
     vec<T> old[S::PS];
     if (kind == COSTA_SCALE_AXPBY) {
 #pragma unroll
