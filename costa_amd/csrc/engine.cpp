@@ -1051,26 +1051,6 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
                     }
                 }
             }
-            if (kDstOrderVariant > 0 && panel <= 0 && one_ld && bf > 0 && bs > 0) {
-                // tuning builds: other walks of the destination bands (band = bf destination
-                // columns, a band's sub-tiles bs rows apart)
-                uint64_t lo = ~uint64_t(0), hi = 0;
-                for (const auto& k : key) {
-                    lo = std::min(lo, k.first);
-                    hi = std::max(hi, k.first);
-                }
-                const uint64_t ld = uint64_t(ld0), nrb = (ld + uint64_t(bs) - 1) / uint64_t(bs);
-                for (auto& k : key) {
-                    const uint64_t e = (k.first - lo) / uint64_t(E);
-                    const uint64_t band = (e / ld) / uint64_t(bf), rb = (e % ld) / uint64_t(bs);
-                    uint64_t a = band, b = rb, c2 = 0;
-                    if (kDstOrderVariant == 1) b = band % 2 ? nrb - 1 - rb : rb;      // boustrophedon
-                    if (kDstOrderVariant == 2) a = band / 2, b = rb, c2 = band % 2;    // band pairs
-                    if (kDstOrderVariant == 3) b = (rb + band * 16) % nrb;             // skewed starts
-                    if (kDstOrderVariant == 4) a = band / 4, b = rb, c2 = band % 4;    // band quads
-                    k.first = (a << 40) | (b << 20) | c2;
-                }
-            }
             std::sort(key.begin(), key.end());
             for (size_t x = 0; x < key.size(); ++x) work[w0 + x] = key[x].second;
         }

@@ -208,9 +208,6 @@ struct launch_args {
 bool any_transpose(const std::vector<costa_tile_op_t>& ops);
 bool any_axpby(const std::vector<costa_tile_op_t>& ops);
 void launch_tiles(costa_dtype_t dtype, const launch_args& a, void* stream /* hipStream_t */);
-// walk of the destination bands in destination-address order (tuning builds: 1 boustrophedon,
-// 2 band pairs interleaved, 3 skewed band starts, 4 band quads; 0 = plain address order)
-constexpr int kDstOrderVariant = 0;
 // destination columns taller than this are walked in panels of this many bytes of rows (engine.cpp
 // build_work)
 constexpr int64_t kPanelBytes = int64_t(128) << 10;

@@ -72,14 +72,43 @@ class Lib:
         return st.local_ms / steps
 
 
+class Contig:
+    """a physically contiguous device buffer (hipExtMallocWithFlags) viewed as a torch tensor"""
+    hip = None
+
+    def __init__(self, nbytes, dt):
+        if Contig.hip is None:
+            Contig.hip = C.CDLL("libamdhip64.so")
+            Contig.hip.hipExtMallocWithFlags.argtypes = [C.POINTER(C.c_void_p), C.c_size_t, C.c_uint]
+        p = C.c_void_p()
+        assert Contig.hip.hipExtMallocWithFlags(C.byref(p), nbytes, 4) == 0
+        self.ptr = p.value
+        ts = {torch.float32: "<f4", torch.float64: "<f8", torch.complex64: "<c8", torch.complex128: "<c16"}[dt]
+        self.__cuda_array_interface__ = {"shape": (nbytes // torch.empty(0, dtype=dt).element_size(),),
+                                         "typestr": ts, "data": (self.ptr, False), "strides": None, "version": 2}
+        self.t = torch.as_tensor(self, device="cuda")
+
+
 def main():
     pairs = int(sys.argv[1])
     libs = []
     for a in sys.argv[2:]:
         lab, _, path = a.partition("=")
         libs.append((lab, Lib(path)))
-    bufs = [(torch.rand(N * N, dtype=TDT, device="cuda"), torch.zeros(N * N, dtype=TDT, device="cuda"))
-            for _ in range(pairs)]
+    # PROBE_ALLOC=mix: odd pairs in physically contiguous memory (hipDeviceMallocContiguous), so
+    # that both placement modes show up among the pairs (r5, tools/alloc_probe.py)
+    bufs, keep = [], []
+    for k in range(pairs):
+        if os.environ.get("PROBE_ALLOC") == "mix" and k % 2:
+            a, c = Contig(N * N * torch.empty(0, dtype=TDT).element_size(), TDT), \
+                Contig(N * N * torch.empty(0, dtype=TDT).element_size(), TDT)
+            keep += [a, c]
+            a, c = a.t, c.t
+            a.copy_(torch.rand(N * N, dtype=TDT, device="cuda"))
+            c.zero_()
+        else:
+            a, c = torch.rand(N * N, dtype=TDT, device="cuda"), torch.zeros(N * N, dtype=TDT, device="cuda")
+        bufs.append((a, c))
     print("pair  " + "  ".join(f"{lab:>10s}" for lab, _ in libs), flush=True)
     for k, (a, c) in enumerate(bufs):
         row = []
