@@ -812,12 +812,12 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         // 2.919 / 2.554 -> 2.101 / 2.103 ms, fp64 96^2 0.800 -> 0.699, 100^2 0.947 -> 0.700, 80^2
         // beta != 0 1.212 -> 1.030; filled sizes unchanged; profiles/r4s/).  COSTA_MERGE=1
         // (tuning): small ops only, as in r3
-        const int64_t half_large = kn0.merge == 1 ? int64_t(sh0.bf) * sh0.bs / 2 : INT64_MAX;
+        const int64_t half_large = kn0.merge == 1 ? int64_t(sh0.cf) * sh0.cs / 2 : INT64_MAX;
         std::vector<costa_tile_op_t> cand;  // the ops that may merge (the rest: ops_merged as they are)
         for (const auto& op : ops_in)
             (int64_t(op.nf) * op.ns < half_large ? cand : ops_merged).push_back(op);
         const size_t n_cand0 = cand.size();
-        cand = merge_filled(cand, int64_t(dtype_size(dtype)), sh0.bf, sh0.bs);
+        cand = merge_filled(cand, int64_t(dtype_size(dtype)), sh0.cf, sh0.cs);
         if (cand.size() < n_cand0) {
             ops_merged.insert(ops_merged.end(), cand.begin(), cand.end());
             ops_src = &ops_merged;
@@ -829,7 +829,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         const uint64_t E = dtype_size(dtype);
         shape_dims shm;
         tile_shapes(dtype, any_transpose(ops_in), &shm);
-        const int64_t min_elems = mis_env >= 0 ? 0 : int64_t(shm.bf) * shm.bs;
+        const int64_t min_elems = mis_env >= 0 ? 0 : int64_t(shm.cf) * shm.cs;
         for (auto& op : ops_mis) {
             if (int64_t(op.nf) * op.ns < min_elems) continue;
             if ((mis & 1) && op.dst % 4 == 0 && (uint64_t(op.ldd) * E) % 4 == 0) op.flags |= COSTA_TILE_VEC_DST;
@@ -847,7 +847,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     std::vector<const costa_tile_op_t*> wave_ops;  // ops for the wavefront path, in list order
     wave_ops.reserve(ops.size());
     const uint32_t vec_both = COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST;
-    const int64_t sub_elems = int64_t(sh.bf) * sh.bs;                // one large sub-tile
+    const int64_t sub_elems = int64_t(sh.cf) * sh.cs;                // one large class unit
     const int64_t med_elems = int64_t(sh.bf_m) * sh.bs_m;            // one medium sub-tile (0: none)
     // classify: wavefront path, the medium shape (aligned ops of at least half its sub-tile, in
     // lists that transpose) or the large shape

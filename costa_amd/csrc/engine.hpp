@@ -222,6 +222,8 @@ inline int64_t cblock_max_elems(int64_t E) { return int64_t(kCblockThreads) * kC
 // and the 32 x 32 shape the medium class takes when its ops all fit it (bf_s x bs_s)
 struct shape_dims {
     int bf = 0, bs = 0, bf_m = 0, bs_m = 0, bf_q = 0, bs_q = 0, bf_s = 0, bs_s = 0;
+    int cf = 0, cs = 0;  // the large class's dimensions (classification, merging): bf x bs for
+                         // transposing lists, the r4 copy sub-tile for copy-only lists
     int bf_k = 0, bs_k = 0;  // the skew shape (transposes into unaligned destinations; 0: none)
     int bf_kw = 0, bs_kw = 0;  // its wide variant (sources off the 16-byte grid too; 4-byte types)
 };

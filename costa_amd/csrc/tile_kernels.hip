@@ -382,20 +382,35 @@ struct shape {
 
 // the large shapes per element size: `large` for copy-only lists, `large_tr` for lists that
 // transpose.  Transposes of fp64 / fp32 / int32 take 512 threads and 64 KiB sub-tiles (~67 KiB
-// of LDS: two workgroups per CU, whose load and store phases overlap); copies, and c64 / c128,
-// 1024 threads and 128 KiB (copies stream 1 KiB column segments; c64 and c128 gained nothing
-// from the halving).  Measured on 16384^2 (r2, profiles/r2/shapes/):
-// fp64 'T' 64 x 128 against 128 x 128 / 1024 threads 0.698 against 0.712 ms with 256^2 and
-// 128^2 blocks, 0.779 against 1.057 with 64^2 blocks (those went to the wavefront path);
-// 128 x 64 slower (0.765-0.811); fp32 'T' 128 x 128 against 256 x 128 / 1024 threads 0.367
-// against 0.578 ms with 128^2 blocks (half-filled sub-tiles before), 0.397 against 0.402 with
-// 256^2; the copy of BASELINE cfg 3 (fp64, 128^2 blocks) 3.17 ms with 64 x 128 against 2.87 with
-// 128 x 128.
+// of LDS: two workgroups per CU, whose load and store phases overlap); c64 / c128 1024 threads
+// and 128 KiB.  Measured on 16384^2 (r2, profiles/r2/shapes/): fp64 'T' 64 x 128 against
+// 128 x 128 / 1024 threads 0.698 against 0.712 ms with 256^2 and 128^2 blocks, 0.779 against
+// 1.057 with 64^2 blocks (those went to the wavefront path); 128 x 64 slower (0.765-0.811); fp32
+// 'T' 128 x 128 against 256 x 128 / 1024 threads 0.367 against 0.578 ms with 128^2 blocks
+// (half-filled sub-tiles before), 0.397 against 0.402 with 256^2.
+// Copies (r5): 512 threads, two 16-byte loads a thread, 1 KiB column segments (16 KiB
+// sub-tiles of 1 KiB x 16 columns; no LDS, so many workgroups a CU).  A plain copy runs fastest
+// with few loads a thread in flight (profiles/r4zj/); side by side against r4's
+// 128 KiB sub-tiles with 8-32 loads a thread (profiles/r5v/, r5w/): BASELINE cfg 3's copy slice
+// (fp64 32768^2, 128^2 blocks) 2.797 -> 2.620 ms (6.56 TB/s), fp64 16384^2 256^2 blocks 0.68 ->
+// 0.65 ms (beta != 0: 1.07 -> 1.01), fp32 0.36 -> 0.322, c64 0.695 -> 0.650, c128 (128^2 blocks)
+// 1.45 -> 1.29; one load a thread (1024 threads) 3.13 ms on cfg 3, 128 x 8 sub-tiles 2.72-2.77,
+// 1024 threads x 2 loads 2.66.  Copy-only lists still classify and merge their ops by r4's
+// sub-tile sizes (copy_class below).
 // `medium_tr`: 256 threads, 16 KiB sub-tiles, for aligned transposing ops of at least half of
 // one that are below half a large sub-tile (before: cut into wavefront pieces of ~128-byte
 // runs): fp32 64^2 blocks 3.60 -> 4.77 TB/s, 96^2 4.18 -> 4.60; fp64 32^2 4.27 -> 4.97, 48^2
 // 4.27 -> 5.26 (profiles/r2/shapes/medium.log).  None for c64 / c128 (has_medium).
 template <typename T> struct shapes;
+// the sub-tile dimensions by which copy-only lists classify and merge their ops (engine.cpp
+// build_work: the large class = ops of at least half of one; merge_filled): r4's copy sub-tiles,
+// so that the r5 copy shapes change how the large class runs, not which ops it holds
+template <typename T> struct copy_class;
+template <> struct copy_class<float> { static constexpr int BF = 256, BS = 128; };
+template <> struct copy_class<int> { static constexpr int BF = 256, BS = 128; };
+template <> struct copy_class<double> { static constexpr int BF = 128, BS = 128; };
+template <> struct copy_class<cpx<float>> { static constexpr int BF = 128, BS = 128; };
+template <> struct copy_class<cpx<double>> { static constexpr int BF = 64, BS = 128; };
 // `small_tr` (fp64): the square 64 x 64 variant of the large transposing shape, 512 threads, for
 // transposing lists whose large ops all fit in it (engine.cpp build_work): a 64^2 block then fills
 // one sub-tile instead of half of a 64 x 128 one, and four workgroups fit a CU.  fp64 16384^2 'T'
@@ -406,7 +421,7 @@ template <typename T> struct shapes;
 // ragged ops 128 / 512 threads lost 12-21 % (48^2, 80^2)
 // and fp64 lost 12-14 % at 32^2 / 48^2 (profiles/r2d/medium_threads.log)
 template <> struct shapes<float> {
-    using large = shape<float, 1024, 256, 128>;
+    using large = shape<float, 512, 256, 16>;
     using large_tr = shape<float, 512, 128, 128>;
     using medium_tr = shape<float, 256, 64, 64>;
     static constexpr bool has_medium = true;
@@ -417,7 +432,7 @@ template <> struct shapes<float> {
     using small32_tr = shape<float, 128, 32, 32>;
 };
 template <> struct shapes<int> {
-    using large = shape<int, 1024, 256, 128>;
+    using large = shape<int, 512, 256, 16>;
     using large_tr = shape<int, 512, 128, 128>;
     using medium_tr = shape<int, 256, 64, 64>;
     static constexpr bool has_medium = true;
@@ -427,13 +442,8 @@ template <> struct shapes<int> {
     using medium_tr_full = shape<int, 128, 64, 64>;
     using small32_tr = shape<int, 128, 32, 32>;
 };
-// Copy lists of fp64 take 256 threads per 128 KiB sub-tile (each thread 32 16-byte loads in
-// flight, one workgroup per CU), c128 512 threads: BASELINE cfg 3's copy (32768^2 fp64, 128^2
-// blocks) 2.80-2.81 ms against 2.89-3.06 with 1024 threads, c128 16384^2 copies 1.469 against
-// 1.577 ms; fp64 256^2 blocks, fp32 and c64 unchanged or slower that way (tools/copy_probe.py,
-// profiles/r2c/copy_shapes/).
 template <> struct shapes<double> {
-    using large = shape<double, 256, 128, 128>;
+    using large = shape<double, 512, 128, 16>;
     using large_tr = shape<double, 512, 64, 128>;
     using medium_tr = shape<double, 256, 32, 64>;
     static constexpr bool has_medium = true;
@@ -448,7 +458,7 @@ template <> struct shapes<double> {
 // work_split::full) and lose 35-55 % with blocks that half-fill them (80^2 3.05 against 1.98 ms,
 // 96^2 2.35 against 1.74; profiles/r2c/tr_shapes/, profiles/r2d/c128_threads.log)
 template <> struct shapes<cpx<float>> {
-    using large = shape<cpx<float>, 1024, 128, 128>;
+    using large = shape<cpx<float>, 512, 128, 16>;
     using large_tr = shape<cpx<float>, 1024, 128, 128>;
     using medium_tr = large_tr;
     static constexpr bool has_medium = false;
@@ -459,7 +469,7 @@ template <> struct shapes<cpx<float>> {
     using small32_tr = shape<cpx<float>, 128, 32, 32>;
 };
 template <> struct shapes<cpx<double>> {
-    using large = shape<cpx<double>, 512, 64, 128>;
+    using large = shape<cpx<double>, 512, 64, 16>;
     using large_tr = shape<cpx<double>, 1024, 64, 128>;
     using medium_tr = large_tr;
     static constexpr bool has_medium = false;
@@ -1276,6 +1286,8 @@ template <typename T>
 void shape_of(bool tr, shape_dims* d) {
     d->bf = tr ? shapes<T>::large_tr::BF : shapes<T>::large::BF;
     d->bs = tr ? shapes<T>::large_tr::BS : shapes<T>::large::BS;
+    d->cf = tr ? shapes<T>::large_tr::BF : copy_class<T>::BF;
+    d->cs = tr ? shapes<T>::large_tr::BS : copy_class<T>::BS;
     const bool med = tr && shapes<T>::has_medium;
     d->bf_m = med ? shapes<T>::medium_tr::BF : 0;
     d->bs_m = med ? shapes<T>::medium_tr::BS : 0;

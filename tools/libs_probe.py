@@ -15,6 +15,7 @@ import torch
 DT = os.environ.get("PROBE_DT", "f64")
 N, B = int(os.environ.get("PROBE_N", "16384")), int(os.environ.get("PROBE_B", "256"))
 BETA = float(os.environ.get("PROBE_BETA", "0"))
+OP = os.environ.get("PROBE_OP", "T")  # N: the copy
 CODE, TDT = {"f32": (0, torch.float32), "f64": (1, torch.float64), "c64": (2, torch.complex64),
              "c128": (3, torch.complex128)}[DT]
 
@@ -59,7 +60,7 @@ class Lib:
     def ms(self, LA, LC, steps=10):
         def run(k):
             for _ in range(k):
-                assert self.L.costa_hip_transform_async(LA, LC, b"T", self.alpha, self.beta,
+                assert self.L.costa_hip_transform_async(LA, LC, OP.encode(), self.alpha, self.beta,
                                                         self.comm, None) == 0
             assert self.L.costa_hip_synchronize(self.comm) == 0
         run(2)
@@ -117,7 +118,8 @@ def main():
             row.append(lib.ms(LA, LC))
             torch.cuda.synchronize()
             if BETA == 0:
-                assert torch.equal(c.view(N, N), a.view(N, N).t()), f"{lab}: wrong result"
+                want = a.view(N, N) if OP == "N" else a.view(N, N).t()
+                assert torch.equal(c.view(N, N), want), f"{lab}: wrong result"
             c.zero_()
         print(f"{k:4d}  " + "  ".join(f"{x:10.4f}" for x in row), flush=True)
 

@@ -78,7 +78,7 @@ static std::set<uint32_t> expected_shaped(costa_dtype_t dt, const std::vector<co
     for (const auto& o : ops) tr = tr || (o.flags & COSTA_TILE_TRANSPOSE);
     shape_dims sh;
     tile_shapes(dt, tr, &sh);
-    const int64_t E = int64_t(dtype_size(dt)), big = int64_t(sh.bf) * sh.bs, med = int64_t(sh.bf_m) * sh.bs_m;
+    const int64_t E = int64_t(dtype_size(dt)), big = int64_t(sh.cf) * sh.cs, med = int64_t(sh.bf_m) * sh.bs_m;
     const uint32_t both = COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST;
     const int64_t skew_elems = int64_t(sh.bf_k) * sh.bs_k;
     std::set<uint32_t> large, medium;
@@ -110,7 +110,7 @@ static int64_t big_elems(costa_dtype_t dt, const std::vector<costa_tile_op_t>& o
     for (const auto& o : ops) tr = tr || (o.flags & COSTA_TILE_TRANSPOSE);
     shape_dims sh;
     tile_shapes(dt, tr, &sh);
-    return int64_t(sh.bf) * sh.bs;
+    return int64_t(sh.cf) * sh.cs;  // the large class (engine.cpp build_work)
 }
 
 // `ops` must carry unique, non-zero hints; expect_large: ops that must go to a sub-tiled shape
