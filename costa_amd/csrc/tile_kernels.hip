@@ -456,7 +456,10 @@ template <> struct shapes<double> {
 // c128 transposes: 1024 threads.  256 gain 3 % when every op is a whole number of sub-tiles (cfg
 // 4's 128^2 blocks: 2.19 against 2.26 ms; the `large_tr_full` launch, engine.cpp
 // work_split::full) and lose 35-55 % with blocks that half-fill them (80^2 3.05 against 1.98 ms,
-// 96^2 2.35 against 1.74; profiles/r2c/tr_shapes/, profiles/r2d/c128_threads.log)
+// 96^2 2.35 against 1.74; profiles/r2c/tr_shapes/, profiles/r2d/c128_threads.log).  The square
+// 64 x 64 sub-tile (cfg 4's destination-ordered lists, r4) takes 1024 threads since r5: 4 loads a
+// thread, one workgroup a CU (72 VGPRs); cfg 4's 32768^2 slice 8.58-8.64 -> 8.38-8.44 ms against
+// 256 threads (512: 8.61-8.64; profiles/r5y/)
 template <> struct shapes<cpx<float>> {
     using large = shape<cpx<float>, 512, 128, 16>;
     using large_tr = shape<cpx<float>, 1024, 128, 128>;
@@ -473,7 +476,7 @@ template <> struct shapes<cpx<double>> {
     using large_tr = shape<cpx<double>, 1024, 64, 128>;
     using medium_tr = large_tr;
     static constexpr bool has_medium = false;
-    using small_tr = shape<cpx<double>, 256, 64, 64>;
+    using small_tr = shape<cpx<double>, 1024, 64, 64>;
     static constexpr bool has_small = true;
     using large_tr_full = shape<cpx<double>, 256, 64, 128>;
     using medium_tr_full = medium_tr;
