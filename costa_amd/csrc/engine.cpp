@@ -334,10 +334,10 @@ bool any_axpby(const std::vector<costa_tile_op_t>& ops) {
 // Copy mode: a part of one wavefront pass (64 lanes x tiny_copy_lane_bytes), an op the wavefront
 // moves in one round trip, cut finer for more wavefronts in flight.  Local lists: half (2 KiB);
 // r3 with the XCD column bands, cfg 5 'N' 0.434-0.436 ms at 2 KiB against 0.446-0.447 at 3 KiB,
-// 0.438 at 2.5, 0.449-0.451 at 1.5, 0.466 at 4, 0.517 at 1 (profiles/r3b/copy_budget/).  Pack
+// 0.438 at 2.5, 0.449-0.451 at 1.5, 0.466 at 4, 0.517 at 1 (profiles/r3b/README.md §copy_budget).  Pack
 // and unpack lists (one side the dense package): three quarters (3 KiB); through the loopback
 // exchange pack 'N' 0.587-0.590 ms against 0.607-0.608 at 2 KiB, unpack 0.592-0.597 against
-// 0.607-0.608 (profiles/r3b/copy_budget/lb2_loopback.txt; r11: 3 KiB best for every list,
+// 0.607-0.608 (profiles/r3b/README.md §copy_budget; r11: 3 KiB best for every list,
 // profiles/r11/c5_budget_uc64.log).
 // (COSTA_TINY_COPY: another budget in bytes up to kTinyCopyBytes, tuning runs only)
 int64_t tiny_copy_budget(int64_t E, bool local) {
@@ -388,7 +388,7 @@ wave_grid wave_pieces(const costa_tile_op_t& op, int64_t E, bool local) {
     // as tall along s as the budget allows: the destination runs (which a beta != 0 op both reads
     // and writes) stay long.  cfg 5 'T' 0.726 ms with near-square pieces (32 wide), 0.716 with 16,
     // 0.728 with 12, 0.758 with 8, 0.754 cut along s first; fp64 / c64 / c128 pack and unpack
-    // lists equal at 16 (profiles/r3b/side/).  Copy: whole columns when one fits, else tall pieces
+    // lists equal at 16 (profiles/r3b/README.md §side).  Copy: whole columns when one fits, else tall pieces
     static const int64_t side_env = [] {  // COSTA_TR_SIDE (tuning): the cut's side along f
         const char* v = tuning_env("COSTA_TR_SIDE");
         return v ? std::max<int64_t>(1, std::atoll(v)) : int64_t(0);
@@ -750,7 +750,7 @@ struct wave_knobs {  // defaults, overridable for tuning runs
                         // bands, k per XCD (xcd_bands); 0: off.  cfg 5 'N' 0.476 -> 0.446 ms with
                         // k = 1 (2 / 4 / 16: 0.464 / 0.475 / 0.490), 'T' equal; through the
                         // loopback exchange unpack 'N' 0.609 -> 0.592, 'T' 1.016 -> 0.960
-                        // (profiles/r3b/bands/)
+                        // (profiles/r3b/README.md §bands)
     int sort = 5;    // COSTA_TINY_SORT 0: list order, 1: by source, 2: by destination address,
                      // 3: by the planner's locality hint (costa_tile_op_t::order), 4: 3 for
                      // copy-only lists, 2 for lists that transpose (cfg 5 'T' 3.88 against
@@ -764,7 +764,7 @@ struct wave_knobs {  // defaults, overridable for tuning runs
                      // 0.751-0.761, unpack equal
 };
 // f-neighbour skew sub-tiles grouped per XCD on the wide variant (fp32 16384^2 'T', both sides
-// lld 16385: 0.453 / 0.440 / 0.428 / 0.419-0.424 ms with groups of 1 / 2 / 4 / 8; profiles/r3b/skew/)
+// lld 16385: 0.453 / 0.440 / 0.428 / 0.419-0.424 ms with groups of 1 / 2 / 4 / 8; profiles/r3b/README.md §skew)
 constexpr int64_t kSkewWideGroup = 8;
 const wave_knobs& knobs() {
     static wave_knobs k = [] {

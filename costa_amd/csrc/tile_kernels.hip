@@ -734,7 +734,7 @@ __global__ __launch_bounds__(S::NT) void tile_kernel(const costa_tile_op_t* __re
 // lines shared with the f-neighbour sub-tiles, which engine.cpp build_work then puts on one XCD);
 // fp32 16384^2 'T' lld 16385 both sides 0.456 -> 0.419-0.424 ms with that grouping, while
 // destination-only lists lost with it (0.384 -> 0.430: they keep 32 x 512, no grouping;
-// profiles/r3b/skew/)
+// profiles/r3b/README.md §skew)
 template <typename T, bool WIDE = false>
 struct skew_shape {
     static constexpr int NT = 512;
@@ -868,11 +868,11 @@ void launch_skew(const launch_args& a, const uint64_t* work, int64_t n, hipStrea
 // (next op's loads in flight while this op stores: 2.9 against 4.4 TB/s), nt cache policy here.
 // r3: transposing ops stage through LDS-DMA and request their old destination values before
 // the one wait (tiny_transpose_glds): cfg 5 'T' 0.781 -> 0.743 ms on one lease (4 waves per
-// workgroup), 0.722 with 8; without the early old-value loads 0.948 (profiles/r3b/glds/).
+// workgroup), 0.722 with 8; without the early old-value loads 0.948 (profiles/r3b/README.md §glds).
 // Wavefronts per workgroup: 8 (4 KiB of LDS each for lists that transpose; copy-only lists
 // without LDS: profiles/r06/c5_knobs.log).
 // r3 (LDS-DMA staging): cfg 5 'T' 0.736-0.738 ms with 4 wavefronts per workgroup, 0.721-0.723
-// with 8, 0.728-0.729 with 16, 0.759-0.761 with 2 (profiles/r3b/glds/)
+// with 8, 0.728-0.729 with 16, 0.759-0.761 with 2 (profiles/r3b/README.md §glds)
 constexpr int TINY_WAVES_TR = 8;
 constexpr int TINY_WAVES_COPY = 8;
 // the same for the copy path (engine.hpp tiny_copy_lane_bytes): 64 for every type since r11
