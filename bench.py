@@ -1064,7 +1064,8 @@ def main():
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
             "traffic_source": traffic_src,
             "kernel": (f"tile_kernel<{kdt}> ({name} list)" if args.workload != "cfg5" else
-                       f"tiny_kernel<float> ({name} list: every op is below the large shape)"),
+                       f"cblock_kernel<float> + tiny_kernel<float> ({name} list: destination-block "
+                       f"groups, the few ops outside them as wavefront pieces)"),
             "bytes_per_launch": int(per_launch),
             "avg_launch_ms": round(avg_ms, 4)}
 
