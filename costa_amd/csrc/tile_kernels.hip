@@ -1067,7 +1067,19 @@ __global__ __launch_bounds__(CB_NT) void cblock_kernel(const costa_tile_op_t* __
     constexpr int V = 16 / int(sizeof(T)), NW = CB_NT / 64;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     T* img = reinterpret_cast<T*>(smem);
-    const uint64_t h = work[blockIdx.x];
+    // Transposing lists: workgroups are dealt round-robin over the 8 XCDs; renumbered so that
+    // each XCD takes 4 consecutive groups of the destination order and the 8 XCDs work on 8
+    // adjacent such chunks -- neighbouring groups read the other parts of the same source cache
+    // lines, now in one L2.  cfg 5 'T' 0.634 -> 0.600 ms (chunks of 2 / 16: 0.603 / 0.605; one
+    // contiguous slice per XCD 0.625, its L2 -> memory reads -36 %); the copy ('N') is level or
+    // slower every way (8 slices: +5 %) and keeps the plain order (profiles/r5ab/, r5ac/)
+    uint64_t g = blockIdx.x;
+    if constexpr (TR) {
+        constexpr int64_t XK = 4, SC = 8 * XK;
+        const int64_t b = blockIdx.x, base = b / SC * SC;
+        if (base + SC <= int64_t(gridDim.x)) g = uint64_t(base + (b % 8) * XK + (b / 8) % XK);
+    }
+    const uint64_t h = work[g];
     const costa_tile_op_t hd = ops[h];
     const int n_ops = int(hd.src), R = hd.nf, K = hd.ns, P = R | 1;
     const uint32_t flags = hd.flags;

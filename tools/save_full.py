@@ -75,8 +75,21 @@ def counter(base, kind, kern):
 def save_pmc(fetch_dir, write_dir, log, kern, name, read_share):
     """one workload's HBM traffic per launch from its FETCH_SIZE and WRITE_SIZE passes;
     read_share: the algorithmic reads' share of the algorithmic bytes"""
-    fk, fi = counter(fetch_dir, "FETCH_SIZE", kern)
-    wk, wi = counter(write_dir, "WRITE_SIZE", kern)
+    # several kernels of one phase (cfg 5: the destination-block groups and the wavefront
+    # pieces): each kernel's largest-grid median, summed
+    kerns = kern if isinstance(kern, tuple) else (kern,)
+    fk = wk = 0.0
+    fi, wi = {}, {}
+    for k in kerns:
+        f1, i1 = counter(fetch_dir, "FETCH_SIZE", k)
+        w1, j1 = counter(write_dir, "WRITE_SIZE", k)
+        if f1 is None or w1 is None:
+            continue
+        fk, wk = fk + f1, wk + w1
+        fi[k], wi[k] = i1, j1
+    if not fi:
+        fk = wk = None
+    kern = " + ".join(kerns)
     d = line(log) if os.path.exists(log) else None
     if fk is None or wk is None or not d:
         return
@@ -99,7 +112,8 @@ save_pmc(os.path.join(src, "pmc_FETCH_SIZE"), os.path.join(src, "pmc_WRITE_SIZE"
 c5 = src + "_c5pmc"
 for op, share in (("N", 0.5), ("T", 2 / 3)):
     save_pmc(os.path.join(c5, f"pmc_{op}_FETCH_SIZE"), os.path.join(c5, f"pmc_{op}_WRITE_SIZE"),
-             os.path.join(c5, f"pmc_{op}_FETCH_SIZE.log"), "tiny_kernel<float", f"pmc_cfg5_{op}.json", share)
+             os.path.join(c5, f"pmc_{op}_FETCH_SIZE.log"), ("cblock_kernel<float", "tiny_kernel<float"),
+             f"pmc_cfg5_{op}.json", share)
     st = os.path.join(c5, f"prof_{op}", "trace_kernel_stats.csv")
     if os.path.exists(st):
         shutil.copy(st, os.path.join(dst, f"c5{op}_trace_kernel_stats.csv"))
