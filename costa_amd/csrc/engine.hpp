@@ -216,6 +216,18 @@ constexpr int64_t kPanelBytes = int64_t(128) << 10;
 constexpr int kCblockThreads = 256;
 constexpr int kCblockChunks = 4;
 inline int64_t cblock_max_elems(int64_t E) { return int64_t(kCblockThreads) * kCblockChunks * (16 / E); }
+// work-list position of workgroup b of a launch of nb destination-block groups of a transposing
+// list (tile_kernels.hip cblock_kernel): the hardware deals workgroups round-robin over the 8
+// XCDs; chunks of kCblockXcdChunk consecutive groups go to one XCD, the 8 XCDs on 8 adjacent
+// chunks; the last partial round of chunks keeps the plain order.  A permutation of [0, nb)
+// (tools/work_check.cpp xcd).  (constexpr: host and device.)
+constexpr int64_t kCblockXcdChunk = 4;
+constexpr int64_t cblock_xcd_order(int64_t b, int64_t nb) {
+    return b / (8 * kCblockXcdChunk) * (8 * kCblockXcdChunk) + 8 * kCblockXcdChunk <= nb
+               ? b / (8 * kCblockXcdChunk) * (8 * kCblockXcdChunk) + (b % 8) * kCblockXcdChunk +
+                     (b / 8) % kCblockXcdChunk
+               : b;
+}
 // sub-tile shapes (elements along the source's fast dim, along its slow dim) of a copy-only list
 // or of a list with transposing ops: the large shape, the medium one (bf_m = bs_m = 0: none) and
 // the large shape's square variant for lists whose large ops all fit it (bf_q = bs_q = 0: none),

@@ -1074,11 +1074,7 @@ __global__ __launch_bounds__(CB_NT) void cblock_kernel(const costa_tile_op_t* __
     // contiguous slice per XCD 0.625, its L2 -> memory reads -36 %); the copy ('N') is level or
     // slower every way (8 slices: +5 %) and keeps the plain order (profiles/r5ab/, r5ac/)
     uint64_t g = blockIdx.x;
-    if constexpr (TR) {
-        constexpr int64_t XK = 4, SC = 8 * XK;
-        const int64_t b = blockIdx.x, base = b / SC * SC;
-        if (base + SC <= int64_t(gridDim.x)) g = uint64_t(base + (b % 8) * XK + (b / 8) % XK);
-    }
+    if constexpr (TR) g = uint64_t(cblock_xcd_order(int64_t(blockIdx.x), int64_t(gridDim.x)));
     const uint64_t h = work[g];
     const costa_tile_op_t hd = ops[h];
     const int n_ops = int(hd.src), R = hd.nf, K = hd.ns, P = R | 1;

@@ -48,6 +48,9 @@ def test_work_lists_cfg5(tmp_path):
     # with the pieces cover every op of cfg 5's lists; column bands of blocks over the budget
     r = subprocess.run([str(exe), "cblock"], capture_output=True, text=True, timeout=300, env=clean)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
+    # the transposing groups' XCD chunk order is a permutation of every launch size
+    r = subprocess.run([str(exe), "xcd"], capture_output=True, text=True, timeout=300, env=clean)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
 
 
 TUNING = {"COSTA_TINY_SORT": "0", "COSTA_FORCE_SQ": "1", "COSTA_LARGE_SORT": "0", "COSTA_XCD_BANDS": "0",

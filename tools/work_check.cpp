@@ -363,6 +363,22 @@ static bool check_cblock(const std::string& name, costa_dtype_t dt, const std::v
     return true;
 }
 
+// the destination-block groups' XCD chunk order (engine.hpp cblock_xcd_order) is a permutation of
+// the launch, whatever its size
+static bool check_xcd() {
+    const std::string name = "xcd order";
+    for (int64_t nb = 1; nb <= 4096; ++nb) {
+        std::vector<char> seen(size_t(nb), 0);
+        for (int64_t b = 0; b < nb; ++b) {
+            const int64_t g = cblock_xcd_order(b, nb);
+            CHECK(g >= 0 && g < nb && !seen[size_t(g)], "nb %lld, b %lld -> %lld", (long long)nb, (long long)b,
+                  (long long)g);
+            seen[size_t(g)] = 1;
+        }
+    }
+    return true;
+}
+
 static bool check_cblocks() {
     const int n = 16384;
     auto LA = layout(splits(0xC5A1, 8, 96, n), splits(0xC5A2, 8, 96, n), uint64_t(1) << 40);
@@ -537,6 +553,11 @@ int main(int argc, char** argv) {
     }
     if (argc > 1 && std::string(argv[1]) == "cover") {
         if (!check_covers()) return 1;
+        std::printf("ok\n");
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "xcd") {
+        if (!check_xcd()) return 1;
         std::printf("ok\n");
         return 0;
     }
