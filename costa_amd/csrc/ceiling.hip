@@ -16,6 +16,14 @@
 //           workgroup copies 4 columns' 1 KiB segments.  Kinds 3 and 4 keep fewer loads in flight
 //           per thread (1 against 4) and ran 6.6-6.7 TB/s against kind 1's 6.2-6.3 on MI355X
 //           (profiles/r4zj/)
+//   kind 5  the headline transpose's access pattern without its LDS exchange (a probe, not a
+//           ceiling: tools/pairs_probe.py): src and dst square column-major fp64 matrices of
+//           `col_bytes`-byte columns, 512-thread workgroups on 64 x 128 sub-tiles in destination
+//           order; each thread loads 8 16-byte vectors where the transpose loads them (128 source
+//           columns x 512 B) and stores 8 where it stores (64 destination columns x 1 KiB),
+//           the data merely moved, not transposed
+//   kind 6  the same pattern for 128 x 128 sub-tiles (1 KiB segments on both sides), 1024 threads
+//   kind 7  kind 5's loads with flat stores; kind 8  flat loads with kind 5's stores
 //
 // costa_ceiling_copy_ms runs `reps` timed repetitions (HIP events on its own stream) after one
 // untimed one and writes every repetition's milliseconds to ms_out[0..reps).  Returns 0, or a
@@ -80,6 +88,65 @@ __global__ __launch_bounds__(kThreads) void seg_copy_1(const u32x4* __restrict__
     __builtin_nontemporal_store(__builtin_nontemporal_load(a + i), c + i);
 }
 
+// kind 5: the transpose's loads and stores without LDS (fp64, 64 x 128 sub-tiles, 512 threads)
+__global__ __launch_bounds__(512) void tr_pattern(const u32x4* __restrict__ a, u32x4* __restrict__ c,
+                                                  long n, long sblocks) {
+    const long w = blockIdx.x;
+    const long f0 = (w / sblocks) * 64, s0 = (w % sblocks) * 128;  // band-major destination order
+    const int t = int(threadIdx.x);
+    u32x4 x[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {  // source column s0 + t / 32 + 16 k, rows f0 + 2 (t % 32) ..
+        const long s = s0 + t / 32 + 16 * k;
+        x[k] = __builtin_nontemporal_load(a + (s * n + f0) / 2 + t % 32);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {  // destination column f0 + 8 (t / 64) + k, rows s0 + 2 (t % 64) ..
+        const long f = f0 + 8 * (t / 64) + k;
+        __builtin_nontemporal_store(x[k], c + (f * n + s0) / 2 + t % 64);
+    }
+}
+
+// kind 6: the same for 128 x 128 sub-tiles (1 KiB segments on both sides), 1024 threads
+__global__ __launch_bounds__(1024) void tr_pattern_sq(const u32x4* __restrict__ a, u32x4* __restrict__ c,
+                                                      long n, long sblocks) {
+    const long w = blockIdx.x;
+    const long f0 = (w / sblocks) * 128, s0 = (w % sblocks) * 128;
+    const int t = int(threadIdx.x);
+    u32x4 x[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {  // source column s0 + t / 64 + 16 k, rows f0 + 2 (t % 64) ..
+        const long s = s0 + t / 64 + 16 * k;
+        x[k] = __builtin_nontemporal_load(a + (s * n + f0) / 2 + t % 64);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {  // destination column f0 + 8 (t / 64) + k, rows s0 + 2 (t % 64) ..
+        const long f = f0 + 8 * (t / 64) + k;
+        __builtin_nontemporal_store(x[k], c + (f * n + s0) / 2 + t % 64);
+    }
+}
+
+// kinds 7 / 8: half of kind 5's pattern each -- 7: its loads, stores flat (workgroup w writes
+// the 64 KiB at w * 64 KiB); 8: loads flat, its stores
+template <bool TR_LOADS>
+__global__ __launch_bounds__(512) void tr_half_pattern(const u32x4* __restrict__ a, u32x4* __restrict__ c,
+                                                       long n, long sblocks) {
+    const long w = blockIdx.x;
+    const long f0 = (w / sblocks) * 64, s0 = (w % sblocks) * 128;
+    const int t = int(threadIdx.x);
+    u32x4 x[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const long s = s0 + t / 32 + 16 * k;
+        x[k] = __builtin_nontemporal_load(TR_LOADS ? a + (s * n + f0) / 2 + t % 32 : a + w * 4096 + k * 512 + t);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const long f = f0 + 8 * (t / 64) + k;
+        __builtin_nontemporal_store(x[k], TR_LOADS ? c + w * 4096 + k * 512 + t : c + (f * n + s0) / 2 + t % 64);
+    }
+}
+
 }  // namespace
 
 extern "C" int costa_ceiling_copy_ms(int kind, const void* src, void* dst, uint64_t bytes,
@@ -90,6 +157,15 @@ extern "C" int costa_ceiling_copy_ms(int kind, const void* src, void* dst, uint6
     if (kind == 1 || kind == 4) {
         // whole 16-column groups of whole 1 KiB segments only: no tail handling needed
         if (col_bytes == 0 || col_bytes % kSegBytes || bytes % (kSegs * col_bytes)) return -1;
+    } else if (kind == 6) {
+        const uint64_t n = col_bytes / 8;
+        if (col_bytes % 1024 || bytes != n * col_bytes) return -1;
+        grid = long((n / 128) * (n / 128));
+    } else if (kind == 5 || kind == 7 || kind == 8) {
+        // square fp64: n = col_bytes / 8 columns of n elements, n a multiple of 128
+        const uint64_t n = col_bytes / 8;
+        if (col_bytes % 1024 || bytes != n * col_bytes) return -1;
+        grid = long((n / 64) * (n / 128));
     } else if (kind != 0 && kind != 2 && kind != 3) {
         return -1;
     }
@@ -111,8 +187,20 @@ extern "C" int costa_ceiling_copy_ms(int kind, const void* src, void* dst, uint6
             hipLaunchKernelGGL(flat_copy, dim3(unsigned(grid)), dim3(kThreads), 0, s, a, c);
         else if (kind == 3)
             hipLaunchKernelGGL(flat_copy_1k, dim3(unsigned(grid)), dim3(64), 0, s, a, c);
-        else
+        else if (kind == 4)
             hipLaunchKernelGGL(seg_copy_1, dim3(unsigned(grid)), dim3(kThreads), 0, s, a, c, col16, spc);
+        else if (kind == 5)
+            hipLaunchKernelGGL(tr_pattern, dim3(unsigned(grid)), dim3(512), 0, s, a, c, long(col_bytes / 8),
+                               long(col_bytes / 8 / 128));
+        else if (kind == 7)
+            hipLaunchKernelGGL(tr_half_pattern<true>, dim3(unsigned(grid)), dim3(512), 0, s, a, c,
+                               long(col_bytes / 8), long(col_bytes / 8 / 128));
+        else if (kind == 8)
+            hipLaunchKernelGGL(tr_half_pattern<false>, dim3(unsigned(grid)), dim3(512), 0, s, a, c,
+                               long(col_bytes / 8), long(col_bytes / 8 / 128));
+        else
+            hipLaunchKernelGGL(tr_pattern_sq, dim3(unsigned(grid)), dim3(1024), 0, s, a, c, long(col_bytes / 8),
+                               long(col_bytes / 8 / 128));
         return hipGetLastError();
     };
     int rc = 0;

@@ -2,7 +2,8 @@
 buffers in one process (r5: its rate depends on where the driver places the buffers physically --
 the same virtual addresses ran 0.665 or 0.70 ms after a reallocation -- while the copy of the same
 bytes does not move).  Per pair: the transpose's kernel time (library events, 10 calls) and the
-one-vector strided copy (libcosta_ceiling kind 4).  Under rocprofv3 --pmc the dispatches can be
+one-vector strided copy (libcosta_ceiling kind 4) and the transpose's access pattern without LDS
+(kind 5).  Under rocprofv3 --pmc the dispatches can be
 split by duration into the two modes.
     python tools/pairs_probe.py [pairs] [rounds]
     python tools/pairs_probe.py cross [n]      n A x n C buffers, every combination"""
@@ -77,8 +78,18 @@ def main():
             costa.set_profiling(False)
             cm = (C.c_float * 10)()
             f(4, a.data_ptr(), c.data_ptr(), BYTES, N * 8, 10, cm)
-            print(f"round {r} pair {k}: transpose {ms:.4f} ms  copy(kind 4) {statistics.median(list(cm)):.4f} ms",
-                  flush=True)
+            pm = (C.c_float * 10)()  # the transpose's access pattern without LDS (ceiling.hip kind 5)
+            rc = f(5, a.data_ptr(), c.data_ptr(), BYTES, N * 8, 10, pm)
+            pat = f"{statistics.median(list(pm)):.4f}" if rc == 0 else f"rc {rc}"
+            qm = (C.c_float * 10)()  # the same for 128 x 128 sub-tiles (kind 6)
+            rc = f(6, a.data_ptr(), c.data_ptr(), BYTES, N * 8, 10, qm)
+            pat += f"  pattern128(kind 6) {statistics.median(list(qm)):.4f}" if rc == 0 else f"  rc6 {rc}"
+            for kd, lab in ((7, "tr-loads"), (8, "tr-stores")):
+                hm = (C.c_float * 10)()
+                rc = f(kd, a.data_ptr(), c.data_ptr(), BYTES, N * 8, 10, hm)
+                pat += f"  {lab}(kind {kd}) {statistics.median(list(hm)):.4f}" if rc == 0 else f"  rc{kd} {rc}"
+            print(f"round {r} pair {k}: transpose {ms:.4f} ms  copy(kind 4) {statistics.median(list(cm)):.4f} ms"
+                  f"  pattern(kind 5) {pat} ms", flush=True)
 
 
 if __name__ == "__main__":
