@@ -24,6 +24,7 @@
 //           the data merely moved, not transposed
 //   kind 6  the same pattern for 128 x 128 sub-tiles (1 KiB segments on both sides), 1024 threads
 //   kind 7  kind 5's loads with flat stores; kind 8  flat loads with kind 5's stores
+//   kinds 100 + 10 g + m  the pattern of other sub-tile geometries (pat_g below)
 //
 // costa_ceiling_copy_ms runs `reps` timed repetitions (HIP events on its own stream) after one
 // untimed one and writes every repetition's milliseconds to ms_out[0..reps).  Returns 0, or a
@@ -147,6 +148,39 @@ __global__ __launch_bounds__(512) void tr_half_pattern(const u32x4* __restrict__
     }
 }
 
+// kinds 100 + 10 g + m (probes): the transposing access pattern of BF x BS fp64 sub-tiles (64 KiB,
+// 512 threads, 8 16-byte vectors a thread each way, destination order), geometry g: 0 64 x 128,
+// 1 32 x 256, 2 16 x 512, 3 128 x 64, 4 256 x 32; m 0: transposed loads and stores, 1: flat
+// loads (workgroup w reads the 64 KiB at w * 64 KiB) with transposed stores, 2: transposed loads
+// with flat stores
+template <int BF, int BS, int M>
+__global__ __launch_bounds__(512) void pat_g(const u32x4* __restrict__ a, u32x4* __restrict__ c, long n) {
+    constexpr int LPC = BF / 2, CPP = 512 / LPC, LPD = BS / 2, CPD = 512 / LPD;
+    static_assert(BF * BS == 8192 && CPP * 8 == BS && CPD * 8 == BF, "geometry");
+    const long sblocks = n / BS, w = blockIdx.x;
+    const long f0 = (w / sblocks) * BF, s0 = (w % sblocks) * BS;
+    const int t = int(threadIdx.x);
+    u32x4 x[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const long s = s0 + t / LPC + CPP * k;
+        x[k] = __builtin_nontemporal_load(M == 1 ? a + w * 4096 + k * 512 + t : a + (s * n + f0) / 2 + t % LPC);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const long f = f0 + t / LPD + CPD * k;
+        __builtin_nontemporal_store(x[k], M == 2 ? c + w * 4096 + k * 512 + t : c + (f * n + s0) / 2 + t % LPD);
+    }
+}
+template <int BF, int BS>
+hipError_t launch_pat(int m, const u32x4* a, u32x4* c, long n, hipStream_t s) {
+    const unsigned grid = unsigned((n / BF) * (n / BS));
+    if (m == 0) hipLaunchKernelGGL((pat_g<BF, BS, 0>), dim3(grid), dim3(512), 0, s, a, c, n);
+    if (m == 1) hipLaunchKernelGGL((pat_g<BF, BS, 1>), dim3(grid), dim3(512), 0, s, a, c, n);
+    if (m == 2) hipLaunchKernelGGL((pat_g<BF, BS, 2>), dim3(grid), dim3(512), 0, s, a, c, n);
+    return hipGetLastError();
+}
+
 }  // namespace
 
 extern "C" int costa_ceiling_copy_ms(int kind, const void* src, void* dst, uint64_t bytes,
@@ -161,6 +195,10 @@ extern "C" int costa_ceiling_copy_ms(int kind, const void* src, void* dst, uint6
         const uint64_t n = col_bytes / 8;
         if (col_bytes % 1024 || bytes != n * col_bytes) return -1;
         grid = long((n / 128) * (n / 128));
+    } else if (kind >= 100 && kind < 150 && kind % 10 < 3) {
+        const uint64_t n = col_bytes / 8;
+        if (col_bytes % 4096 || bytes != n * col_bytes) return -1;
+        grid = 1;
     } else if (kind == 5 || kind == 7 || kind == 8) {
         // square fp64: n = col_bytes / 8 columns of n elements, n a multiple of 128
         const uint64_t n = col_bytes / 8;
@@ -181,6 +219,15 @@ extern "C" int costa_ceiling_copy_ms(int kind, const void* src, void* dst, uint6
     const long col16 = long(col_bytes / 16), spc = long(col_bytes / kSegBytes);
     auto once = [&]() -> hipError_t {
         if (kind == 0) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s);
+        if (kind >= 100) {
+            const long n = long(col_bytes / 8);
+            const int g = (kind - 100) / 10, m = kind % 10;
+            if (g == 0) return launch_pat<64, 128>(m, a, c, n, s);
+            if (g == 1) return launch_pat<32, 256>(m, a, c, n, s);
+            if (g == 2) return launch_pat<16, 512>(m, a, c, n, s);
+            if (g == 3) return launch_pat<128, 64>(m, a, c, n, s);
+            return launch_pat<256, 32>(m, a, c, n, s);
+        }
         if (kind == 1)
             hipLaunchKernelGGL(seg_copy, dim3(unsigned(grid)), dim3(kThreads), 0, s, a, c, col16, spc);
         else if (kind == 2)
