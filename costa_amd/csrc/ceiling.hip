@@ -25,6 +25,7 @@
 //   kind 6  the same pattern for 128 x 128 sub-tiles (1 KiB segments on both sides), 1024 threads
 //   kind 7  kind 5's loads with flat stores; kind 8  flat loads with kind 5's stores
 //   kinds 100 + 10 g + m  the pattern of other sub-tile geometries (pat_g below)
+//   kinds 200 + p  kind 5 with other store cache policies (tr_pattern_pol below)
 //
 // costa_ceiling_copy_ms runs `reps` timed repetitions (HIP events on its own stream) after one
 // untimed one and writes every repetition's milliseconds to ms_out[0..reps).  Returns 0, or a
@@ -181,6 +182,36 @@ hipError_t launch_pat(int m, const u32x4* a, u32x4* c, long n, hipStream_t s) {
     return hipGetLastError();
 }
 
+// kinds 200 + p (probes): kind 5's pattern with the stores' cache policy p: 0 nt, 1 default,
+// 2 sc1, 3 sc1 nt, 4 sc0 nt, 5 sc0 sc1 nt (vector stores through inline asm)
+template <int P>
+__device__ __forceinline__ void st_pol(u32x4* p, u32x4 v) {
+    if constexpr (P == 0) __builtin_nontemporal_store(v, p);
+    if constexpr (P == 1) asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(p), "v"(v) : "memory");
+    if constexpr (P == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+    if constexpr (P == 3) asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
+    if constexpr (P == 4) asm volatile("global_store_dwordx4 %0, %1, off sc0 nt" ::"v"(p), "v"(v) : "memory");
+    if constexpr (P == 5) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
+}
+template <int P>
+__global__ __launch_bounds__(512) void tr_pattern_pol(const u32x4* __restrict__ a, u32x4* __restrict__ c,
+                                                      long n, long sblocks) {
+    const long w = blockIdx.x;
+    const long f0 = (w / sblocks) * 64, s0 = (w % sblocks) * 128;
+    const int t = int(threadIdx.x);
+    u32x4 x[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const long s = s0 + t / 32 + 16 * k;
+        x[k] = __builtin_nontemporal_load(a + (s * n + f0) / 2 + t % 32);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const long f = f0 + 8 * (t / 64) + k;
+        st_pol<P>(c + (f * n + s0) / 2 + t % 64, x[k]);
+    }
+}
+
 }  // namespace
 
 extern "C" int costa_ceiling_copy_ms(int kind, const void* src, void* dst, uint64_t bytes,
@@ -199,7 +230,7 @@ extern "C" int costa_ceiling_copy_ms(int kind, const void* src, void* dst, uint6
         const uint64_t n = col_bytes / 8;
         if (col_bytes % 4096 || bytes != n * col_bytes) return -1;
         grid = 1;
-    } else if (kind == 5 || kind == 7 || kind == 8) {
+    } else if (kind == 5 || kind == 7 || kind == 8 || (kind >= 200 && kind <= 205)) {
         // square fp64: n = col_bytes / 8 columns of n elements, n a multiple of 128
         const uint64_t n = col_bytes / 8;
         if (col_bytes % 1024 || bytes != n * col_bytes) return -1;
@@ -219,6 +250,19 @@ extern "C" int costa_ceiling_copy_ms(int kind, const void* src, void* dst, uint6
     const long col16 = long(col_bytes / 16), spc = long(col_bytes / kSegBytes);
     auto once = [&]() -> hipError_t {
         if (kind == 0) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s);
+        if (kind >= 200) {
+            const long n = long(col_bytes / 8), sb = n / 128;
+            const dim3 gr(unsigned((n / 64) * (n / 128)));
+            switch (kind - 200) {
+            case 0: hipLaunchKernelGGL(tr_pattern_pol<0>, gr, dim3(512), 0, s, a, c, n, sb); break;
+            case 1: hipLaunchKernelGGL(tr_pattern_pol<1>, gr, dim3(512), 0, s, a, c, n, sb); break;
+            case 2: hipLaunchKernelGGL(tr_pattern_pol<2>, gr, dim3(512), 0, s, a, c, n, sb); break;
+            case 3: hipLaunchKernelGGL(tr_pattern_pol<3>, gr, dim3(512), 0, s, a, c, n, sb); break;
+            case 4: hipLaunchKernelGGL(tr_pattern_pol<4>, gr, dim3(512), 0, s, a, c, n, sb); break;
+            default: hipLaunchKernelGGL(tr_pattern_pol<5>, gr, dim3(512), 0, s, a, c, n, sb); break;
+            }
+            return hipGetLastError();
+        }
         if (kind >= 100) {
             const long n = long(col_bytes / 8);
             const int g = (kind - 100) / 10, m = kind % 10;

@@ -2,7 +2,8 @@
 100 + 10 g + m: fp64 sub-tile geometry g = 64 x 128 / 32 x 256 / 16 x 512 / 128 x 64 / 256 x 32;
 m 0 both sides transposed, 1 flat loads + transposed stores, 2 transposed loads + flat stores)
 beside the headline transpose and the one-vector copy, per buffer pair (16384^2 fp64).
-    python tools/pattern_probe.py [pairs]"""
+    python tools/pattern_probe.py [pairs] [pol]   (pol: kind 5 with each store cache policy,
+                                                   kinds 200-205)"""
 import ctypes as C
 import os
 import statistics
@@ -17,10 +18,13 @@ import costa_amd as costa  # noqa: E402
 N, B = 16384, 256
 BYTES = N * N * 8
 GEO = ["64x128", "32x256", "16x512", "128x64", "256x32"]
+POL = False
 
 
 def main():
     pairs = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+    global POL
+    POL = len(sys.argv) > 2 and sys.argv[2] == "pol"
     costa.lib()
     comm = costa.Comm.self(0)
     ceil = C.CDLL(os.path.join(ROOT, "costa_amd", "lib", "libcosta_ceiling.so"))
@@ -47,8 +51,12 @@ def main():
         ms = costa.get_stats(reset=True)["local_ms"] / 10
         costa.set_profiling(False)
         line = [f"pair {k}: transpose {ms:.4f} copy {med(4, a, c):.4f}"]
-        for g, name in enumerate(GEO):
-            line.append(f"{name} " + "/".join(f"{med(100 + 10 * g + m, a, c):.4f}" for m in range(3)))
+        if POL:  # kind 5's pattern with each store cache policy
+            line.append("stores nt / default / sc1 / sc1 nt / sc0 nt / sc0 sc1 nt " +
+                        " / ".join(f"{med(200 + q, a, c):.4f}" for q in range(6)))
+        else:
+            for g, name in enumerate(GEO):
+                line.append(f"{name} " + "/".join(f"{med(100 + 10 * g + m, a, c):.4f}" for m in range(3)))
         print("  ".join(line), flush=True)
         del LA, LC, a, c
         costa.release_caches()
