@@ -26,6 +26,7 @@
 //   kind 7  kind 5's loads with flat stores; kind 8  flat loads with kind 5's stores
 //   kinds 100 + 10 g + m  the pattern of other sub-tile geometries (pat_g below)
 //   kinds 200 + p  kind 5 with other store cache policies (tr_pattern_pol below)
+//   kinds 300 + o  kind 5 with other sub-tile orders (tr_pattern_ord below)
 //
 // costa_ceiling_copy_ms runs `reps` timed repetitions (HIP events on its own stream) after one
 // untimed one and writes every repetition's milliseconds to ms_out[0..reps).  Returns 0, or a
@@ -212,6 +213,35 @@ __global__ __launch_bounds__(512) void tr_pattern_pol(const u32x4* __restrict__ 
     }
 }
 
+// kinds 300 + o (probes): kind 5's pattern with another order of the sub-tiles (workgroup i ->
+// band, s-block; nb bands of 64 destination columns, sb s-blocks of 128 rows):
+// 0 band-major (shipped), 1 each band bottom to top, 2 the bands in reverse, 3 boustrophedon,
+// 4 one band per XCD (workgroups are dealt round-robin over 8 XCDs: 8 bands in flight, XCD x on
+// band 8 j + x), 5 four bands advancing together one s-block at a time
+__global__ __launch_bounds__(512) void tr_pattern_ord(const u32x4* __restrict__ a, u32x4* __restrict__ c,
+                                                      long n, int o) {
+    const long sb = n / 128, nb = n / 64, i = blockIdx.x;
+    long band = i / sb, blk = i % sb;
+    if (o == 1) blk = sb - 1 - blk;
+    if (o == 2) band = nb - 1 - band;
+    if (o == 3 && band % 2) blk = sb - 1 - blk;
+    if (o == 4) band = 8 * (i / (8 * sb)) + i % 8, blk = (i / 8) % sb;
+    if (o == 5) band = 4 * (i / (4 * sb)) + i % 4, blk = (i % (4 * sb)) / 4;
+    const long f0 = band * 64, s0 = blk * 128;
+    const int t = int(threadIdx.x);
+    u32x4 x[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const long s = s0 + t / 32 + 16 * k;
+        x[k] = __builtin_nontemporal_load(a + (s * n + f0) / 2 + t % 32);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const long f = f0 + 8 * (t / 64) + k;
+        __builtin_nontemporal_store(x[k], c + (f * n + s0) / 2 + t % 64);
+    }
+}
+
 }  // namespace
 
 extern "C" int costa_ceiling_copy_ms(int kind, const void* src, void* dst, uint64_t bytes,
@@ -230,7 +260,8 @@ extern "C" int costa_ceiling_copy_ms(int kind, const void* src, void* dst, uint6
         const uint64_t n = col_bytes / 8;
         if (col_bytes % 4096 || bytes != n * col_bytes) return -1;
         grid = 1;
-    } else if (kind == 5 || kind == 7 || kind == 8 || (kind >= 200 && kind <= 205)) {
+    } else if (kind == 5 || kind == 7 || kind == 8 || (kind >= 200 && kind <= 205) ||
+               (kind >= 300 && kind <= 305)) {
         // square fp64: n = col_bytes / 8 columns of n elements, n a multiple of 128
         const uint64_t n = col_bytes / 8;
         if (col_bytes % 1024 || bytes != n * col_bytes) return -1;
@@ -250,6 +281,12 @@ extern "C" int costa_ceiling_copy_ms(int kind, const void* src, void* dst, uint6
     const long col16 = long(col_bytes / 16), spc = long(col_bytes / kSegBytes);
     auto once = [&]() -> hipError_t {
         if (kind == 0) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s);
+        if (kind >= 300) {
+            const long n = long(col_bytes / 8);
+            hipLaunchKernelGGL(tr_pattern_ord, dim3(unsigned((n / 64) * (n / 128))), dim3(512), 0, s, a, c, n,
+                               kind - 300);
+            return hipGetLastError();
+        }
         if (kind >= 200) {
             const long n = long(col_bytes / 8), sb = n / 128;
             const dim3 gr(unsigned((n / 64) * (n / 128)));
