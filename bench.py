@@ -196,6 +196,10 @@ def start_watchdog(rank: int, world: int, budget_s: float):
         if rank == 0:
             line = {"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world}
             line.update(_partial_line)
+            # a timed-out run is no measurement: value stays null, the headline measured so far
+            # goes under partial_value
+            line["partial_value"] = line.pop("value", None)
+            line["value"] = None
             line.update({"error": "timeout", "budget_s": budget_s,
                          "last_phase": {"0": _last_phase[0]}})
             print(json.dumps(line), flush=True)
@@ -601,6 +605,96 @@ def cpu_baseline_configs(items, target_s: float = 8.0):
     return out
 
 
+CPU_MR_ENV = "COSTA_BENCH_CPU_MR"
+MPIEXEC = "/opt/conda/bin/mpiexec"  # MPICH, the MPI the reference harness is linked against
+
+
+def cpu_baseline_multirank(world: int, keys_x, target_s: float = 6.0, exe=None):
+    """The REFERENCE's multi-rank path beside an N-rank line (N = world): oracle/_ref/ref_harness
+    bench_mr under `mpiexec -n N` on the host cores -- every rank packs, exchanges by MPI
+    Isend / Irecv and unpacks (transform.cpp:46-128), each call between two MPI_Barriers
+    (utils/pxgemr2d_utils.hpp:284-292).  The usable CPUs are split over the ranks (OpenMP threads
+    per rank).  Workloads, shrunk to slices the host holds and runs in seconds:
+      headline  pxtran fp64 'T' weak-scaled, 8192^2 per rank (the GPU line: 16384^2) on the
+                same pm x pn grid, 256^2 blocks
+      cfg3      pxgemr2d fp64 'N' 2x2 -> 4x1 remap (N = 4), 8192^2 per rank (16384^2 global;
+                the GPU line: 65536^2), 128^2 blocks
+      cfg4      pztranu c128 'T' alpha, beta on 2x4 (N = 8), 16384^2 global (GPU: 32768^2)
+      cfg5      the full 16384^2 fp32 custom layouts, owners uniform over the N ranks ('N'/'T')
+    Child processes only, started before anything touches the GPU.
+    -> {"headline" | entry key: cpu_baseline dict (kind "reference", ranks N)}; a workload the
+    binary cannot run is left out with a warning on stderr."""
+    import shutil
+    import subprocess
+    import tempfile
+    import numpy as np
+    exe = exe or os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    mpiexec = MPIEXEC if os.path.exists(MPIEXEC) else shutil.which("mpiexec")
+    if not os.path.exists(exe) or not mpiexec:
+        print("bench.py: WARNING oracle/_ref/ref_harness or mpiexec absent: no multi-rank CPU "
+              "baseline", file=sys.stderr)
+        return {}
+    threads, info = host_cpus()
+    per = max(1, threads // world)
+    pm, pn = grid_for(world)
+    env = dict(os.environ, OMP_NUM_THREADS=str(per))
+    env["PATH"] = os.path.dirname(mpiexec) + ":" + env.get("PATH", "")
+    out = {}
+    for key, kind, edge in [("headline", "pxtran", None)] + list(keys_x):
+        spec = None
+        if kind == "pxtran":
+            args = ["pxtran", "8192", "256", str(pm), str(pn)]
+            sample = (f"pxtran fp64 'T' alpha=1 beta=0 weak-scaled, {8192 * pm}x{8192 * pn} on the "
+                      f"{pm}x{pn} rank grid (8192^2 per rank: a quarter of the GPU line's), 256x256 "
+                      f"blocks")
+        elif kind == "cfg3":
+            cm = world  # C on world x 1
+            args = ["cfg3", "8192", "128", str(pm), str(pn)]
+            sample = (f"pxgemr2d fp64 'N' {8192 * pm}x{8192 * pn}, {pm}x{pn} -> {cm}x1 remap, "
+                      f"128x128 blocks (a slice of configs[2]'s 65536^2)")
+        elif kind == "cfg4":
+            args = ["cfg4", "16384", "128", str(pm), str(pn)]
+            sample = (f"pztranu complex<double> 'T' alpha=(0.75,-0.5) beta=(1.25,0.25), 16384x16384 "
+                      f"on the {pm}x{pn} rank grid, 128x128 blocks (a slice of configs[3]'s 32768^2)")
+        elif kind == "cfg5":
+            op = edge if edge in ("N", "T") else "N"
+            fd, spec = tempfile.mkstemp(suffix=".txt")
+            ars, acs, crs, ccs = cfg5_splits()
+            aown = np.random.default_rng(0xC5A5).integers(0, world, (len(ars) - 1, len(acs) - 1))
+            cown = np.random.default_rng(0xC5A6).integers(0, world, (len(crs) - 1, len(ccs) - 1))
+            with os.fdopen(fd, "w") as f:
+                for rs, cs, own in ((ars, acs, aown), (crs, ccs, cown)):
+                    f.write(f"{len(rs)} " + " ".join(map(str, rs)) + "\n")
+                    f.write(f"{len(cs)} " + " ".join(map(str, cs)) + "\n")
+                    f.write(" ".join(map(str, own.reshape(-1).tolist())) + "\n")
+            args = ["custom", spec, op]
+            sample = (f"configs[4]'s full 16384x16384 fp32 custom layouts, owners uniform over the "
+                      f"{world} ranks (as the GPU line), op {op}")
+        else:
+            continue
+        try:
+            r = subprocess.run([mpiexec, "-n", str(world), exe, "bench_mr"] + args + [str(target_s)],
+                               capture_output=True, text=True, timeout=8 * target_s + 120, env=env)
+            d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+            if r.returncode != 0 or not d.get("verified"):
+                raise RuntimeError(f"rc {r.returncode}, verified {d.get('verified')}")
+        except Exception as e:
+            print(f"bench.py: WARNING multi-rank reference CPU baseline of {key} failed ({e})",
+                  file=sys.stderr)
+            continue
+        finally:
+            if spec:
+                os.unlink(spec)
+        out[key] = {"value": round(d["GBps"], 3), "unit": "GB/s", "cores": d["threads"] * d["ranks"],
+                    "kind": "reference", "ranks": d["ranks"],
+                    "sample": f"{sample}: the reference's costa::transform on {d['ranks']} MPI ranks "
+                              f"(MPICH, one host; planning included, as every reference call "
+                              f"re-plans), each call between two MPI_Barriers, {d['reps']} calls in "
+                              f"{d['seconds']:.1f} s, OpenMP {d['threads']} threads a rank, verified"}
+        out[key].update(info)
+    return out
+
+
 def cfg5_workload(costa, torch, rank, world, op):
     """BASELINE configs[4]: fp32 16384^2 custom_layout; A tile edges uniform in
     [8, 96] (seeds 0xC5A1 rows / 0xC5A2 cols), C edges uniform in [16, 160] (0xC5A3 / 0xC5A4),
@@ -689,6 +783,51 @@ def mismatch_arena(Cm, ca, op, gen, C0=None, al=1.0, be=0.0, n=None):
     return count_mismatch(Cm[e], exp)
 
 
+def extra_keys(world: int, args):
+    """BASELINE's other configurations, measured after the headline in the same processes: at
+    the GPU counts they are quoted on (cfg 3 at 4 GPUs, cfg 4 and cfg 5 at 8), and at one GPU
+    their single-GPU slices, each beside the reference's own CPU rate.
+    -> [(entry key, config, edge / op)]"""
+    extra_plan = {1: [("cfg3", None), ("cfg4", 32768), ("cfg5", "N"), ("cfg5", "T")],
+                  4: [("cfg3", None)], 8: [("cfg4", 32768), ("cfg5", "N")]}
+    plan_x = extra_plan.get(world, [])
+    if args.extra:
+        plan_x = []
+        for item in args.extra.split(","):
+            k, _, e = item.partition(":")
+            plan_x.append((k, (int(e) if e.isdigit() else e) if e else None))
+    if args.workload != "pxtran" or args.no_extra:
+        plan_x = []
+    keys_x = []
+    for kind, edge in plan_x:
+        used = {k for k, _, _ in keys_x}
+        keys_x.append((kind if kind not in used else f"{kind}_{edge}", kind, edge))
+    return keys_x
+
+
+def spawn_ranks(cmd, args, runner=None) -> int:
+    """The parent of `bench.py --gpus N` (N > 1, no launcher): the reference's multi-rank CPU
+    baselines first (cpu_baseline_multirank, before any rank touches the GPU; their results reach
+    rank 0 through a file named by COSTA_BENCH_CPU_MR), then the N ranks (run_ranks, or `runner`
+    in the tests) -> the ranks' exit code"""
+    import tempfile
+    runner = runner or run_ranks
+    budget = float(os.environ.get("COSTA_BENCH_BUDGET_S", RUN_BUDGET_S))
+    path = None
+    if not args.no_cpu_baseline and args.workload == "pxtran":
+        mr = cpu_baseline_multirank(args.gpus, extra_keys(args.gpus, args))
+        fd, path = tempfile.mkstemp(prefix="costa_cpu_mr_", suffix=".json")
+        with os.fdopen(fd, "w") as f:
+            json.dump(mr, f)
+        os.environ[CPU_MR_ENV] = path
+    try:
+        return runner(cmd, budget, args.gpus)
+    finally:
+        if path:
+            os.environ.pop(CPU_MR_ENV, None)
+            os.unlink(path)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -723,35 +862,29 @@ def main():
         if have < args.gpus:
             print(f"bench.py: --gpus {args.gpus} but {have} GPU(s) visible", file=sys.stderr)
             raise SystemExit(2)
-        budget = float(os.environ.get("COSTA_BENCH_BUDGET_S", RUN_BUDGET_S))
-        raise SystemExit(run_ranks(cmd, budget, args.gpus))
+        raise SystemExit(spawn_ranks(cmd, args))
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "pxtran"
-    # BASELINE's other configurations, measured after the headline in the same processes: at
-    # the GPU counts they are quoted on (cfg 3 at 4 GPUs, cfg 4 and cfg 5 at 8), and at one GPU
-    # their single-GPU slices, each beside the reference's own CPU rate
-    extra_plan = {1: [("cfg3", None), ("cfg4", 32768), ("cfg5", "N"), ("cfg5", "T")],
-                  4: [("cfg3", None)], 8: [("cfg4", 32768), ("cfg5", "N")]}
-    plan_x = extra_plan.get(world, [])
-    if args.extra:
-        plan_x = []
-        for item in args.extra.split(","):
-            k, _, e = item.partition(":")
-            plan_x.append((k, (int(e) if e.isdigit() else e) if e else None))
-    if args.workload != "pxtran" or args.no_extra:
-        plan_x = []
-    keys_x = []  # (entry key, config, edge / op)
-    for kind, edge in plan_x:
-        used = {k for k, _, _ in keys_x}
-        keys_x.append((kind if kind not in used else f"{kind}_{edge}", kind, edge))
+    keys_x = extra_keys(world, args)
     # the reference's own CPU path, as child processes before anything touches the GPU
     if want_cpu:
         phase(rank, "CPU baselines (the reference on the host cores)")
     cpu_ref = cpu_baseline_reference(n=args.edge, b=args.block) if want_cpu else None
     cpu_x = cpu_baseline_configs(keys_x) if want_cpu and keys_x else {}
+    # N > 1: the reference's multi-rank path (mpiexec -n N), measured by the spawning parent
+    # (COSTA_BENCH_CPU_MR names its file) or, under an outside launcher, here by rank 0 -- in
+    # both cases before this process touches the GPU
+    cpu_mr = {}
+    if rank == 0 and world > 1 and not args.no_cpu_baseline and args.workload == "pxtran":
+        path = os.environ.get(CPU_MR_ENV)
+        if path and os.path.exists(path):
+            cpu_mr = json.load(open(path))
+        else:
+            phase(rank, f"CPU baselines (the reference on {world} MPI ranks)")
+            cpu_mr = cpu_baseline_multirank(world, keys_x)
     import torch
     import torch.distributed as dist
     import costa_amd as costa
@@ -1020,7 +1153,10 @@ def main():
                "exchange_ms_per_step": round(r["exchange_ms"], 4),
                "phase_ms_per_step": {k: round(r["st"][k + "_ms"] / steps, 4)
                                      for k in ("pack", "local", "unpack")},
-               "first_call_ms": round(r["first_call_ms"], 2), "verified": r["verified"]}
+               "first_call_ms": round(r["first_call_ms"], 2), "verified": r["verified"],
+               # the pass the phase (kernel) times come from, so that kernel <= step reads off
+               # the entry itself
+               "events_pass_ms_per_step": round(r["el_ev"] / steps * 1e3, 4)}
         for k in ("grid", "m", "n", "block"):
             if k in w:
                 out[k] = w[k]
@@ -1195,9 +1331,8 @@ def main():
             extra[key] = summary(wx, rx, ksteps)
             if key in cpu_x:
                 extra[key]["cpu_baseline"] = cpu_x[key]
-            elif world > 1:
-                extra[key]["cpu_baseline"] = ("measured at N = 1 only (rank 0's host cores): the "
-                                              "one-GPU line's baseline_configs entry of this config")
+            elif key in cpu_mr:
+                extra[key]["cpu_baseline"] = cpu_mr[key]
             del wx, rx
             costa.release_caches()
             torch.cuda.empty_cache()
@@ -1213,6 +1348,8 @@ def main():
             cpu["port"] = {k: port[k] for k in ("value", "cores", "kind", "sample")}
         else:
             cpu["note"] = "REFERENCE BINARY ABSENT: this is our restatement (kind 'port')"
+    elif cpu_mr.get("headline"):
+        cpu = cpu_mr["headline"]
 
     if rank == 0:
         def js(x):  # complex scalars as [re, im]

@@ -601,12 +601,19 @@ namespace {
 // header indices in destination order; the grouped ops leave `wave_ops`.  COSTA_CBLOCK=0
 // (tuning): off.
 int64_t cblock_groups(costa_dtype_t dtype, std::vector<const costa_tile_op_t*>& wave_ops, list_kind kind,
-                      std::vector<costa_tile_op_t>& ordered, std::vector<uint64_t>& work, int64_t& lds) {
+                      std::vector<costa_tile_op_t>& ordered, std::vector<uint64_t>& work, int64_t& lds,
+                      int& map) {
     static const int on = [] {
         const char* s = tuning_env("COSTA_CBLOCK");
         return s ? std::atoi(s) : 1;
     }();
+    // COSTA_CB_BANDS (tuning): 1 XCD column bands for every list, 0 never, -1 (default) as below
+    static const int bands_env = [] {
+        const char* s = tuning_env("COSTA_CB_BANDS");
+        return s ? std::atoi(s) : -1;
+    }();
     lds = 0;
+    map = cb_round_robin;
     // real types (complex elements are on the large shapes wherever it matters: cfg 4)
     const bool real = dtype == COSTA_FLOAT || dtype == COSTA_DOUBLE || dtype == COSTA_INT32;
     if (!on || !real || kind == list_pack || wave_ops.size() < 2) return 0;
@@ -693,6 +700,44 @@ int64_t cblock_groups(costa_dtype_t dtype, std::vector<const costa_tile_op_t*>& 
     }
     if (out.empty()) return 0;
     std::sort(out.begin(), out.end(), [](const group& x, const group& y) { return x.dst < y.dst; });
+    bool any_tr = false;
+    for (const auto& g : out) any_tr = any_tr || (g.flags & COSTA_TILE_TRANSPOSE);
+    map = any_tr ? cb_xcd_chunks : cb_round_robin;
+    const bool bands = bands_env == 1;
+    if (bands && out.size() >= 16) {
+        // XCD column bands: the groups in the planner's column-major order of their first target
+        // tile are cut into 8 slices of the kernel's sizes (xcd_slice_order), slice x -- one band
+        // of target columns -- walked by XCD x in destination order.  A source block split by a
+        // target block-row boundary is then read by two groups of one XCD about 1/8 of a
+        // block-row of its traffic apart, and the line they share is still in its L2.
+        std::vector<uint32_t> hint(out.size(), 0);
+        bool hints = true;
+        for (size_t i = 0; i < out.size() && hints; ++i) {
+            uint32_t h = UINT32_MAX;
+            for (const auto& op : out[i].ops) h = std::min(h, op.order);
+            hints = h != 0 && h != UINT32_MAX;
+            hint[i] = h;
+        }
+        if (hints) {
+            const size_t n = out.size(), per = n / 8, rem = n % 8;
+            std::vector<uint32_t> by(n);
+            for (size_t i = 0; i < n; ++i) by[i] = uint32_t(i);
+            std::stable_sort(by.begin(), by.end(), [&](uint32_t x, uint32_t y) { return hint[x] < hint[y]; });
+            std::vector<uint32_t> band(n);
+            for (size_t k = 0; k < n; ++k) {
+                const size_t x = k < rem * (per + 1) ? k / (per + 1) : rem + (k - rem * (per + 1)) / per;
+                band[by[k]] = uint32_t(x);
+            }
+            std::vector<uint32_t> perm(n);
+            for (size_t i = 0; i < n; ++i) perm[i] = uint32_t(i);
+            std::stable_sort(perm.begin(), perm.end(), [&](uint32_t x, uint32_t y) { return band[x] < band[y]; });
+            std::vector<group> o2;
+            o2.reserve(n);
+            for (const uint32_t i : perm) o2.push_back(std::move(out[i]));
+            out.swap(o2);
+            map = cb_xcd_bands;
+        }
+    }
     for (auto& g : out) {
         costa_tile_op_t h{};
         h.src = g.ops.size();
@@ -1082,7 +1127,8 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     }
     // destination-block groups out of the wavefront ops (after the skew items in `work`)
     int64_t cblock_lds = 0;
-    const int64_t n_cblock = cblock_groups(dtype, wave_ops, kind, ordered, work, cblock_lds);
+    int cb_map = cb_round_robin;
+    const int64_t n_cblock = cblock_groups(dtype, wave_ops, kind, ordered, work, cblock_lds, cb_map);
     // ops are independent (disjoint destinations), so any order is valid; neighbours in
     // memory run at the same time and share the partially used cache lines at their edges.
     // The wavefront ops are ordered first, then cut into their pieces straight into the ordered
@@ -1171,6 +1217,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     w.skew_wide = skew_wide && n_work[2] > 0;
     w.n_cblock = n_cblock;
     w.cblock_lds = cblock_lds;
+    w.cb_map = cb_map;
 
     w.tiny_first = int64_t(ordered.size());
     w.n_tiny = int64_t(at_piece[nw]);
@@ -1194,6 +1241,7 @@ launch_args make_launch(const work_split& w, const void* d_ordered, const void* 
     a.n_skew = w.n_skew;
     a.n_cblock = w.n_cblock;
     a.cblock_lds = w.cblock_lds;
+    a.cb_map = w.cb_map;
     a.tiny_first = w.tiny_first;
     a.n_tiny = w.n_tiny;
     a.src_base = src_base;

@@ -191,6 +191,7 @@ struct launch_args {
     int64_t n_skew = 0;     // then n_skew items of the skew shape (unaligned destinations)
     int64_t n_cblock = 0;   // then n_cblock destination-block groups: index of the group's header op
     int64_t cblock_lds = 0; // LDS image of the largest group (elements)
+    int cb_map = 0;         // cblock_map of the groups
     int64_t tiny_first;     // ops[tiny_first, tiny_first + n_tiny) run one per wavefront
     int64_t n_tiny;
     const char* src_base;
@@ -228,6 +229,16 @@ constexpr int64_t cblock_xcd_order(int64_t b, int64_t nb) {
                      (b / 8) % kCblockXcdChunk
                : b;
 }
+// work-list position of workgroup b of nb when XCD x (= b mod 8) walks the x-th of 8 contiguous
+// slices of the list, slice x holding nb / 8 items (one more for the first nb mod 8 slices).  A
+// permutation of [0, nb); tiny_kernel's remap and the destination-block groups' XCD column bands
+// (engine.cpp cblock_groups).  (constexpr: host and device.)
+constexpr int64_t xcd_slice_order(int64_t b, int64_t nb) {
+    return (b % 8) < nb % 8 ? (b % 8) * (nb / 8 + 1) + b / 8
+                            : (nb % 8) * (nb / 8 + 1) + ((b % 8) - nb % 8) * (nb / 8) + b / 8;
+}
+// how a launch of destination-block groups maps workgroups onto the list (work_split::cb_map)
+enum cblock_map { cb_round_robin = 0, cb_xcd_chunks = 1, cb_xcd_bands = 2 };
 // sub-tile shapes (elements along the source's fast dim, along its slow dim) of a copy-only list
 // or of a list with transposing ops: the large shape, the medium one (bf_m = bs_m = 0: none) and
 // the large shape's square variant for lists whose large ops all fit it (bf_q = bs_q = 0: none),
@@ -249,6 +260,7 @@ struct work_split {
     int64_t n_skew = 0;     // skew-shape work items, after the medium ones
     int64_t n_cblock = 0;   // destination-block groups, after the skew items (cblock_groups)
     int64_t cblock_lds = 0; // elements of the largest group's LDS image
+    int cb_map = 0;         // cblock_map: how the groups' launch maps workgroups onto them
     bool tr_shape = false;  // sub-tiles cut with tile_shapes(dtype, true, ...)
     bool sq = false;        // ... the large ops with its square variant (bf_q x bs_q)
     bool full = false;      // every large op of a transposing list is aligned and a whole number

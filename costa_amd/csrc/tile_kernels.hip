@@ -1063,7 +1063,7 @@ template <typename T, bool TR, bool AX>
 __global__ __launch_bounds__(CB_NT) void cblock_kernel(const costa_tile_op_t* __restrict__ ops,
                                                        const uint64_t* __restrict__ work,
                                                        const char* src_base, char* dst_base,
-                                                       const T* __restrict__ scalars) {
+                                                       const T* __restrict__ scalars, int map) {
     constexpr int V = 16 / int(sizeof(T)), NW = CB_NT / 64;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     T* img = reinterpret_cast<T*>(smem);
@@ -1073,8 +1073,11 @@ __global__ __launch_bounds__(CB_NT) void cblock_kernel(const costa_tile_op_t* __
     // lines, now in one L2.  cfg 5 'T' 0.634 -> 0.600 ms (chunks of 2 / 16: 0.603 / 0.605; one
     // contiguous slice per XCD 0.625, its L2 -> memory reads -36 %); the copy ('N') is level or
     // slower every way (8 slices: +5 %) and keeps the plain order (profiles/r5ab/, r5ac/)
+    // (map == cb_xcd_bands: XCD x walks the x-th slice of the list, one band of target columns;
+    // engine.cpp cblock_groups)
     uint64_t g = blockIdx.x;
-    if constexpr (TR) g = uint64_t(cblock_xcd_order(int64_t(blockIdx.x), int64_t(gridDim.x)));
+    if (map == cb_xcd_chunks) g = uint64_t(cblock_xcd_order(int64_t(blockIdx.x), int64_t(gridDim.x)));
+    else if (map == cb_xcd_bands) g = uint64_t(xcd_slice_order(int64_t(blockIdx.x), int64_t(gridDim.x)));
     const uint64_t h = work[g];
     const costa_tile_op_t hd = ops[h];
     const int n_ops = int(hd.src), R = hd.nf, K = hd.ns, P = R | 1;
@@ -1186,7 +1189,7 @@ void launch_cblock_v(const launch_args& a, const uint64_t* work, int64_t n, hipS
     for (int64_t off = 0; off < n; off += max_grid) {
         const int64_t m = std::min(max_grid, n - off);
         hipLaunchKernelGGL((cblock_kernel<T, TR, AX>), dim3(unsigned(m)), dim3(CB_NT), lds, stream, a.ops,
-                           work + off, a.src_base, a.dst_base, static_cast<const T*>(a.scalars));
+                           work + off, a.src_base, a.dst_base, static_cast<const T*>(a.scalars), a.cb_map);
     }
 }
 template <typename T>
@@ -1220,9 +1223,7 @@ __global__ __launch_bounds__(64 * W, tiny_min_waves<T>::value) void tiny_kernel(
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = int(threadIdx.x) % 64;
     const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / 64);
-    const int64_t nb = gridDim.x, x = int64_t(blockIdx.x) % 8, per = nb / 8, rem = nb % 8;
-    const int64_t i = int64_t(blockIdx.x) / 8;
-    const int64_t b = x < rem ? x * (per + 1) + i : rem * (per + 1) + (x - rem) * per + i;
+    const int64_t b = xcd_slice_order(int64_t(blockIdx.x), int64_t(gridDim.x));
     const int64_t w = b * W + wave;
     if (w >= n_ops) return;
     T* t = reinterpret_cast<T*>(smem) + int64_t(wave) * lds_per_wave;

@@ -464,6 +464,205 @@ int run_bench_custom(const char* spec, char op, double seconds) {
     return ok ? 0 : 1;
 }
 
+// ---- multi-rank CPU baselines (bench.py cpu_baseline at N > 1)
+// Every rank of `mpiexec -n P` holds its share of the layouts and runs the reference's own
+// costa::transform (pack -> MPI Isend / Irecv -> unpack, local tiles on the side;
+// transform.cpp:46-128).  Each call is bracketed by MPI_Barrier, as the reference's miniapps time
+// pxgemr2d (utils/pxgemr2d_utils.hpp:284-292); calls repeat until rank 0 has spent ~s seconds in
+// them (its sum, broadcast, so every rank stops together).  Values are a function of the GLOBAL
+// position (gen at i + j * M), so every rank checks sampled local elements of C after the first
+// call against the definition; the mismatch counts are summed over the ranks.
+//   bench_mr pxtran <n> <nb> <pm> <pn> <s>  fp64 'T' alpha 1 beta 0: A (n pm) x (n pn) on the pm x pn
+//                                           'R' grid, C = A^T on the same grid (bench.py's N-rank
+//                                           headline, n per rank)
+//   bench_mr cfg3 <n> <nb> <pm> <pn> <s>    fp64 'N' copy (no scale): A (n pm) x (n pn) on pm x pn ->
+//                                           C on a P x 1 grid (BASELINE configs[2]'s remap)
+//   bench_mr cfg4 <e> <nb> <pm> <pn> <s>    complex<double> 'T' alpha (0.75, -0.5), beta (1.25, 0.25),
+//                                           e x e on pm x pn (BASELINE configs[3])
+//   bench_mr custom <spec> <N|T> <s>        custom layouts (BASELINE configs[4]); spec: A's row and
+//                                           column splits and owners (row-major), then C's; every
+//                                           owned block its own column-major buffer
+// Rank 0 prints one JSON line {GBps (algorithmic bytes of all ranks: read + write of every
+// element, + read of C when beta != 0, per call / rank 0's time), reps, seconds, ranks, threads
+// (OpenMP threads per rank), verified}.
+int bc_global(int l, int nb, int p, int pr) { return (l / nb) * p * nb + pr * nb + l % nb; }
+
+template <typename T>
+int bench_mr_bc(const std::string& kind, int n, int nb, int pm, int pn, double seconds, int rank, int P) {
+    const bool c4 = kind == "cfg4", c3 = kind == "cfg3";
+    const int M = c4 ? n : n * pm, N = c4 ? n : n * pn;  // A is M x N
+    const int pr = rank / pn, pc = rank % pn;             // 'R' rank order
+    const int lr_a = M / pm, lc_a = N / pn;
+    // C: cfg3 M x N on P x 1; else N x M on pm x pn
+    const int cpm = c3 ? P : pm, cpn = c3 ? 1 : pn, cpr = c3 ? rank : pr, cpc = c3 ? 0 : pc;
+    const int Mc = c3 ? M : N, Nc = c3 ? N : M;
+    const int lr_c = Mc / cpm, lc_c = Nc / cpn;
+    if (M % (pm * nb) || N % (pn * nb) || Mc % (cpm * nb) || Nc % (cpn * nb)) {
+        if (rank == 0) std::fprintf(stderr, "bench_mr: sizes not multiples of the grid blocks\n");
+        return 2;
+    }
+    const uint64_t sa = 0xC057A0, sc = 0xC057C0;
+    std::vector<T> a(size_t(lr_a) * lc_a), c(size_t(lr_c) * lc_c);
+#pragma omp parallel for schedule(static)
+    for (int lj = 0; lj < lc_a; ++lj)
+        for (int li = 0; li < lr_a; ++li)
+            a[size_t(lj) * lr_a + li] =
+                gen<T>(sa, 0, uint64_t(bc_global(li, nb, pm, pr)) + uint64_t(bc_global(lj, nb, pn, pc)) * uint64_t(M));
+#pragma omp parallel for schedule(static)
+    for (int lj = 0; lj < lc_c; ++lj)
+        for (int li = 0; li < lr_c; ++li)
+            c[size_t(lj) * lr_c + li] = gen<T>(
+                sc, 0, uint64_t(bc_global(li, nb, cpm, cpr)) + uint64_t(bc_global(lj, nb, cpn, cpc)) * uint64_t(Mc));
+    auto A = costa::block_cyclic_layout<T>(M, N, nb, nb, 1, 1, M, N, pm, pn, 'R', 0, 0, a.data(), lr_a, 'C', rank);
+    auto C = costa::block_cyclic_layout<T>(Mc, Nc, nb, nb, 1, 1, Mc, Nc, cpm, cpn, 'R', 0, 0, c.data(), lr_c, 'C',
+                                           rank);
+    T alpha = T(1), beta = T(0);
+    if constexpr (std::is_same<T, std::complex<double>>::value) {
+        alpha = T(0.75, -0.5);
+        beta = T(1.25, 0.25);
+    }
+    const char op = c3 ? 'N' : 'T';
+    auto call = [&] {
+        if (c3)
+            costa::transform<T>(A, C, MPI_COMM_WORLD);
+        else
+            costa::transform<T>(A, C, op, alpha, beta, MPI_COMM_WORLD);
+    };
+    call();  // warm-up (first touch, the MPI buffers); checked
+    long bad = 0;
+    for (size_t k = 0; k < c.size(); k += 97) {
+        const int li = int(k % size_t(lr_c)), lj = int(k / size_t(lr_c));
+        const int i = bc_global(li, nb, cpm, cpr), j = bc_global(lj, nb, cpn, cpc);
+        const T x = op == 'N' ? gen<T>(sa, 0, uint64_t(i) + uint64_t(j) * M) : gen<T>(sa, 0, uint64_t(j) + uint64_t(i) * M);
+        const T want = beta == T(0) ? alpha * x : beta * gen<T>(sc, 0, uint64_t(i) + uint64_t(j) * Mc) + alpha * x;
+        bad += !(c[k] == want);
+    }
+    long bad_all = 0;
+    MPI_Allreduce(&bad, &bad_all, 1, MPI_LONG, MPI_SUM, MPI_COMM_WORLD);
+    int reps = 0;
+    double tsum = 0;
+    for (;;) {
+        MPI_Barrier(MPI_COMM_WORLD);
+        const auto t0 = std::chrono::steady_clock::now();
+        call();
+        MPI_Barrier(MPI_COMM_WORLD);
+        tsum += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        ++reps;
+        double el = tsum;
+        MPI_Bcast(&el, 1, MPI_DOUBLE, 0, MPI_COMM_WORLD);
+        if (el >= seconds || reps >= 100000) {
+            tsum = el;
+            break;
+        }
+    }
+    const double bytes = (beta == T(0) ? 2.0 : 3.0) * sizeof(T) * double(M) * N;
+    if (rank == 0)
+        std::printf("{\"GBps\": %.3f, \"reps\": %d, \"seconds\": %.3f, \"ranks\": %d, \"threads\": %d, "
+                    "\"verified\": %s}\n",
+                    bytes * reps / tsum / 1e9, reps, tsum, P, omp_get_max_threads(), bad_all == 0 ? "true" : "false");
+    return bad_all == 0 ? 0 : 1;
+}
+
+int bench_mr_custom(const char* spec, char op, double seconds, int rank, int P) {
+    std::ifstream in(spec);
+    auto vec = [&]() {
+        int k;
+        in >> k;
+        std::vector<int> v(static_cast<size_t>(k));
+        for (auto& x : v) in >> x;
+        return v;
+    };
+    struct grid {
+        std::vector<int> rs, cs, owners;
+        std::vector<float> buf;
+        std::vector<costa::block_t> blocks;
+    };
+    auto read = [&] {
+        grid g;
+        g.rs = vec();
+        g.cs = vec();
+        g.owners.resize((g.rs.size() - 1) * (g.cs.size() - 1));
+        for (auto& x : g.owners) in >> x;
+        return g;
+    };
+    grid ga = read(), gc = read();
+    const uint64_t sa = 0xC057A0, sc = 0xC057C0;
+    const int M = ga.rs.back(), N = ga.cs.back();
+    // this rank's blocks, each its own column-major buffer (ld = rows) at 256-byte aligned offsets
+    auto make = [&](grid& g, uint64_t seed, int rows) {
+        std::vector<size_t> off;
+        std::vector<int> bi, bj;
+        size_t o = 0;
+        for (size_t i = 0; i + 1 < g.rs.size(); ++i)
+            for (size_t j = 0; j + 1 < g.cs.size(); ++j)
+                if (g.owners[i * (g.cs.size() - 1) + j] == rank) {
+                    off.push_back(o);
+                    bi.push_back(int(i));
+                    bj.push_back(int(j));
+                    o += (size_t(g.rs[i + 1] - g.rs[i]) * size_t(g.cs[j + 1] - g.cs[j]) + 63) / 64 * 64;
+                }
+        g.buf.assign(std::max<size_t>(o, 64), 0.f);
+#pragma omp parallel for schedule(dynamic, 16)
+        for (size_t b = 0; b < off.size(); ++b) {
+            const int r0 = g.rs[size_t(bi[b])], r1 = g.rs[size_t(bi[b]) + 1];
+            const int c0 = g.cs[size_t(bj[b])], c1 = g.cs[size_t(bj[b]) + 1];
+            for (int j = c0; j < c1; ++j)
+                for (int i = r0; i < r1; ++i)
+                    g.buf[off[b] + size_t(j - c0) * size_t(r1 - r0) + size_t(i - r0)] =
+                        gen<float>(seed, 0, uint64_t(i) + uint64_t(j) * uint64_t(rows));
+        }
+        for (size_t b = 0; b < off.size(); ++b)
+            g.blocks.push_back({g.buf.data() + off[b], g.rs[size_t(bi[b]) + 1] - g.rs[size_t(bi[b])], bi[b], bj[b]});
+    };
+    make(ga, sa, M);
+    const int Mc = gc.rs.back();
+    make(gc, sc, Mc);
+    auto A = costa::custom_layout<float>(int(ga.rs.size()) - 1, int(ga.cs.size()) - 1, ga.rs.data(), ga.cs.data(),
+                                         ga.owners.data(), int(ga.blocks.size()), ga.blocks.data(), 'C');
+    auto C = costa::custom_layout<float>(int(gc.rs.size()) - 1, int(gc.cs.size()) - 1, gc.rs.data(), gc.cs.data(),
+                                         gc.owners.data(), int(gc.blocks.size()), gc.blocks.data(), 'C');
+    const float alpha = op == 'N' ? 1.f : -0.5f, beta = op == 'N' ? 0.f : 2.f;
+    auto call = [&] { costa::transform<float>(A, C, op, alpha, beta, MPI_COMM_WORLD); };
+    call();
+    long bad = 0;  // every 7th column of every local C block against the definition
+    for (const auto& b : gc.blocks) {
+        const int r0 = gc.rs[size_t(b.row)], r1 = gc.rs[size_t(b.row) + 1];
+        const int c0 = gc.cs[size_t(b.col)], c1 = gc.cs[size_t(b.col) + 1];
+        const float* p = static_cast<const float*>(b.data);
+        for (int j = c0; j < c1; j += 7)
+            for (int i = r0; i < r1; ++i) {
+                const float x = op == 'N' ? gen<float>(sa, 0, uint64_t(i) + uint64_t(j) * uint64_t(M))
+                                          : gen<float>(sa, 0, uint64_t(j) + uint64_t(i) * uint64_t(M));
+                const float want = op == 'N' ? x : beta * gen<float>(sc, 0, uint64_t(i) + uint64_t(j) * uint64_t(Mc)) + alpha * x;
+                bad += p[size_t(j - c0) * size_t(r1 - r0) + size_t(i - r0)] != want;
+            }
+    }
+    long bad_all = 0;
+    MPI_Allreduce(&bad, &bad_all, 1, MPI_LONG, MPI_SUM, MPI_COMM_WORLD);
+    int reps = 0;
+    double tsum = 0;
+    for (;;) {
+        MPI_Barrier(MPI_COMM_WORLD);
+        const auto t0 = std::chrono::steady_clock::now();
+        call();
+        MPI_Barrier(MPI_COMM_WORLD);
+        tsum += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        ++reps;
+        double el = tsum;
+        MPI_Bcast(&el, 1, MPI_DOUBLE, 0, MPI_COMM_WORLD);
+        if (el >= seconds || reps >= 100000) {
+            tsum = el;
+            break;
+        }
+    }
+    const double bytes = (op == 'N' ? 2.0 : 3.0) * sizeof(float) * double(M) * N;
+    if (rank == 0)
+        std::printf("{\"GBps\": %.3f, \"reps\": %d, \"seconds\": %.3f, \"ranks\": %d, \"threads\": %d, "
+                    "\"verified\": %s}\n",
+                    bytes * reps / tsum / 1e9, reps, tsum, P, omp_get_max_threads(), bad_all == 0 ? "true" : "false");
+    return bad_all == 0 ? 0 : 1;
+}
+
 // spec: P trans / per grid: n_rs rs... n_cs cs... owners (row-major)
 costa::assigned_grid2D read_grid(std::istream& in, int P) {
     auto vec = [&]() {
@@ -545,6 +744,18 @@ int main(int argc, char** argv) {
         rc = rank == 0 ? run_bench_c128(std::atoi(argv[2]), std::atoi(argv[3]), std::atof(argv[4])) : 0;
     } else if (argc >= 5 && std::string(argv[1]) == "bench_custom") {
         rc = rank == 0 ? run_bench_custom(argv[2], argv[3][0], std::atof(argv[4])) : 0;
+    } else if (argc >= 6 && std::string(argv[1]) == "bench_mr" && std::string(argv[2]) == "custom") {
+        rc = bench_mr_custom(argv[3], argv[4][0], std::atof(argv[5]), rank, P);
+    } else if (argc >= 8 && std::string(argv[1]) == "bench_mr") {
+        const std::string kind = argv[2];
+        const int n = std::atoi(argv[3]), nb = std::atoi(argv[4]), pm = std::atoi(argv[5]), pn = std::atoi(argv[6]);
+        const double s = std::atof(argv[7]);
+        if (pm * pn != P)
+            rc = 2;
+        else if (kind == "pxtran" || kind == "cfg3")
+            rc = bench_mr_bc<double>(kind, n, nb, pm, pn, s, rank, P);
+        else if (kind == "cfg4")
+            rc = bench_mr_bc<std::complex<double>>(kind, n, nb, pm, pn, s, rank, P);
     } else if (argc >= 3 && std::string(argv[1]) == "relabel") {
         rc = rank == 0 ? run_relabel(argv[2]) : 0;
     } else {

@@ -329,7 +329,12 @@ static bool check_cblock(const std::string& name, costa_dtype_t dt, const std::v
         // (a range off the 16-byte grid needs up to V - 1 more elements of whole vectors)
         CHECK(R > 0 && K > 0 && n >= 1 && hd.ldd == R && R * K + 16 / E - 1 <= cblock_max_elems(E),
               "group %lld shape", (long long)x);
-        CHECK(hd.dst >= last, "group %lld out of destination order", (long long)x);
+        // destination order (with XCD column bands: inside each of the 8 slices of the kernel's sizes)
+        const int64_t gi = x - (w.n_large + w.n_medium + w.n_skew), ng = w.n_cblock;
+        const bool slice_start = w.cb_map == cb_xcd_bands &&
+                                 (gi < (ng % 8) * (ng / 8 + 1) ? gi % (ng / 8 + 1) == 0
+                                                               : ng / 8 > 0 && (gi - (ng % 8) * (ng / 8 + 1)) % (ng / 8) == 0);
+        CHECK(slice_start || hd.dst >= last, "group %lld out of destination order", (long long)x);
         last = hd.dst;
         lds = std::max(lds, (R | 1) * K);
         std::vector<char> cov(size_t(R * K), 0);
@@ -374,6 +379,15 @@ static bool check_xcd() {
             CHECK(g >= 0 && g < nb && !seen[size_t(g)], "nb %lld, b %lld -> %lld", (long long)nb, (long long)b,
                   (long long)g);
             seen[size_t(g)] = 1;
+        }
+        // and so is the slice order (xcd_slice_order), XCD b mod 8 inside slice b mod 8
+        std::vector<char> seen2(size_t(nb), 0);
+        for (int64_t b = 0; b < nb; ++b) {
+            const int64_t g = xcd_slice_order(b, nb);
+            const int64_t x = b % 8, lo = x < nb % 8 ? x * (nb / 8 + 1) : (nb % 8) * (nb / 8 + 1) + (x - nb % 8) * (nb / 8);
+            CHECK(g >= 0 && g < nb && !seen2[size_t(g)] && g >= lo && g < lo + nb / 8 + (x < nb % 8),
+                  "slice order: nb %lld, b %lld -> %lld", (long long)nb, (long long)b, (long long)g);
+            seen2[size_t(g)] = 1;
         }
     }
     return true;
