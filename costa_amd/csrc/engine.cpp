@@ -15,6 +15,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <numeric>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -671,6 +672,34 @@ int64_t cblock_groups(costa_dtype_t dtype, std::vector<const costa_tile_op_t*>& 
             K = std::max(K, e / R + runs);
         }
         if (!ok || area != R * K || K > INT32_MAX) continue;
+        // ... and tile it exactly: with the areas adding up to R x K, the ops tile the range iff
+        // every corner point occurs an even number of times, the range's own four corners
+        // apart, which occur once ("perfect rectangle").  Overlapping ops whose areas happen
+        // to add up would leave elements no op writes, and the group kernel would store its
+        // uninitialised LDS there (costa_hip_execute_tiles takes caller ops).
+        {
+            std::vector<uint64_t> corner;
+            corner.reserve(4 * (b - a0));
+            const uint64_t W = uint64_t(K) + 1;
+            for (size_t k = a0; k < b; ++k) {
+                const costa_tile_op_t& op = *wave_ops[cs[k].i];
+                const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
+                const uint64_t run = uint64_t(tr ? op.ns : op.nf), runs = uint64_t(tr ? op.nf : op.ns);
+                const uint64_t e = (op.dst - base) / uint64_t(E), r0 = e % uint64_t(R), c0 = e / uint64_t(R);
+                for (const uint64_t r : {r0, r0 + run})
+                    for (const uint64_t c : {c0, c0 + runs}) corner.push_back(r * W + c);
+            }
+            std::sort(corner.begin(), corner.end());
+            std::vector<uint64_t> odd;
+            for (size_t k = 0; k < corner.size();) {
+                size_t m = k;
+                while (m < corner.size() && corner[m] == corner[k]) ++m;
+                if ((m - k) & 1) odd.push_back(corner[k]);
+                k = m;
+            }
+            const uint64_t ur = uint64_t(R), uk = uint64_t(K);
+            if (odd != std::vector<uint64_t>{0, uk, ur * W, ur * W + uk}) continue;
+        }
         // column bands of at most `budget` elements
         const int64_t KB = std::max<int64_t>(1, budget / R);
         for (int64_t cb0 = 0; cb0 < K; cb0 += KB) {
@@ -786,6 +815,8 @@ struct wave_knobs {  // defaults, overridable for tuning runs
                          // 128 x 128 sub-tiles 0.366 against 0.396 with 256^2, 0.366 against
                          // 0.454 with 512^2), else 1 (c128 with 128^2 blocks: 2.87 against 2.27
                          // ms; copy lists untested under 2; profiles/r2/order/)
+    int copy_granule = 0;  // COSTA_COPY_GRANULE=1 (tuning): copy ops into destinations off the
+                           // 64-byte grid cut at each column's granules (granule_split)
     int force_sq = 0;   // COSTA_FORCE_SQ=1 (tuning): transposing lists of fp64 / c64 / c128 take the
                         // square sub-tile whatever their ops' size
     int merge = 2;      // COSTA_MERGE=0: ops that continue each other are not merged, 1: only
@@ -822,11 +853,76 @@ const wave_knobs& knobs() {
         if (const char* s = tuning_env("COSTA_XCD_BANDS")) x.xcd_bands = std::atoi(s);
         if (const char* s = tuning_env("COSTA_MERGE")) x.merge = std::atoi(s);
         if (const char* s = tuning_env("COSTA_FORCE_SQ")) x.force_sq = std::atoi(s);
+        if (const char* s = tuning_env("COSTA_COPY_GRANULE")) x.copy_granule = std::atoi(s);
         return x;
     }();
     return k;
 }
 }  // namespace
+
+// Copies into destinations off the 64-byte grid (a ScaLAPACK lld that is not a multiple of 64
+// bytes, or a sub-matrix offset): the large copy shape writes each destination column in 1 KiB
+// segments from the op's first row, so every segment boundary inside a column is a 64-byte
+// granule shared by two workgroups, which HBM services as a read-modify-write.  Cut
+// instead at each column's own granules: the op's columns are split by their residue modulo the
+// period p after which a column starts at the same granule offset again (p * ldd * E = 0 mod 64),
+// so each part has one offset eps for every column; its first G - eps rows (G = 64 / E elements:
+// the head of each column's first granule) become an op of their own (the wavefront path), and
+// the rest starts every column on a granule boundary, its segments whole granules.  Sub-rectangles
+// of a copy op are copy ops: the same elements, the same transform; only the op boundaries move.
+// Ops below `min_elems` (the wavefront path anyway) and transposing ops (the skew shape, §3b) stay
+// as they are.  -> true when `out` holds a split list
+bool granule_split(const std::vector<costa_tile_op_t>& ops, int64_t E, int64_t min_elems,
+                   std::vector<costa_tile_op_t>& out) {
+    const int64_t G = 64 / E;
+    auto split_it = [&](const costa_tile_op_t& op) {
+        if (G <= 1 || (op.flags & COSTA_TILE_TRANSPOSE) || op.dst % uint64_t(E) != 0) return false;
+        if (int64_t(op.nf) * op.ns < min_elems || op.nf < 2 * G) return false;
+        if (int64_t(std::max(op.lds, op.ldd)) * 64 > INT32_MAX) return false;  // p * ld must fit
+        return op.dst % 64 != 0 || (uint64_t(op.ldd) * uint64_t(E)) % 64 != 0;
+    };
+    bool any = false;
+    for (const auto& op : ops) any = any || split_it(op);
+    if (!any) return false;
+    out.clear();
+    out.reserve(ops.size() + 64);
+    const uint32_t vec_bits = COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST;
+    for (const auto& op : ops) {
+        if (!split_it(op)) {
+            out.push_back(op);
+            continue;
+        }
+        const uint64_t row_bytes = uint64_t(op.ldd) * uint64_t(E);
+        const int64_t p = 64 / int64_t(std::gcd(row_bytes % 64 == 0 ? uint64_t(64) : row_bytes % 64, uint64_t(64)));
+        // 4-byte sources are read as 16-byte vectors at dword alignment (build_work: mis)
+        const uint32_t keep_vs = E == 4 ? (op.flags & COSTA_TILE_VEC_SRC) : 0u;
+        for (int64_t r = 0; r < std::min<int64_t>(p, op.ns); ++r) {
+            costa_tile_op_t part = op;
+            part.src = op.src + uint64_t(r * int64_t(op.lds) * E);
+            part.dst = op.dst + uint64_t(r * int64_t(op.ldd) * E);
+            part.ns = int32_t((op.ns - r + p - 1) / p);
+            part.lds = int32_t(int64_t(op.lds) * p);
+            part.ldd = int32_t(int64_t(op.ldd) * p);
+            const int64_t eps = int64_t(part.dst % 64) / E;
+            const int64_t h = eps > 0 ? std::min<int64_t>(op.nf, G - eps) : 0;
+            if (h > 0) {  // the head of each column's first granule
+                costa_tile_op_t head = part;
+                head.nf = int32_t(h);
+                head.flags = (op.flags & ~vec_bits) | vec_flags(head.src, head.lds, head.dst, head.ldd, E) | keep_vs;
+                out.push_back(head);
+            }
+            if (h < op.nf) {
+                costa_tile_op_t body = part;
+                body.src += uint64_t(h * E);
+                body.dst += uint64_t(h * E);
+                body.nf = int32_t(op.nf - h);
+                body.flags = (op.flags & ~vec_bits) | vec_flags(body.src, body.lds, body.dst, body.ldd, E) | keep_vs;
+                out.push_back(body);
+            }
+        }
+    }
+    return true;
+}
 
 work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops_in,
                       std::vector<costa_tile_op_t>& ordered, std::vector<uint64_t>& work,
@@ -881,7 +977,15 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
             if ((mis & 2) && op.src % 4 == 0 && (uint64_t(op.lds) * E) % 4 == 0) op.flags |= COSTA_TILE_VEC_SRC;
         }
     }
-    const std::vector<costa_tile_op_t>& ops = mis ? ops_mis : *ops_src;
+    const std::vector<costa_tile_op_t>* ops_pre = mis ? &ops_mis : ops_src;
+    std::vector<costa_tile_op_t> ops_gran;
+    if (kn0.copy_granule) {
+        shape_dims shg;
+        tile_shapes(dtype, any_transpose(ops_in), &shg);
+        if (granule_split(*ops_pre, int64_t(dtype_size(dtype)), int64_t(shg.cf) * shg.cs / 2, ops_gran))
+            ops_pre = &ops_gran;
+    }
+    const std::vector<costa_tile_op_t>& ops = *ops_pre;
     const bool tr_shape = any_transpose(ops);
     shape_dims sh;
     tile_shapes(dtype, tr_shape, &sh);

@@ -184,15 +184,19 @@ struct ring {
     int device = 0;
     size_t slot = 0;          // bytes of one package; at most kSlot, sized to the largest group
     hipStream_t up = nullptr, down = nullptr;
+    hipStream_t pk = nullptr;  // direct PACK groups' pack kernels (not behind earlier exchange
+                               // rounds on the exchange stream: ADVICE r5)
     char* pin_in = nullptr;   // kRing x 2*slot: [source package | old target package]
     char* pin_out = nullptr;  // kRing x slot: target package
     char* dev = nullptr;      // kRing x 2*slot: [source package | target package]
     hipEvent_t up_done[kRing]{}, kern_done[kRing]{}, down_done[kRing]{};
     hipEvent_t packed[kMaxRounds]{}, moved[kMaxRounds]{};  // per exchange round: its part of
                                                              // the send buffer uploaded / moved
+    hipEvent_t packed_k[kMaxRounds]{};  // ... and packed by the direct groups' kernels (on pk)
     ring(int d, size_t slot_bytes) : device(d), slot(slot_bytes) {
         HP_CHECK(hipStreamCreateWithFlags(&up, hipStreamNonBlocking));
         HP_CHECK(hipStreamCreateWithFlags(&down, hipStreamNonBlocking));
+        HP_CHECK(hipStreamCreateWithFlags(&pk, hipStreamNonBlocking));
         HP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&pin_in), kRing * 2 * slot, hipHostMallocDefault));
         HP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&pin_out), kRing * slot, hipHostMallocDefault));
         HP_CHECK(hipMalloc(reinterpret_cast<void**>(&dev), kRing * 2 * slot));
@@ -201,6 +205,7 @@ struct ring {
                 HP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
         for (int r = 0; r < kMaxRounds; ++r) {
             HP_CHECK(hipEventCreateWithFlags(&packed[r], hipEventDisableTiming));
+            HP_CHECK(hipEventCreateWithFlags(&packed_k[r], hipEventDisableTiming));
             HP_CHECK(hipEventCreateWithFlags(&moved[r], hipEventDisableTiming));
         }
     }
@@ -208,10 +213,12 @@ struct ring {
         (void)hipSetDevice(device);
         (void)hipStreamSynchronize(up);
         (void)hipStreamSynchronize(down);
+        (void)hipStreamSynchronize(pk);
         for (int k = 0; k < kRing; ++k)
             for (hipEvent_t e : {up_done[k], kern_done[k], down_done[k]}) (void)hipEventDestroy(e);
         for (int r = 0; r < kMaxRounds; ++r) {
             (void)hipEventDestroy(packed[r]);
+            (void)hipEventDestroy(packed_k[r]);
             (void)hipEventDestroy(moved[r]);
         }
         (void)hipFree(dev);
@@ -219,6 +226,7 @@ struct ring {
         (void)hipHostFree(pin_out);
         (void)hipStreamDestroy(up);
         (void)hipStreamDestroy(down);
+        (void)hipStreamDestroy(pk);
     }
 };
 
@@ -761,6 +769,8 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
         for (; issued < upto && exchange; ++issued) {
             HP_CHECK(hipEventRecord(R.packed[issued], R.up));
             HP_CHECK(hipStreamWaitEvent(xs, R.packed[issued], 0));
+            HP_CHECK(hipEventRecord(R.packed_k[issued], R.pk));  // direct groups' pack kernels
+            HP_CHECK(hipStreamWaitEvent(xs, R.packed_k[issued], 0));
             if (prof && !x0) x0 = ev(xs);
             exchange(xs, issued);
             if (prof) x1 = ev(xs);
@@ -842,21 +852,23 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
         n_direct_run += gd;
         if (g->kind == hpl::PACK && gd) {
             // direct: the source rectangle up into the device slot, then the pack kernel into the
-            // send buffer on the exchange stream, ahead of its round's RCCL group there
+            // send buffer on the ring's pack stream; its round's RCCL group waits for that stream
+            // (issue_rounds).  On the exchange stream itself the kernel -- and with it the slot's
+            // next user, every later upload -- queued behind the earlier rounds' exchange
             HP_CHECK(hipStreamWaitEvent(R.up, R.down_done[k], 0));  // the slot's previous user
             if (prof && !up0) up0 = ev(R.up);
             move_rect(g->src_rect, dev, true);
             HP_CHECK(hipEventRecord(R.up_done[k], R.up));
             if (prof) up1 = ev(R.up);
-            HP_CHECK(hipStreamWaitEvent(xs, R.up_done[k], 0));
-            hipEvent_t k0 = prof ? ev(xs) : nullptr;
+            HP_CHECK(hipStreamWaitEvent(R.pk, R.up_done[k], 0));
+            hipEvent_t k0 = prof ? ev(R.pk) : nullptr;
             launch_tiles(hp.dtype,
                          make_launch(g->split_d, static_cast<const costa_tile_op_t*>(hp.d_ops_d) + g->ord_first_d,
                                      static_cast<const uint64_t*>(hp.d_work_d) + g->work_first_d, dev, send_buf,
                                      d_scalars, g->any_tr_d, false),
-                         xs);
-            if (prof) pack_t.push_back({k0, ev(xs), false});
-            HP_CHECK(hipEventRecord(R.down_done[k], xs));  // the device slot is free again
+                         R.pk);
+            if (prof) pack_t.push_back({k0, ev(R.pk), false});
+            HP_CHECK(hipEventRecord(R.down_done[k], R.pk));  // the device slot is free again
             issue_rounds(hp.rounds_after[t]);
             t_issue += now() - t3;
             return;
@@ -955,6 +967,7 @@ void run_host_pipeline(host_pipeline& hp, int device, void* compute_stream, void
                      direct ? (n_direct_run == G ? " (direct DMA)" : " (direct DMA: some groups)") : "",
                      (now() - t_begin) * 1e3, t_copy * 1e3, t_wait_up * 1e3, t_wait_down * 1e3, t_issue * 1e3);
     HP_CHECK(hipStreamSynchronize(R.up));
+    HP_CHECK(hipStreamSynchronize(R.pk));
     HP_CHECK(hipStreamSynchronize(xs));
     HP_CHECK(hipStreamSynchronize(comp));
     HP_CHECK(hipStreamSynchronize(R.down));

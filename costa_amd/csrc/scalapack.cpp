@@ -115,8 +115,10 @@ void free_at_finalize() {
 // The communicator of one call: the cached one, or -- when some grid process lies outside this
 // process's MPI_COMM_WORLD (MPI_Comm_spawn / MPI_Comm_connect: its world rank translates to
 // MPI_UNDEFINED, and two different grids could then share a key) -- one made for the call and
-// freed after it, with the RCCL communicator cached on it.  Every member of such a grid sees an
-// undefined rank (the members share no world), so all of them take the uncached way together.
+// freed after it.  Its RCCL communicator lives on it as an attribute, so it too is made and
+// destroyed per call: such a call pays MPI_Comm_create_group, a unique-id broadcast and
+// ncclCommInitRank every time.  Every member of such a grid sees
+// an undefined rank (the members share no world), so all of them take the uncached way together.
 struct call_comm {
     MPI_Comm comm = MPI_COMM_NULL;
     bool owned = false;

@@ -2,7 +2,7 @@
 path custom layouts whose blocks are their own buffers take (BASELINE cfg 5): one workgroup per
 contiguous destination range, 16-byte stores.  Ranges off the 16-byte grid (a `gap` of 1-3
 elements after each block), C blocks larger than one group (cut into column bands), ragged A
-blocks of 8-60, 'N' and 'T', alpha / beta, fp32 / fp64 -- against the oracle bit for bit, the
+blocks of 8-60, 'N' and 'T', alpha / beta, fp32 / fp64 / int32 -- against the oracle bit for bit, the
 arena's gaps untouched.  The same geometry's groups are checked on the CPU
 (tools/work_check.cpp cblock, test_work_lists.py)."""
 import numpy as np
@@ -23,13 +23,15 @@ def _splits(rng, n, lo, hi):
     return s
 
 
-@pytest.mark.parametrize("dt", [oracle.FLOAT, oracle.DOUBLE])
+@pytest.mark.parametrize("dt", [oracle.FLOAT, oracle.DOUBLE, oracle.INT32])
 @pytest.mark.parametrize("op,alpha,beta", [("T", 1.0, 0.0), ("T", -0.5, 2.0), ("N", 1.0, 0.0),
                                            ("N", 0.75, -1.25)])
 @pytest.mark.parametrize("gap", [0, 1, 3])
 def test_cblock_vs_oracle(costa, dt, op, alpha, beta, gap):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    if dt == oracle.INT32:  # cblock_kernel<int>: integer scalars, exact products
+        alpha, beta = {1.0: 1, -0.5: -3, 0.75: 3}[alpha], {0.0: 0, 2.0: 2, -1.25: -1}[beta]
     rng = np.random.default_rng(100 + gap + 7 * dt)
     m, n = 1500, 1300
     am, an = (n, m) if op == "T" else (m, n)  # A is op(C)'s shape

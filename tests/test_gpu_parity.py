@@ -359,6 +359,64 @@ def test_unaligned_skew_vs_oracle(gpu, dtype, pad, ab, geo):
     assert got.tobytes() == expected.tobytes()
 
 
+@pytest.mark.parametrize("dtype", [0, 1, 4])
+@pytest.mark.parametrize("pads", [(0, 1), (0, 2), (0, 3), (1, 2), (3, 1)], ids=lambda p: f"a{p[0]}c{p[1]}")
+@pytest.mark.parametrize("ab", [(1, 0), (-1.5, 0.25)], ids=["copy", "axpby"])
+@pytest.mark.parametrize("geo", [(1500, 1100, 256, 256, 1, 1), (1437, 1203, 300, 170, 5, 9)],
+                         ids=["b256", "ragged-sub"])
+def test_unaligned_copy_vs_oracle(gpu, dtype, pads, ab, geo):
+    """'N' (p?gemr2d) into destination columns off the 64-byte grid (lld = LOCr + pad, sub-matrices
+    starting inside a granule): the copies cut at each column's granules (engine.cpp
+    granule_split) where that is on, the large copy shape otherwise; beta != 0 cases read C;
+    bit-exact vs the oracle over the whole buffer, padding rows untouched"""
+    m, n, mb, nb, ia, ja = geo
+    pa, pc = pads
+    rng = np.random.default_rng(41 + pa + 7 * pc)
+    a_case = BC(m + ia, n + ja, mb, nb, ia=ia, ja=ja, subm=m, subn=n, lld_pad=pa)
+    c_case = BC(m + ia, n + ja, mb, nb, ia=ia, ja=ja, subm=m, subn=n, lld_pad=pc)
+    npd = oracle.NP[dtype]
+    na, nc = a_case.buf_elems(0, 1), c_case.buf_elems(0, 1)
+    if dtype == 4:
+        a = rng.integers(-2**20, 2**20, na).astype(npd)
+        c = rng.integers(-2**20, 2**20, nc).astype(npd)
+        alpha, beta = int(ab[0] * 2), int(ab[1] * 4)
+    else:
+        a = rng.standard_normal(na).astype(npd)
+        c = rng.standard_normal(nc).astype(npd)
+        alpha, beta = ab
+    expected = c.copy()
+    oracle.transform(dtype, "N", alpha, beta, a_case.geom(1), [a], c_case.geom(1), [expected])
+    da, dc = dev(a), dev(c)
+    A = a_case.make_layout(0, da.data_ptr(), 1, dtype)
+    Cl = c_case.make_layout(0, dc.data_ptr(), 1, dtype)
+    gpu.transform(A, Cl, gpu.Comm.self(0), "N", alpha, beta)
+    got = host(dc, npd)
+    assert got.tobytes() == expected.tobytes()
+
+
+@pytest.mark.parametrize("dtype,lda,ldc", [(1, 16384, 16386), (1, 16385, 16385), (0, 16384, 16388),
+                                           (4, 16384, 16387)],
+                         ids=["f64-c2", "f64-odd", "f32-c4", "i32-c3"])
+def test_unaligned_copy_full_size(gpu, dtype, lda, ldc):
+    """a ScaLAPACK-sized p?gemr2d copy into columns off the 64-byte grid: C == A bit for bit,
+    padding rows untouched"""
+    n, b = 16384, 256
+    tdt = {0: torch.float32, 1: torch.float64, 4: torch.int32}[dtype]
+    if tdt == torch.int32:
+        A = torch.randint(-2**31, 2**31 - 1, (n, lda), dtype=torch.int32, device="cuda")
+    else:
+        A = torch.randn(n, lda, dtype=tdt, device="cuda")
+    Cm = torch.full((n, ldc), 7, dtype=tdt, device="cuda")
+    LA = gpu.block_cyclic_layout(n, n, b, b, 1, 1, n, n, 1, 1, "R", 0, 0, A.data_ptr(), lda, "C", 0,
+                                 dtype=dtype)
+    LC = gpu.block_cyclic_layout(n, n, b, b, 1, 1, n, n, 1, 1, "R", 0, 0, Cm.data_ptr(), ldc, "C", 0,
+                                 dtype=dtype)
+    gpu.transform(LA, LC, gpu.Comm.self(0), "N", 1, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(Cm[:, :n], A[:, :n])
+    assert bool((Cm[:, n:] == 7).all())
+
+
 @pytest.mark.parametrize("dtype", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("trans", ["N", "T", "C"])
 @pytest.mark.parametrize("geo", [(1000, 1100, 24, 24, 1, 1, 0), (1037, 997, 24, 20, 3, 5, 2),

@@ -438,6 +438,73 @@ static std::unique_ptr<plan> square_plan(int m, int nb, int lld, char op) {
     return make_plan({j}, 0, 1);
 }
 
+// copies into destinations off the 64-byte grid cut at the granules (engine.cpp granule_split,
+// run with COSTA_TUNING=1 COSTA_COPY_GRANULE=1): every destination element is written exactly once,
+// from the source element of the same (row, column); the sub-tiled ops start every destination
+// column on a 64-byte granule
+template <typename T>
+static bool check_granule_case(int m, int nb, int lda, int ldc, T beta) {
+    const std::string name = "granule";
+    const int64_t E = int64_t(sizeof(T));
+    const uint64_t A0 = uint64_t(1) << 40, C0 = uint64_t(1) << 42;
+    auto A = block_cyclic_layout<T>(m, m, nb, nb, 1, 1, m, m, 1, 1, 'R', 0, 0, reinterpret_cast<T*>(A0), lda, 'C', 0);
+    auto C = block_cyclic_layout<T>(m, m, nb, nb, 1, 1, m, m, 1, 1, 'R', 0, 0, reinterpret_cast<T*>(C0), ldc, 'C', 0);
+    elayout ea = erase(A), ec = erase(C);
+    job j{&ea, &ec, 'N', {}};
+    const T one = T(1);
+    std::memcpy(j.s.alpha.data(), &one, sizeof(T));
+    std::memcpy(j.s.beta.data(), &beta, sizeof(T));
+    auto p = make_plan({j}, 0, 1);
+    std::vector<costa_tile_op_t> ord;
+    std::vector<uint64_t> work;
+    const work_split w = build_work(p->dtype, p->local_ops, ord, work, list_local);
+    std::vector<char> hit(size_t(ldc) * size_t(m), 0);
+    int64_t aligned_ops = 0;
+    auto walk = [&](const costa_tile_op_t& o) {
+        CHECK(!(o.flags & COSTA_TILE_TRANSPOSE), "a copy became a transpose");
+        for (int64_t s = 0; s < o.ns; ++s)
+            for (int64_t f = 0; f < o.nf; ++f) {
+                const int64_t ea_ = int64_t(o.src - A0) / E + s * o.lds + f;
+                const int64_t ec_ = int64_t(o.dst - C0) / E + s * o.ldd + f;
+                const int64_t i = ea_ % lda, jj = ea_ / lda;
+                CHECK(i < m && jj < m && ec_ == i + jj * int64_t(ldc), "element (%lld, %lld) misplaced", (long long)i,
+                      (long long)jj);
+                CHECK(!hit[size_t(ec_)], "element (%lld, %lld) written twice", (long long)i, (long long)jj);
+                hit[size_t(ec_)] = 1;
+            }
+        return true;
+    };
+    for (int64_t i = 0; i < w.tiny_first; ++i) {
+        const costa_tile_op_t& o = ord[size_t(i)];
+        if (!walk(o)) return false;
+        // every sub-tiled op's destination columns start on a granule
+        CHECK(o.dst % 64 == 0 && (uint64_t(o.ldd) * uint64_t(E)) % 64 == 0, "sub-tiled op %lld off the granules",
+              (long long)i);
+        ++aligned_ops;
+    }
+    for (int64_t i = w.tiny_first; i < w.tiny_first + w.n_tiny; ++i)
+        if (!walk(ord[size_t(i)])) return false;
+    int64_t n_hit = 0;
+    for (char h : hit) n_hit += h;
+    CHECK(n_hit == int64_t(m) * m, "%lld of %lld elements written", (long long)n_hit, (long long)int64_t(m) * m);
+    CHECK(aligned_ops > 0, "no sub-tiled op");
+    std::printf("granule E=%lld lda %d ldc %d: %lld sub-tiled ops (granule-aligned), %lld large items, %lld pieces\n",
+                (long long)E, lda, ldc, (long long)aligned_ops, (long long)w.n_large, (long long)w.n_tiny);
+    return true;
+}
+
+static bool check_granule() {
+    for (int pad : {1, 2, 3, 8})
+        if (!check_granule_case<double>(2048, 256, 2048, 2048 + pad, 0.0) ||
+            !check_granule_case<double>(2048, 256, 2048 + pad, 2048 + pad, 2.0))
+            return false;
+    for (int pad : {1, 4, 8, 24})
+        if (!check_granule_case<float>(2048, 256, 2048, 2048 + pad, 0.f) ||
+            !check_granule_case<float>(2048, 200, 2048 + 3, 2048 + pad, 0.5f))
+            return false;
+    return check_granule_case<int>(2048, 256, 2048, 2051, 0);
+}
+
 static bool check_covers() {
     using z = std::complex<double>;
     struct g {
@@ -567,6 +634,11 @@ int main(int argc, char** argv) {
     }
     if (argc > 1 && std::string(argv[1]) == "cover") {
         if (!check_covers()) return 1;
+        std::printf("ok\n");
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "granule") {
+        if (!check_granule()) return 1;
         std::printf("ok\n");
         return 0;
     }
