@@ -217,7 +217,10 @@ __global__ __launch_bounds__(512) void tr_pattern_pol(const u32x4* __restrict__ 
 // band, s-block; nb bands of 64 destination columns, sb s-blocks of 128 rows):
 // 0 band-major (shipped), 1 each band bottom to top, 2 the bands in reverse, 3 boustrophedon,
 // 4 one band per XCD (workgroups are dealt round-robin over 8 XCDs: 8 bands in flight, XCD x on
-// band 8 j + x), 5 four bands advancing together one s-block at a time
+// band 8 j + x), 5 four bands advancing together one s-block at a time, 6 (r6) band-major with
+// a per-XCD row-band rotation: XCD x = i mod 8 starts its share of each band x eighths of the
+// column further down (s-block (j + x sb / 8) mod sb), so the workgroups resident at one time on
+// different XCDs write different in-column offsets
 __global__ __launch_bounds__(512) void tr_pattern_ord(const u32x4* __restrict__ a, u32x4* __restrict__ c,
                                                       long n, int o) {
     const long sb = n / 128, nb = n / 64, i = blockIdx.x;
@@ -227,6 +230,7 @@ __global__ __launch_bounds__(512) void tr_pattern_ord(const u32x4* __restrict__ 
     if (o == 3 && band % 2) blk = sb - 1 - blk;
     if (o == 4) band = 8 * (i / (8 * sb)) + i % 8, blk = (i / 8) % sb;
     if (o == 5) band = 4 * (i / (4 * sb)) + i % 4, blk = (i % (4 * sb)) / 4;
+    if (o == 6) blk = (blk + (i % 8) * (sb / 8)) % sb;  // a permutation of the band when 8 | sb
     const long f0 = band * 64, s0 = blk * 128;
     const int t = int(threadIdx.x);
     u32x4 x[8];
@@ -239,6 +243,28 @@ __global__ __launch_bounds__(512) void tr_pattern_ord(const u32x4* __restrict__ 
     for (int k = 0; k < 8; ++k) {
         const long f = f0 + 8 * (t / 64) + k;
         __builtin_nontemporal_store(x[k], c + (f * n + s0) / 2 + t % 64);
+    }
+}
+
+// kinds 400 / 401 (probes, r6): 64 x 256 fp64 sub-tiles (128 KiB), destination order; each
+// wavefront writes whole 2 KiB destination column segments, a column's two 1 KiB halves by two
+// back-to-back instructions.  400: 1024 threads x 8 vectors; 401: 512 threads x 16
+template <int NT>
+__global__ __launch_bounds__(NT) void tr_pattern_2k(const u32x4* __restrict__ a, u32x4* __restrict__ c, long n) {
+    constexpr int PL = 8192 / NT;  // 16-byte vectors a thread
+    const long sb = n / 256, w = blockIdx.x;
+    const long f0 = (w / sb) * 64, s0 = (w % sb) * 256;
+    const int t = int(threadIdx.x), lane = t % 64, wave = t / 64;
+    u32x4 x[PL];
+#pragma unroll
+    for (int k = 0; k < PL; ++k) {  // source column s0 + t / 32 + (NT / 32) k, rows f0 + 2 (t % 32) ..
+        const long s = s0 + t / 32 + (NT / 32) * k;
+        x[k] = __builtin_nontemporal_load(a + (s * n + f0) / 2 + t % 32);
+    }
+#pragma unroll
+    for (int k = 0; k < PL; ++k) {  // column f0 + (PL / 2) wave + k / 2, rows s0 + 128 (k % 2) + 2 lane ..
+        const long f = f0 + (PL / 2) * wave + k / 2;
+        __builtin_nontemporal_store(x[k], c + (f * n + s0) / 2 + 64 * (k % 2) + lane);
     }
 }
 
@@ -260,8 +286,12 @@ extern "C" int costa_ceiling_copy_ms(int kind, const void* src, void* dst, uint6
         const uint64_t n = col_bytes / 8;
         if (col_bytes % 4096 || bytes != n * col_bytes) return -1;
         grid = 1;
+    } else if (kind == 400 || kind == 401) {
+        const uint64_t n = col_bytes / 8;
+        if (col_bytes % 2048 || bytes != n * col_bytes) return -1;
+        grid = long((n / 64) * (n / 256));
     } else if (kind == 5 || kind == 7 || kind == 8 || (kind >= 200 && kind <= 205) ||
-               (kind >= 300 && kind <= 305)) {
+               (kind >= 300 && kind <= 306)) {
         // square fp64: n = col_bytes / 8 columns of n elements, n a multiple of 128
         const uint64_t n = col_bytes / 8;
         if (col_bytes % 1024 || bytes != n * col_bytes) return -1;
@@ -281,6 +311,14 @@ extern "C" int costa_ceiling_copy_ms(int kind, const void* src, void* dst, uint6
     const long col16 = long(col_bytes / 16), spc = long(col_bytes / kSegBytes);
     auto once = [&]() -> hipError_t {
         if (kind == 0) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s);
+        if (kind >= 400) {
+            const long n = long(col_bytes / 8);
+            if (kind == 400)
+                hipLaunchKernelGGL(tr_pattern_2k<1024>, dim3(unsigned(grid)), dim3(1024), 0, s, a, c, n);
+            else
+                hipLaunchKernelGGL(tr_pattern_2k<512>, dim3(unsigned(grid)), dim3(512), 0, s, a, c, n);
+            return hipGetLastError();
+        }
         if (kind >= 300) {
             const long n = long(col_bytes / 8);
             hipLaunchKernelGGL(tr_pattern_ord, dim3(unsigned((n / 64) * (n / 128))), dim3(512), 0, s, a, c, n,

@@ -1058,6 +1058,10 @@ __device__ __forceinline__ void tiny_op(const costa_tile_op_t& op, int lane, T* 
 constexpr int CB_NT = kCblockThreads;              // threads per workgroup
 constexpr int CB_CHUNKS = kCblockChunks;           // 16-byte destination vectors per thread
 constexpr int CB_U = 16;                           // source elements a lane has in flight
+#ifndef COSTA_CB_VLOAD  // 1 (tuning builds): sources read as aligned 16-byte chunks (4-byte types)
+#define COSTA_CB_VLOAD 0
+#endif
+[[maybe_unused]] constexpr int CB_UV = 4;          // ... chunks a lane has in flight then
 
 template <typename T, bool TR, bool AX>
 __global__ __launch_bounds__(CB_NT) void cblock_kernel(const costa_tile_op_t* __restrict__ ops,
@@ -1126,6 +1130,47 @@ __global__ __launch_bounds__(CB_NT) void cblock_kernel(const costa_tile_op_t* __
         // image position of source element (f, s): transpose (r0 + s, c0 + f), copy (r0 + f, c0 + s)
         const int di_f = tr ? P : 1, di_s = tr ? 1 : P;
         const int ibase = c0 * P + r0;
+#if COSTA_CB_VLOAD
+        if constexpr (sizeof(T) == 4) {
+            // (tuning) each source column run read as the aligned 16-byte chunks covering it: ncm
+            // chunk slots a column (enough for any alignment), slot (k, s) -> the k-th chunk from
+            // the one holding the column's first element; elements outside the run are dropped.
+            // An aligned chunk never crosses a page, and holds at least one element of the run.
+            const int ncm = (nf + 6) / 4, nq = ncm * op.ns;
+            lin<T> q(lane, ncm);
+            for (int b = 0; b < nq; b += 64 * CB_UV) {
+                raw16 x[CB_UV];
+                int fb[CB_UV], sv[CB_UV];
+#pragma unroll
+                for (int u = 0; u < CB_UV; ++u) {
+                    fb[u] = nf;
+                    if (b + u * 64 + lane < nq) {
+                        const T* col = src + int64_t(q.s) * lds;
+                        const int mis = int((reinterpret_cast<uintptr_t>(col) >> 2) & 3);
+                        const int f = 4 * q.f - mis;  // the chunk's first element, relative to the run
+                        if (f < nf) {
+                            x[u] = ld16(col + f);
+                            fb[u] = f;
+                            sv[u] = q.s;
+                        }
+                    }
+                    q.step();
+                }
+#pragma unroll
+                for (int u = 0; u < CB_UV; ++u) {
+                    if (fb[u] >= nf) continue;
+                    T v[4];
+                    __builtin_memcpy(v, &x[u], 16);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int f = fb[u] + e;
+                        if (f >= 0 && f < nf) img[ibase + f * di_f + sv[u] * di_s] = v[e];
+                    }
+                }
+            }
+            continue;
+        }
+#endif
         lin<T> p(lane, nf);
         for (int b = 0; b < n; b += 64 * CB_U) {
             T x[CB_U];

@@ -3,7 +3,8 @@
 m 0 both sides transposed, 1 flat loads + transposed stores, 2 transposed loads + flat stores)
 beside the headline transpose and the one-vector copy, per buffer pair (16384^2 fp64).
     python tools/pattern_probe.py [pairs] [pol]   (pol: kind 5 with each store cache policy,
-                                                   kinds 200-205; ord: sub-tile orders, 300-305)"""
+                                                   kinds 200-205; ord: sub-tile orders, 300-305;
+                                                   r6: kinds 5, 306, 400, 401)"""
 import ctypes as C
 import os
 import statistics
@@ -18,15 +19,16 @@ import costa_amd as costa  # noqa: E402
 N, B = 16384, 256
 BYTES = N * N * 8
 GEO = ["64x128", "32x256", "16x512", "128x64", "256x32"]
-POL = ORD = False
+POL = ORD = R6 = False
 
 
 def main():
     pairs = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     global POL
     POL = len(sys.argv) > 2 and sys.argv[2] == "pol"
-    global ORD
+    global ORD, R6
     ORD = len(sys.argv) > 2 and sys.argv[2] == "ord"
+    R6 = len(sys.argv) > 2 and sys.argv[2] == "r6"
     costa.lib()
     comm = costa.Comm.self(0)
     ceil = C.CDLL(os.path.join(ROOT, "costa_amd", "lib", "libcosta_ceiling.so"))
@@ -53,7 +55,10 @@ def main():
         ms = costa.get_stats(reset=True)["local_ms"] / 10
         costa.set_profiling(False)
         line = [f"pair {k}: transpose {ms:.4f} copy {med(4, a, c):.4f}"]
-        if ORD:  # kind 5's pattern with each sub-tile order
+        if R6:  # the two candidates not probed before, beside kind 5
+            line.append("kind 5 / XCD row-band rotation (306) / 2 KiB segments 1024 thr (400) / 512 thr (401) " +
+                        " / ".join(f"{med(q, a, c):.4f}" for q in (5, 306, 400, 401)))
+        elif ORD:  # kind 5's pattern with each sub-tile order
             line.append("orders band-major / band up / bands reversed / boustrophedon / band per XCD / "
                         "4 bands abreast " + " / ".join(f"{med(300 + q, a, c):.4f}" for q in range(6)))
         elif POL:  # kind 5's pattern with each store cache policy

@@ -17,3 +17,5 @@ done
 for op in N T; do
   COSTA_PLAN_TRACE=1 timeout -k 10 300 python3 bench.py --workload cfg5 --cfg5-op $op --steps 5 --warmup 2 --no-cpu-baseline --no-e2e --no-extra > $O/trace_$op.json 2> $O/trace_$op.err || exit 1
 done
+# the headline's two unprobed pattern candidates beside kind 5, per buffer pair
+timeout -k 10 300 python3 tools/pattern_probe.py 8 r6 > $O/pattern_r6.txt 2>&1 || exit 1
