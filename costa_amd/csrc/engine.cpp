@@ -566,11 +566,11 @@ bool few_strides(const std::vector<costa_tile_op_t>& ops) {
     return true;
 }
 
-// runs fn(begin, end) over [0, n) on up to 8 host threads (one when n is small)
+// runs fn(begin, end) over [0, n) on up to 8 host threads (one when n < min_items)
 template <typename F>
-void host_parallel(size_t n, F fn) {
+void host_parallel(size_t n, F fn, size_t min_items = 32768) {
     const size_t hw = std::max(1u, std::thread::hardware_concurrency());
-    const size_t T = n < 32768 ? 1 : std::min<size_t>(8, hw);
+    const size_t T = n < min_items ? 1 : std::min<size_t>(8, hw);
     if (T == 1) return fn(size_t(0), n);
     std::vector<std::thread> th;
     std::vector<std::exception_ptr> err(T);
@@ -638,51 +638,77 @@ int64_t cblock_groups(costa_dtype_t dtype, std::vector<const costa_tile_op_t*>& 
         if (run > op.ldd || op.ldd > budget) continue;
         cs.push_back({op.dst, op.dst + uint64_t(((runs - 1) * int64_t(op.ldd) + run) * E), op.ldd, i});
     }
-    std::sort(cs.begin(), cs.end(), [](const cand& a, const cand& b) {
-        return a.ldd != b.ldd ? a.ldd < b.ldd : a.lo < b.lo;
-    });
-    std::vector<char> taken(wave_ops.size(), 0);
-    struct group {
-        uint64_t dst;
-        std::vector<costa_tile_op_t> ops;
-        int32_t R, K;
-        uint32_t flags;
+    if (cs.size() < 2) return 0;
+    // order by (ldd, lo): stable LSD radix sorts, lo (element offsets from the lowest) first, then
+    // ldd (<= budget); a comparison sort of cfg 5's 245 k candidates cost ~10 ms of a plan miss
+    {
+        uint64_t lo_min = ~uint64_t(0), lo_max = 0;
+        for (const auto& c : cs) lo_min = std::min(lo_min, c.lo), lo_max = std::max(lo_max, c.lo);
+        std::vector<cand> tmp(cs.size());
+        constexpr int B = 12;
+        std::vector<uint32_t> at((size_t(1) << B) + 1);
+        auto pass = [&](auto digit) {
+            std::fill(at.begin(), at.end(), 0u);
+            for (const auto& c : cs) ++at[digit(c) + 1];
+            for (size_t d = 1; d < at.size(); ++d) at[d] += at[d - 1];
+            for (const auto& c : cs) tmp[at[digit(c)]++] = c;
+            cs.swap(tmp);
+        };
+        const uint64_t span = (lo_max - lo_min) / uint64_t(E);
+        for (int sh = 0; sh == 0 || (sh < 64 && (span >> sh) != 0); sh += B)
+            pass([&](const cand& c) { return size_t(((c.lo - lo_min) / uint64_t(E) >> sh) & ((1u << B) - 1)); });
+        for (int sh = 0; sh == 0 || (sh < 31 && (uint64_t(budget) >> sh) != 0); sh += B)
+            pass([&](const cand& c) { return size_t((uint32_t(c.ldd) >> sh) & ((1u << B) - 1)); });
+    }
+    // components: runs of candidates (one leading dimension) whose footprints overlap or touch
+    struct comp {
+        size_t a, b;
     };
-    std::vector<group> out;
+    std::vector<comp> comps;
     for (size_t a = 0; a < cs.size();) {
         size_t b = a + 1;
         uint64_t hi = cs[a].hi;
         while (b < cs.size() && cs[b].ldd == cs[a].ldd && cs[b].lo <= hi) hi = std::max(hi, cs[b].hi), ++b;
-        const size_t a0 = a;
+        if (b - a >= 2) comps.push_back({a, b});
         a = b;
-        if (b - a0 < 2) continue;
-        const int64_t R = cs[a0].ldd;
-        const uint64_t base = cs[a0].lo;
-        const costa_tile_op_t& first = *wave_ops[cs[a0].i];
-        const uint32_t fl = first.flags & ~vec_bits;
-        int64_t area = 0, K = 0;
-        bool ok = true;
-        for (size_t k = a0; k < b && ok; ++k) {
-            const costa_tile_op_t& op = *wave_ops[cs[k].i];
-            const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
-            const int64_t run = tr ? op.ns : op.nf, runs = tr ? op.nf : op.ns;
-            const int64_t e = int64_t(op.dst - base) / E;
-            ok = (op.flags & ~vec_bits) == fl && e % R + run <= R;
-            area += run * runs;
-            K = std::max(K, e / R + runs);
-        }
-        if (!ok || area != R * K || K > INT32_MAX) continue;
-        // ... and tile it exactly: with the areas adding up to R x K, the ops tile the range iff
-        // every corner point occurs an even number of times, the range's own four corners
-        // apart, which occur once ("perfect rectangle").  Overlapping ops whose areas happen
-        // to add up would leave elements no op writes, and the group kernel would store its
-        // uninitialised LDS there (costa_hip_execute_tiles takes caller ops).
-        {
-            std::vector<uint64_t> corner;
-            corner.reserve(4 * (b - a0));
+    }
+    // per component (host threads): does it tile its R x K range exactly, and how many groups
+    // (column bands of at most `budget` elements) it makes
+    struct cinfo {
+        int64_t K = 0, KB = 0;
+        uint64_t n_groups = 0;
+        uint32_t fl = 0;
+    };
+    std::vector<cinfo> ci(comps.size());
+    auto op_of = [&](size_t k) -> const costa_tile_op_t& { return *wave_ops[cs[k].i]; };
+    host_parallel(comps.size(), [&](size_t x0, size_t x1) {
+        std::vector<uint64_t> corner;
+        for (size_t x = x0; x < x1; ++x) {
+            const size_t a0 = comps[x].a, b = comps[x].b;
+            const int64_t R = cs[a0].ldd;
+            const uint64_t base = cs[a0].lo;
+            const uint32_t fl = op_of(a0).flags & ~vec_bits;
+            int64_t area = 0, K = 0;
+            bool ok = true;
+            for (size_t k = a0; k < b && ok; ++k) {
+                const costa_tile_op_t& op = op_of(k);
+                const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
+                const int64_t run = tr ? op.ns : op.nf, runs = tr ? op.nf : op.ns;
+                const int64_t e = int64_t(op.dst - base) / E;
+                ok = (op.flags & ~vec_bits) == fl && e % R + run <= R;
+                area += run * runs;
+                K = std::max(K, e / R + runs);
+            }
+            if (!ok || area != R * K || K > INT32_MAX) continue;
+            // ... and tile it exactly: with the areas adding up to R x K, the ops tile the range
+            // iff every corner point occurs an even number of times, the range's own four corners
+            // apart, which occur once ("perfect rectangle").  Overlapping ops whose areas happen to
+            // add up would leave elements no op writes, and the group kernel would store its
+            // uninitialised LDS there (costa_hip_execute_tiles takes caller ops).
+            corner.clear();
             const uint64_t W = uint64_t(K) + 1;
             for (size_t k = a0; k < b; ++k) {
-                const costa_tile_op_t& op = *wave_ops[cs[k].i];
+                const costa_tile_op_t& op = op_of(k);
                 const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
                 const uint64_t run = uint64_t(tr ? op.ns : op.nf), runs = uint64_t(tr ? op.nf : op.ns);
                 const uint64_t e = (op.dst - base) / uint64_t(E), r0 = e % uint64_t(R), c0 = e / uint64_t(R);
@@ -690,23 +716,139 @@ int64_t cblock_groups(costa_dtype_t dtype, std::vector<const costa_tile_op_t*>& 
                     for (const uint64_t c : {c0, c0 + runs}) corner.push_back(r * W + c);
             }
             std::sort(corner.begin(), corner.end());
-            std::vector<uint64_t> odd;
-            for (size_t k = 0; k < corner.size();) {
+            const uint64_t ur = uint64_t(R), uk = uint64_t(K), want[4] = {0, uk, ur * W, ur * W + uk};
+            int n_odd = 0;
+            for (size_t k = 0; k < corner.size() && ok;) {
                 size_t m = k;
                 while (m < corner.size() && corner[m] == corner[k]) ++m;
-                if ((m - k) & 1) odd.push_back(corner[k]);
+                if ((m - k) & 1) ok = n_odd < 4 && corner[k] == want[n_odd++];
                 k = m;
             }
-            const uint64_t ur = uint64_t(R), uk = uint64_t(K);
-            if (odd != std::vector<uint64_t>{0, uk, ur * W, ur * W + uk}) continue;
+            if (!ok || n_odd != 4) continue;
+            const int64_t KB = std::max<int64_t>(1, budget / R);
+            ci[x] = {K, KB, uint64_t((K + KB - 1) / KB), fl};
         }
-        // column bands of at most `budget` elements
-        const int64_t KB = std::max<int64_t>(1, budget / R);
-        for (int64_t cb0 = 0; cb0 < K; cb0 += KB) {
-            const int64_t cb1 = std::min(K, cb0 + KB);
-            group g{base + uint64_t(cb0 * R * E), {}, int32_t(R), int32_t(cb1 - cb0), fl};
+    }, 4096);
+    std::vector<uint64_t> g_at(comps.size() + 1, 0);
+    for (size_t x = 0; x < comps.size(); ++x) g_at[x + 1] = g_at[x] + ci[x].n_groups;
+    const size_t ng = size_t(g_at.back());
+    if (ng == 0) return 0;
+    // per group (host threads): its range, its op count (an op cut at the band edges counts once
+    // per band), the smallest locality hint of its ops (0: one lacks a hint)
+    struct group {
+        uint64_t dst;
+        uint32_t comp, band, n_ops, hint;
+    };
+    std::vector<group> gs(ng);
+    std::vector<char> taken(wave_ops.size(), 0);
+    auto band_cols = [&](size_t x, uint32_t band, int64_t& cb0, int64_t& cb1) {
+        cb0 = int64_t(band) * ci[x].KB;
+        cb1 = std::min(ci[x].K, cb0 + ci[x].KB);
+    };
+    host_parallel(comps.size(), [&](size_t x0, size_t x1) {
+        for (size_t x = x0; x < x1; ++x) {
+            if (ci[x].n_groups == 0) continue;
+            const size_t a0 = comps[x].a, b = comps[x].b;
+            const int64_t R = cs[a0].ldd;
+            const uint64_t base = cs[a0].lo;
+            for (uint32_t band = 0; band < ci[x].n_groups; ++band) {
+                int64_t cb0, cb1;
+                band_cols(x, band, cb0, cb1);
+                group& g = gs[size_t(g_at[x]) + band];
+                g = {base + uint64_t(cb0 * R * E), uint32_t(x), band, 0, UINT32_MAX};
+                for (size_t k = a0; k < b; ++k) {
+                    const costa_tile_op_t& op = op_of(k);
+                    const int64_t c0 = int64_t(op.dst - base) / E / R;
+                    const int64_t runs = (op.flags & COSTA_TILE_TRANSPOSE) ? op.nf : op.ns;
+                    if (std::max(cb0, c0) >= std::min(cb1, c0 + runs)) continue;
+                    ++g.n_ops;
+                    g.hint = op.order ? std::min(g.hint, op.order) : 0;
+                }
+            }
+            for (size_t k = a0; k < b; ++k) taken[cs[k].i] = 1;
+        }
+    }, 4096);
+    // destination order: a stable radix sort of the groups by range offset
+    std::vector<uint32_t> order(ng);
+    {
+        uint64_t lo = ~uint64_t(0), hi = 0;
+        for (const auto& g : gs) lo = std::min(lo, g.dst), hi = std::max(hi, g.dst);
+        std::vector<uint32_t> tmp(ng);
+        for (size_t g = 0; g < ng; ++g) order[g] = uint32_t(g);
+        constexpr int B = 12;
+        std::vector<uint32_t> at((size_t(1) << B) + 1);
+        const uint64_t span = (hi - lo) / uint64_t(E);
+        for (int sh = 0; sh == 0 || (sh < 64 && (span >> sh) != 0); sh += B) {
+            auto digit = [&](uint32_t g) { return size_t(((gs[g].dst - lo) / uint64_t(E) >> sh) & ((1u << B) - 1)); };
+            std::fill(at.begin(), at.end(), 0u);
+            for (const uint32_t g : order) ++at[digit(g) + 1];
+            for (size_t d = 1; d < at.size(); ++d) at[d] += at[d - 1];
+            for (const uint32_t g : order) tmp[at[digit(g)]++] = g;
+            order.swap(tmp);
+        }
+    }
+    bool any_tr = false;
+    for (const auto& g : gs) any_tr = any_tr || (ci[g.comp].fl & COSTA_TILE_TRANSPOSE);
+    map = any_tr ? cb_xcd_chunks : cb_round_robin;
+    bool hints = true;
+    for (const auto& g : gs) hints = hints && g.hint != 0 && g.hint != UINT32_MAX;
+    // XCD column bands for copy-only lists (r6, COSTA_CB_BANDS=0 / 1 (tuning): never / always):
+    // the groups in the planner's column-major order of their first target tile are cut into 8
+    // slices of the kernel's sizes (xcd_slice_order), slice x -- one band of target columns --
+    // walked by XCD x in destination order.  A source block split by a target block-row boundary
+    // is then read by two groups of one XCD about 1/8 of a block-row of its traffic apart, while
+    // the line they share is still in its L2: cfg 5 'N' reads 1.46x -> 1.03x their bytes, and
+    // with the 16-byte chunk loads of copy groups 0.436 -> 0.427 ms (each alone: +1 %, +1 %;
+    // profiles/r6c/, r6d/).  Transposing lists keep the 4-group XCD chunks ('T' 0.600 against
+    // 0.619 ms with bands).
+    const bool bands = bands_env == 1 || (bands_env == -1 && !any_tr);
+    if (bands && ng >= 16 && hints) {
+        const size_t per = ng / 8, rem = ng % 8;
+        std::vector<uint32_t> by(ng);
+        for (size_t i = 0; i < ng; ++i) by[i] = uint32_t(i);
+        std::stable_sort(by.begin(), by.end(), [&](uint32_t x, uint32_t y) { return gs[x].hint < gs[y].hint; });
+        std::vector<uint32_t> band(ng);
+        for (size_t k = 0; k < ng; ++k)
+            band[by[k]] = uint32_t(k < rem * (per + 1) ? k / (per + 1) : rem + (k - rem * (per + 1)) / per);
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return band[x] < band[y]; });
+        map = cb_xcd_bands;
+    }
+    // [header, ops...] per group in that order, each op cut at its band's edges (a sub-rectangle
+    // of a tile op is a tile op), written straight into their places (host threads)
+    const size_t base_at = ordered.size();
+    std::vector<uint64_t> at(ng + 1, 0);
+    for (size_t q = 0; q < ng; ++q) at[q + 1] = at[q] + 1 + gs[order[q]].n_ops;
+    size_t rest = 0;  // the remaining wavefront ops' pieces follow: room for most of them
+    for (size_t i = 0; i < wave_ops.size(); ++i) rest += !taken[i];
+    ordered.reserve(base_at + size_t(at[ng]) + 4 * rest + 1024);
+    ordered.resize(base_at + size_t(at[ng]));
+    work.reserve(work.size() + ng);
+    for (size_t q = 0; q < ng; ++q) {
+        work.push_back(uint64_t(base_at + at[q]));
+        const group& g = gs[order[q]];
+        int64_t cb0, cb1;
+        band_cols(g.comp, g.band, cb0, cb1);
+        lds = std::max(lds, int64_t(cs[comps[g.comp].a].ldd | 1) * (cb1 - cb0));
+    }
+    host_parallel(ng, [&](size_t q0, size_t q1) {
+        for (size_t q = q0; q < q1; ++q) {
+            const group& g = gs[order[q]];
+            const size_t x = g.comp, a0 = comps[x].a, b = comps[x].b;
+            const int64_t R = cs[a0].ldd;
+            const uint64_t base = cs[a0].lo;
+            int64_t cb0, cb1;
+            band_cols(x, g.band, cb0, cb1);
+            costa_tile_op_t* out = &ordered[base_at + size_t(at[q])];
+            costa_tile_op_t h{};
+            h.src = g.n_ops;
+            h.dst = g.dst;
+            h.nf = int32_t(R);
+            h.ns = int32_t(cb1 - cb0);
+            h.ldd = int32_t(R);
+            h.flags = ci[x].fl;
+            *out++ = h;
             for (size_t k = a0; k < b; ++k) {
-                costa_tile_op_t op = *wave_ops[cs[k].i];
+                costa_tile_op_t op = op_of(k);
                 const bool tr = op.flags & COSTA_TILE_TRANSPOSE;
                 const int64_t c0 = int64_t(op.dst - base) / E / R;
                 const int64_t runs = tr ? op.nf : op.ns;
@@ -721,70 +863,15 @@ int64_t cblock_groups(costa_dtype_t dtype, std::vector<const costa_tile_op_t*>& 
                     op.src += uint64_t(d0 * int64_t(op.lds) * E);
                     op.ns = int32_t(dn);
                 }
-                g.ops.push_back(op);
+                *out++ = op;
             }
-            out.push_back(std::move(g));
         }
-        for (size_t k = a0; k < b; ++k) taken[cs[k].i] = 1;
-    }
-    if (out.empty()) return 0;
-    std::sort(out.begin(), out.end(), [](const group& x, const group& y) { return x.dst < y.dst; });
-    bool any_tr = false;
-    for (const auto& g : out) any_tr = any_tr || (g.flags & COSTA_TILE_TRANSPOSE);
-    map = any_tr ? cb_xcd_chunks : cb_round_robin;
-    const bool bands = bands_env == 1;
-    if (bands && out.size() >= 16) {
-        // XCD column bands: the groups in the planner's column-major order of their first target
-        // tile are cut into 8 slices of the kernel's sizes (xcd_slice_order), slice x -- one band
-        // of target columns -- walked by XCD x in destination order.  A source block split by a
-        // target block-row boundary is then read by two groups of one XCD about 1/8 of a
-        // block-row of its traffic apart, and the line they share is still in its L2.
-        std::vector<uint32_t> hint(out.size(), 0);
-        bool hints = true;
-        for (size_t i = 0; i < out.size() && hints; ++i) {
-            uint32_t h = UINT32_MAX;
-            for (const auto& op : out[i].ops) h = std::min(h, op.order);
-            hints = h != 0 && h != UINT32_MAX;
-            hint[i] = h;
-        }
-        if (hints) {
-            const size_t n = out.size(), per = n / 8, rem = n % 8;
-            std::vector<uint32_t> by(n);
-            for (size_t i = 0; i < n; ++i) by[i] = uint32_t(i);
-            std::stable_sort(by.begin(), by.end(), [&](uint32_t x, uint32_t y) { return hint[x] < hint[y]; });
-            std::vector<uint32_t> band(n);
-            for (size_t k = 0; k < n; ++k) {
-                const size_t x = k < rem * (per + 1) ? k / (per + 1) : rem + (k - rem * (per + 1)) / per;
-                band[by[k]] = uint32_t(x);
-            }
-            std::vector<uint32_t> perm(n);
-            for (size_t i = 0; i < n; ++i) perm[i] = uint32_t(i);
-            std::stable_sort(perm.begin(), perm.end(), [&](uint32_t x, uint32_t y) { return band[x] < band[y]; });
-            std::vector<group> o2;
-            o2.reserve(n);
-            for (const uint32_t i : perm) o2.push_back(std::move(out[i]));
-            out.swap(o2);
-            map = cb_xcd_bands;
-        }
-    }
-    for (auto& g : out) {
-        costa_tile_op_t h{};
-        h.src = g.ops.size();
-        h.dst = g.dst;
-        h.nf = g.R;
-        h.ns = g.K;
-        h.ldd = g.R;
-        h.flags = g.flags;
-        work.push_back(uint64_t(ordered.size()));
-        ordered.push_back(h);
-        ordered.insert(ordered.end(), g.ops.begin(), g.ops.end());
-        lds = std::max(lds, int64_t(g.R | 1) * g.K);
-    }
+    }, 4096);
     size_t o = 0;
     for (size_t i = 0; i < wave_ops.size(); ++i)
         if (!taken[i]) wave_ops[o++] = wave_ops[i];
     wave_ops.resize(o);
-    return int64_t(out.size());
+    return int64_t(ng);
 }
 
 struct wave_knobs {  // defaults, overridable for tuning runs
@@ -815,8 +902,11 @@ struct wave_knobs {  // defaults, overridable for tuning runs
                          // 128 x 128 sub-tiles 0.366 against 0.396 with 256^2, 0.366 against
                          // 0.454 with 512^2), else 1 (c128 with 128^2 blocks: 2.87 against 2.27
                          // ms; copy lists untested under 2; profiles/r2/order/)
-    int copy_granule = 0;  // COSTA_COPY_GRANULE=1 (tuning): copy ops into destinations off the
-                           // 64-byte grid cut at each column's granules (granule_split)
+    int copy_granule = 1;  // copy ops into destinations off the 64-byte grid cut at each column's
+                           // granules (granule_split; r6: fp64 16384^2 'N' ldc + 1 / + 2 / + 3
+                           // 0.89 / 0.79 / 0.93 -> 0.76 / 0.76 / 0.74 ms, fp32 + 1 0.51 -> 0.41,
+                           // int32 + 3 0.51 -> 0.41, 16-byte aligned fp32 + 4 level; profiles/r6b/);
+                           // COSTA_COPY_GRANULE=0 (tuning): off
     int force_sq = 0;   // COSTA_FORCE_SQ=1 (tuning): transposing lists of fp64 / c64 / c128 take the
                         // square sub-tile whatever their ops' size
     int merge = 2;      // COSTA_MERGE=0: ops that continue each other are not merged, 1: only
@@ -943,6 +1033,15 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     // (a 16384^2 'T' with 24^2 blocks on one rank: one op on the large shape instead of 466 k
     // wavefront tiles)
     const wave_knobs& kn0 = knobs();
+    // COSTA_PLAN_TRACE=1: where build_work spends its time (stderr; get_plan traces the whole miss)
+    static const bool trace = std::getenv("COSTA_PLAN_TRACE") != nullptr;
+    const auto bw0 = std::chrono::steady_clock::now();
+    double bw_t[4] = {0, 0, 0, 0};  // classify + shaped lists, groups, wavefront order, pieces
+    auto lap = [&](int k) {
+        if (!trace) return;
+        const double t = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - bw0).count();
+        bw_t[k] = t;
+    };
     std::vector<costa_tile_op_t> ops_merged;
     const std::vector<costa_tile_op_t>* ops_src = &ops_in;
     if (kn0.merge && ops_in.size() > 1 && few_strides(ops_in)) {
@@ -965,19 +1064,27 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         }
     }
     std::vector<costa_tile_op_t> ops_mis;
+    bool mis_any = false;  // (the list is copied only when some op gains a flag: cfg 5's 245 k
+                           // small ops gain none, and the copy cost a plan-cache miss ~2 ms)
     if (mis) {
-        ops_mis = *ops_src;
         const uint64_t E = dtype_size(dtype);
         shape_dims shm;
         tile_shapes(dtype, any_transpose(ops_in), &shm);
         const int64_t min_elems = mis_env >= 0 ? 0 : int64_t(shm.cf) * shm.cs;
-        for (auto& op : ops_mis) {
-            if (int64_t(op.nf) * op.ns < min_elems) continue;
-            if ((mis & 1) && op.dst % 4 == 0 && (uint64_t(op.ldd) * E) % 4 == 0) op.flags |= COSTA_TILE_VEC_DST;
-            if ((mis & 2) && op.src % 4 == 0 && (uint64_t(op.lds) * E) % 4 == 0) op.flags |= COSTA_TILE_VEC_SRC;
+        auto gain = [&](const costa_tile_op_t& op) {
+            uint32_t f = 0;
+            if (int64_t(op.nf) * op.ns < min_elems) return f;
+            if ((mis & 1) && op.dst % 4 == 0 && (uint64_t(op.ldd) * E) % 4 == 0) f |= COSTA_TILE_VEC_DST;
+            if ((mis & 2) && op.src % 4 == 0 && (uint64_t(op.lds) * E) % 4 == 0) f |= COSTA_TILE_VEC_SRC;
+            return f & ~op.flags;
+        };
+        for (const auto& op : *ops_src) mis_any = mis_any || gain(op) != 0;
+        if (mis_any) {
+            ops_mis = *ops_src;
+            for (auto& op : ops_mis) op.flags |= gain(op);
         }
     }
-    const std::vector<costa_tile_op_t>* ops_pre = mis ? &ops_mis : ops_src;
+    const std::vector<costa_tile_op_t>* ops_pre = mis_any ? &ops_mis : ops_src;
     std::vector<costa_tile_op_t> ops_gran;
     if (kn0.copy_granule) {
         shape_dims shg;
@@ -1229,10 +1336,12 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         }
         n_work[c] = int64_t(work.size() - w0);
     }
+    lap(0);
     // destination-block groups out of the wavefront ops (after the skew items in `work`)
     int64_t cblock_lds = 0;
     int cb_map = cb_round_robin;
     const int64_t n_cblock = cblock_groups(dtype, wave_ops, kind, ordered, work, cblock_lds, cb_map);
+    lap(1);
     // ops are independent (disjoint destinations), so any order is valid; neighbours in
     // memory run at the same time and share the partially used cache lines at their edges.
     // The wavefront ops are ordered first, then cut into their pieces straight into the ordered
@@ -1295,6 +1404,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         for (size_t i = 0; i < nw; ++i) perm[i] = uint32_t(i);
     }
     if (kn.xcd_bands && mode == 2 && top > 0 && nw > 1) xcd_bands(wave_ops, E, kn.xcd_bands, local, perm);
+    lap(2);
     // pieces: count per op, scan, fill (host threads for long lists)
     std::vector<wave_grid> grid(nw);
     std::vector<size_t> at_piece(nw + 1, 0);
@@ -1331,6 +1441,14 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         for (size_t i = b; i < e; ++i)
             emit_pieces(*wave_ops[perm[i]], E, grid[i], local, &ordered[base + at_piece[i]]);
     });
+    if (trace) {
+        lap(3);
+        std::fprintf(stderr,
+                     "[costa build_work] %zu ops (%s list): classify + shaped %.2f ms, groups %.2f (%lld), "
+                     "wavefront order %.2f, pieces %.2f (%lld)\n",
+                     ops_in.size(), pack_list ? "pack" : local ? "local" : "unpack", bw_t[0], bw_t[1] - bw_t[0],
+                     (long long)n_cblock, bw_t[2] - bw_t[1], bw_t[3] - bw_t[2], (long long)w.n_tiny);
+    }
     return w;
 }
 

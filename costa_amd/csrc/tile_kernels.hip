@@ -1058,10 +1058,7 @@ __device__ __forceinline__ void tiny_op(const costa_tile_op_t& op, int lane, T* 
 constexpr int CB_NT = kCblockThreads;              // threads per workgroup
 constexpr int CB_CHUNKS = kCblockChunks;           // 16-byte destination vectors per thread
 constexpr int CB_U = 16;                           // source elements a lane has in flight
-#ifndef COSTA_CB_VLOAD  // 1 (tuning builds): sources read as aligned 16-byte chunks (4-byte types)
-#define COSTA_CB_VLOAD 0
-#endif
-[[maybe_unused]] constexpr int CB_UV = 4;          // ... chunks a lane has in flight then
+constexpr int CB_UV = 8;                           // ... 16-byte chunks, for 4-byte copy groups
 
 template <typename T, bool TR, bool AX>
 __global__ __launch_bounds__(CB_NT) void cblock_kernel(const costa_tile_op_t* __restrict__ ops,
@@ -1130,12 +1127,17 @@ __global__ __launch_bounds__(CB_NT) void cblock_kernel(const costa_tile_op_t* __
         // image position of source element (f, s): transpose (r0 + s, c0 + f), copy (r0 + f, c0 + s)
         const int di_f = tr ? P : 1, di_s = tr ? 1 : P;
         const int ibase = c0 * P + r0;
-#if COSTA_CB_VLOAD
-        if constexpr (sizeof(T) == 4) {
-            // (tuning) each source column run read as the aligned 16-byte chunks covering it: ncm
-            // chunk slots a column (enough for any alignment), slot (k, s) -> the k-th chunk from
-            // the one holding the column's first element; elements outside the run are dropped.
-            // An aligned chunk never crosses a page, and holds at least one element of the run.
+        if constexpr (sizeof(T) == 4 && !TR) {
+            // copy-only lists of 4-byte elements (r6): each source column run read as the aligned
+            // 16-byte chunks covering it -- a quarter of the load instructions: ncm chunk slots a
+            // column (enough for any alignment), slot (k, s) -> the k-th chunk from the one
+            // holding the column's first element; elements outside the run are dropped.  An
+            // aligned chunk never crosses a page, and holds at least one element of the run.
+            // cfg 5 'N', with the XCD column bands (engine.cpp cblock_groups): 0.436 -> 0.427 ms
+            // (CB_UV chunks a lane in flight: 2 / 4 / 8 0.438 / 0.429 / 0.427; 32 KiB groups 0.523;
+            // each change alone +1 %: profiles/r6c/, r6d/).  Transposing groups keep dword loads:
+            // a chunk's four elements land P x 4 apart in the transposed image (4-way LDS bank
+            // conflicts), 'T' 0.600 -> 0.857 ms
             const int ncm = (nf + 6) / 4, nq = ncm * op.ns;
             lin<T> q(lane, ncm);
             for (int b = 0; b < nq; b += 64 * CB_UV) {
@@ -1170,7 +1172,6 @@ __global__ __launch_bounds__(CB_NT) void cblock_kernel(const costa_tile_op_t* __
             }
             continue;
         }
-#endif
         lin<T> p(lane, nf);
         for (int b = 0; b < n; b += 64 * CB_U) {
             T x[CB_U];

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Per-kernel median of one rocprofv3 --pmc pass (counter_collection.csv under <dir>), for the
 costa kernels of the largest grid: python tools/pmc_brief.py <dir> [<alg bytes per launch>]
-FETCH_SIZE is doubled (gfx950 correction, MI355X_MICROARCH.md), values in KiB -> bytes."""
+FETCH_SIZE is doubled (gfx950 correction, MI355X_MICROARCH.md; exact for dword, 16-byte and
+partial-line loads: profiles/r6c/, tools/pmc_bytes.py), values in KiB -> bytes."""
 import csv
 import glob
 import statistics

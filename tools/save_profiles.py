@@ -10,9 +10,10 @@ grid are taken, the median per kernel is summed.  One json per workload:
   pmc_tile_kernel.json  (default bench, BASELINE cfg 2)
   pmc_cfg5_N.json / pmc_cfg5_T.json
 bench.py's measured_traffic() picks the file whose bytes_per_launch_alg equals its own.
-Caveat written into each file: the x2 FETCH correction is calibrated for 16-B-per-lane loads;
-the wavefront path of cfg 5 uses 4-B loads: calibrated in profiles/r11/calib/calib.json
-(x1.95-1.98 on a line-aligned geometry, so x2 is within 2.5 %)."""
+The x2 FETCH correction is exact for every access width the kernels use (r6, profiles/r6c/:
+TCC_EA0_RDREQ_128B / _64B / _32B show that gfx950's L2 reads memory in whole 128-byte lines for
+dword, 16-byte and partial-line loads alike, FETCH_SIZE tallying each at 64 B;
+tools/pmc_bytes.py computes the bytes from those counters directly)."""
 import csv
 import json
 import os
@@ -89,7 +90,8 @@ def derive(prefix, dtype, out_name):
            "kernels_fetch": fper, "kernels_write": wper,
            "hbm_bytes_per_launch_corrected": int((2 * fk + wk) * 1024),
            "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halving; "
-                         "16-B loads exact, 4-B loads within 2.5 %: profiles/r11/calib)"}
+                         "exact for dword, 16-byte and partial-line loads: every memory read is a 128-byte "
+                         "request, profiles/r6c/)"}
     d = bench_line(os.path.join(src, f"{prefix}pmc_fetch.log"))
     if d:
         out["bytes_per_launch_alg"] = d["roofline"]["bytes_per_launch"]

@@ -215,7 +215,11 @@ static bool check_merge() {
             // (pieces of wavefront ops are in `ord` after tiny_first; shaped ops before)
             CHECK(area == int64_t(m) * m, "%c %d: ops cover %lld of %lld elements", op, m, (long long)area,
                   (long long)int64_t(m) * m);
-            CHECK(p->local_ops.size() > 1000 && w.tiny_first <= 2 && w.n_tiny == 0 && w.n_large + w.n_skew > 0,
+            // ('N' with columns off the 64-byte grid: the merged op is then cut at the granules,
+            // engine.cpp granule_split -- 4 column classes, their heads as wavefront pieces)
+            const bool gran = op == 'N' && (int64_t(m) * 4) % 64 != 0;
+            CHECK(p->local_ops.size() > 1000 && w.tiny_first <= (gran ? 8 : 2) && (gran || w.n_tiny == 0) &&
+                      w.n_large + w.n_skew > 0,
                   "%c %d: %zu tiles -> %lld shaped ops, %lld pieces", op, m, p->local_ops.size(),
                   (long long)w.tiny_first, (long long)w.n_tiny);
             std::printf("merge %c %d: %zu tiles -> %lld op(s), %lld large / %lld skew sub-tiles\n", op, m,
