@@ -615,6 +615,13 @@ int64_t cblock_groups(costa_dtype_t dtype, std::vector<const costa_tile_op_t*>& 
     }();
     lds = 0;
     map = cb_round_robin;
+    // COSTA_PLAN_TRACE=1: the phases of the group builder (stderr)
+    static const bool trace = std::getenv("COSTA_PLAN_TRACE") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    double lap_ms[7] = {0, 0, 0, 0, 0, 0, 0};  // candidates, sort, components, check, groups, order, emit
+    auto lap = [&](int k) {
+        if (trace) lap_ms[k] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    };
     // real types (complex elements are on the large shapes wherever it matters: cfg 4)
     const bool real = dtype == COSTA_FLOAT || dtype == COSTA_DOUBLE || dtype == COSTA_INT32;
     if (!on || !real || kind == list_pack || wave_ops.size() < 2) return 0;
@@ -639,6 +646,7 @@ int64_t cblock_groups(costa_dtype_t dtype, std::vector<const costa_tile_op_t*>& 
         cs.push_back({op.dst, op.dst + uint64_t(((runs - 1) * int64_t(op.ldd) + run) * E), op.ldd, i});
     }
     if (cs.size() < 2) return 0;
+    lap(0);
     // order by (ldd, lo): stable LSD radix sorts, lo (element offsets from the lowest) first, then
     // ldd (<= budget); a comparison sort of cfg 5's 245 k candidates cost ~10 ms of a plan miss
     {
@@ -660,6 +668,7 @@ int64_t cblock_groups(costa_dtype_t dtype, std::vector<const costa_tile_op_t*>& 
         for (int sh = 0; sh == 0 || (sh < 31 && (uint64_t(budget) >> sh) != 0); sh += B)
             pass([&](const cand& c) { return size_t((uint32_t(c.ldd) >> sh) & ((1u << B) - 1)); });
     }
+    lap(1);
     // components: runs of candidates (one leading dimension) whose footprints overlap or touch
     struct comp {
         size_t a, b;
@@ -672,6 +681,7 @@ int64_t cblock_groups(costa_dtype_t dtype, std::vector<const costa_tile_op_t*>& 
         if (b - a >= 2) comps.push_back({a, b});
         a = b;
     }
+    lap(2);
     // per component (host threads): does it tile its R x K range exactly, and how many groups
     // (column bands of at most `budget` elements) it makes
     struct cinfo {
@@ -729,6 +739,7 @@ int64_t cblock_groups(costa_dtype_t dtype, std::vector<const costa_tile_op_t*>& 
             ci[x] = {K, KB, uint64_t((K + KB - 1) / KB), fl};
         }
     }, 4096);
+    lap(3);
     std::vector<uint64_t> g_at(comps.size() + 1, 0);
     for (size_t x = 0; x < comps.size(); ++x) g_at[x + 1] = g_at[x] + ci[x].n_groups;
     const size_t ng = size_t(g_at.back());
@@ -768,6 +779,7 @@ int64_t cblock_groups(costa_dtype_t dtype, std::vector<const costa_tile_op_t*>& 
             for (size_t k = a0; k < b; ++k) taken[cs[k].i] = 1;
         }
     }, 4096);
+    lap(4);
     // destination order: a stable radix sort of the groups by range offset
     std::vector<uint32_t> order(ng);
     {
@@ -803,16 +815,28 @@ int64_t cblock_groups(costa_dtype_t dtype, std::vector<const costa_tile_op_t*>& 
     // 0.619 ms with bands).
     const bool bands = bands_env == 1 || (bands_env == -1 && !any_tr);
     if (bands && ng >= 16 && hints) {
+        // (stable counting sorts: by hint, 2 x 16-bit digits; then the slices, 8 buckets)
         const size_t per = ng / 8, rem = ng % 8;
-        std::vector<uint32_t> by(ng);
+        std::vector<uint32_t> by(ng), tmp(ng), at16((size_t(1) << 16) + 1);
         for (size_t i = 0; i < ng; ++i) by[i] = uint32_t(i);
-        std::stable_sort(by.begin(), by.end(), [&](uint32_t x, uint32_t y) { return gs[x].hint < gs[y].hint; });
-        std::vector<uint32_t> band(ng);
+        for (int sh = 0; sh < 32; sh += 16) {
+            std::fill(at16.begin(), at16.end(), 0u);
+            for (const uint32_t g : by) ++at16[((gs[g].hint >> sh) & 0xFFFFu) + 1];
+            for (size_t d = 1; d < at16.size(); ++d) at16[d] += at16[d - 1];
+            for (const uint32_t g : by) tmp[at16[(gs[g].hint >> sh) & 0xFFFFu]++] = g;
+            by.swap(tmp);
+        }
+        std::vector<uint8_t> band(ng);
         for (size_t k = 0; k < ng; ++k)
-            band[by[k]] = uint32_t(k < rem * (per + 1) ? k / (per + 1) : rem + (k - rem * (per + 1)) / per);
-        std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return band[x] < band[y]; });
+            band[by[k]] = uint8_t(k < rem * (per + 1) ? k / (per + 1) : rem + (k - rem * (per + 1)) / per);
+        uint32_t at8[9] = {0};
+        for (const uint32_t g : order) ++at8[band[g] + 1];
+        for (int d = 1; d < 9; ++d) at8[d] += at8[d - 1];
+        for (const uint32_t g : order) tmp[at8[band[g]]++] = g;
+        order.swap(tmp);
         map = cb_xcd_bands;
     }
+    lap(5);
     // [header, ops...] per group in that order, each op cut at its band's edges (a sub-rectangle
     // of a tile op is a tile op), written straight into their places (host threads)
     const size_t base_at = ordered.size();
@@ -871,6 +895,14 @@ int64_t cblock_groups(costa_dtype_t dtype, std::vector<const costa_tile_op_t*>& 
     for (size_t i = 0; i < wave_ops.size(); ++i)
         if (!taken[i]) wave_ops[o++] = wave_ops[i];
     wave_ops.resize(o);
+    if (trace) {
+        lap(6);
+        std::fprintf(stderr,
+                     "[costa groups] %zu candidates, %zu components, %zu groups: candidates %.2f ms, sort %.2f, "
+                     "components %.2f, tiling check %.2f, group table %.2f, order %.2f, emit %.2f\n",
+                     cs.size(), comps.size(), ng, lap_ms[0], lap_ms[1] - lap_ms[0], lap_ms[2] - lap_ms[1],
+                     lap_ms[3] - lap_ms[2], lap_ms[4] - lap_ms[3], lap_ms[5] - lap_ms[4], lap_ms[6] - lap_ms[5]);
+    }
     return int64_t(ng);
 }
 
