@@ -653,7 +653,7 @@ int64_t cblock_groups(costa_dtype_t dtype, std::vector<const costa_tile_op_t*>& 
         uint64_t lo_min = ~uint64_t(0), lo_max = 0;
         for (const auto& c : cs) lo_min = std::min(lo_min, c.lo), lo_max = std::max(lo_max, c.lo);
         std::vector<cand> tmp(cs.size());
-        constexpr int B = 12;
+        constexpr int B = 16;  // 2 passes for cfg 5's 1 GiB arena, 1 for the leading dimensions
         std::vector<uint32_t> at((size_t(1) << B) + 1);
         auto pass = [&](auto digit) {
             std::fill(at.begin(), at.end(), 0u);
@@ -690,7 +690,14 @@ int64_t cblock_groups(costa_dtype_t dtype, std::vector<const costa_tile_op_t*>& 
         uint32_t fl = 0;
     };
     std::vector<cinfo> ci(comps.size());
-    auto op_of = [&](size_t k) -> const costa_tile_op_t& { return *wave_ops[cs[k].i]; };
+    // the candidates' ops gathered once in sorted order: the passes below read them sequentially
+    // (through the pointers they were cache misses all over a 10 MB list: cfg 5's group table and
+    // emission 5 ms each on the box)
+    std::vector<costa_tile_op_t> sop(cs.size());
+    host_parallel(cs.size(), [&](size_t k0, size_t k1) {
+        for (size_t k = k0; k < k1; ++k) sop[k] = *wave_ops[cs[k].i];
+    });
+    auto op_of = [&](size_t k) -> const costa_tile_op_t& { return sop[k]; };
     host_parallel(comps.size(), [&](size_t x0, size_t x1) {
         std::vector<uint64_t> corner;
         for (size_t x = x0; x < x1; ++x) {
@@ -776,9 +783,13 @@ int64_t cblock_groups(costa_dtype_t dtype, std::vector<const costa_tile_op_t*>& 
                     g.hint = op.order ? std::min(g.hint, op.order) : 0;
                 }
             }
-            for (size_t k = a0; k < b; ++k) taken[cs[k].i] = 1;
         }
     }, 4096);
+    // (one thread: the grouped ops are scattered over the list, and threads marking them shared
+    // cache lines)
+    for (size_t x = 0; x < comps.size(); ++x)
+        if (ci[x].n_groups)
+            for (size_t k = comps[x].a; k < comps[x].b; ++k) taken[cs[k].i] = 1;
     lap(4);
     // destination order: a stable radix sort of the groups by range offset
     std::vector<uint32_t> order(ng);
@@ -787,7 +798,7 @@ int64_t cblock_groups(costa_dtype_t dtype, std::vector<const costa_tile_op_t*>& 
         for (const auto& g : gs) lo = std::min(lo, g.dst), hi = std::max(hi, g.dst);
         std::vector<uint32_t> tmp(ng);
         for (size_t g = 0; g < ng; ++g) order[g] = uint32_t(g);
-        constexpr int B = 12;
+        constexpr int B = 16;
         std::vector<uint32_t> at((size_t(1) << B) + 1);
         const uint64_t span = (hi - lo) / uint64_t(E);
         for (int sh = 0; sh == 0 || (sh < 64 && (span >> sh) != 0); sh += B) {
