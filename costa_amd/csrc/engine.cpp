@@ -690,14 +690,9 @@ int64_t cblock_groups(costa_dtype_t dtype, std::vector<const costa_tile_op_t*>& 
         uint32_t fl = 0;
     };
     std::vector<cinfo> ci(comps.size());
-    // the candidates' ops gathered once in sorted order: the passes below read them sequentially
-    // (through the pointers they were cache misses all over a 10 MB list: cfg 5's group table and
-    // emission 5 ms each on the box)
-    std::vector<costa_tile_op_t> sop(cs.size());
-    host_parallel(cs.size(), [&](size_t k0, size_t k1) {
-        for (size_t k = k0; k < k1; ++k) sop[k] = *wave_ops[cs[k].i];
-    });
-    auto op_of = [&](size_t k) -> const costa_tile_op_t& { return sop[k]; };
+    // (gathering the candidates' ops into sorted order first made the passes below no faster on
+    // the box: tiling check + group table + emission 16.5 against 12.4 ms, profiles/r6g/)
+    auto op_of = [&](size_t k) -> const costa_tile_op_t& { return *wave_ops[cs[k].i]; };
     host_parallel(comps.size(), [&](size_t x0, size_t x1) {
         std::vector<uint64_t> corner;
         for (size_t x = x0; x < x1; ++x) {
