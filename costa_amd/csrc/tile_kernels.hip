@@ -1135,9 +1135,10 @@ __global__ __launch_bounds__(CB_NT) void cblock_kernel(const costa_tile_op_t* __
             // aligned chunk never crosses a page, and holds at least one element of the run.
             // cfg 5 'N', with the XCD column bands (engine.cpp cblock_groups): 0.436 -> 0.427 ms
             // (CB_UV chunks a lane in flight: 2 / 4 / 8 0.438 / 0.429 / 0.427; 32 KiB groups 0.523;
-            // each change alone +1 %: profiles/r6c/, r6d/).  Transposing groups keep dword loads:
-            // a chunk's four elements land P x 4 apart in the transposed image (4-way LDS bank
-            // conflicts), 'T' 0.600 -> 0.857 ms
+            // each change alone +1 %; 8 KiB groups 0.484, 128 / 512 threads 0.452 / 0.641:
+            // profiles/r6c/, r6d/, r6f/, r6h/).  Transposing groups keep dword loads: a chunk's
+            // four elements land P x 4 apart in the transposed image, 'T' 0.600 -> 0.857 ms, 0.775
+            // with the writes in lane-rotated order
             const int ncm = (nf + 6) / 4, nq = ncm * op.ns;
             lin<T> q(lane, ncm);
             for (int b = 0; b < nq; b += 64 * CB_UV) {
@@ -1163,6 +1164,9 @@ __global__ __launch_bounds__(CB_NT) void cblock_kernel(const costa_tile_op_t* __
                     if (fb[u] >= nf) continue;
                     T v[4];
                     __builtin_memcpy(v, &x[u], 16);
+                    // (in element order: the 4-way bank conflicts of one write step -- lanes 4
+                    // elements apart -- cost less than a lane-rotated order's selects, 'N' 0.428
+                    // against 0.441 ms; profiles/r6h/)
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         const int f = fb[u] + e;
