@@ -783,6 +783,19 @@ def mismatch_arena(Cm, ca, op, gen, C0=None, al=1.0, be=0.0, n=None):
     return count_mismatch(Cm[e], exp)
 
 
+def kernels_ran(st: dict, steps: int, tname: str) -> dict:
+    """the kernels a step launched and their work items per step, from the library's counters
+    (costa_stats_t tile_items / skew_items / cblock_items / tiny_items): tile_kernel sub-tiles,
+    skew_kernel sub-tiles, cblock_kernel destination-block groups, tiny_kernel wavefront pieces"""
+    out = {}
+    for key, name in (("tile_items", "tile_kernel"), ("skew_items", "skew_kernel"),
+                      ("cblock_items", "cblock_kernel"), ("tiny_items", "tiny_kernel")):
+        n = st.get(key, 0) / max(steps, 1)
+        if n:
+            out[f"{name}<{tname}>"] = int(n) if float(n).is_integer() else round(n, 1)
+    return out
+
+
 def extra_keys(world: int, args):
     """BASELINE's other configurations, measured after the headline in the same processes: at
     the GPU counts they are quoted on (cfg 3 at 4 GPUs, cfg 4 and cfg 5 at 8), and at one GPU
@@ -1142,6 +1155,8 @@ def main():
         r["rank_frac"] = [round(-max_over_ranks(-own) / HBM_PEAK_GBPS, 4),
                           round(max_over_ranks(own) / HBM_PEAK_GBPS, 4)]
         r["exchange_ms"] = max_over_ranks(st["exchange_ms"] / steps)
+        r["kernels"] = kernels_ran(st, steps, {"pxtran": "double", "cfg3": "double", "cfg4": "cpx<double>",
+                                               "cfg5": "float"}[w["kind"]])
         return r
 
     def summary(w, r, steps):  # one extra-config entry of the JSON line
@@ -1156,7 +1171,8 @@ def main():
                "first_call_ms": round(r["first_call_ms"], 2), "verified": r["verified"],
                # the pass the phase (kernel) times come from, so that kernel <= step reads off
                # the entry itself
-               "events_pass_ms_per_step": round(r["el_ev"] / steps * 1e3, 4)}
+               "events_pass_ms_per_step": round(r["el_ev"] / steps * 1e3, 4),
+               "kernels": r["kernels"]}
         for k in ("grid", "m", "n", "block"):
             if k in w:
                 out[k] = w[k]
@@ -1203,7 +1219,8 @@ def main():
                        f"cblock_kernel<float> + tiny_kernel<float> ({name} list: destination-block "
                        f"groups, the few ops outside them as wavefront pieces)"),
             "bytes_per_launch": int(per_launch),
-            "avg_launch_ms": round(avg_ms, 4)}
+            "avg_launch_ms": round(avg_ms, 4),
+            "kernels": res["kernels"]}
 
     roof.update(pass_fracs(per_launch, kl / args.steps, avg_ms, el / args.steps * 1e3,
                            el_ev / args.steps * 1e3))

@@ -98,7 +98,8 @@ class Stats(C.Structure):
                 ("transforms", C.c_int64), ("plan_hits", C.c_int64),
                 ("plan_misses", C.c_int64), ("host_groups", C.c_int64),
                 ("device_plans", C.c_int64), ("plan_ms", C.c_double), ("host_direct", C.c_int64),
-                ("host_direct_groups", C.c_int64)]
+                ("host_direct_groups", C.c_int64), ("tile_items", C.c_int64), ("skew_items", C.c_int64),
+                ("cblock_items", C.c_int64), ("tiny_items", C.c_int64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

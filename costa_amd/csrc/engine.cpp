@@ -2248,14 +2248,23 @@ void transform(const std::vector<job>& jobs, comm* c, void* user_stream, bool as
     }
 
     g_stats.transforms++;
+    auto count_items = [](const work_split& w) {
+        g_stats.tile_items += w.n_large + w.n_medium;
+        g_stats.skew_items += w.n_skew;
+        g_stats.cblock_items += w.n_cblock;
+        g_stats.tiny_items += w.n_tiny;
+    };
     if (cp.l_local.n_items()) {
         g_stats.local_launches++;
         g_stats.local_bytes += p.local_bytes;
+        count_items(cp.l_local);
     }
     if (exchange) {
         for (const auto& x : cp.rounds) {
             g_stats.pack_launches += x->l_pack.n_items() ? 1 : 0;
             g_stats.unpack_launches += x->l_unpack.n_items() ? 1 : 0;
+            count_items(x->l_pack);
+            count_items(x->l_unpack);
         }
         g_stats.pack_bytes += p.pack_bytes;
         g_stats.unpack_bytes += p.unpack_bytes;

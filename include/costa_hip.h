@@ -231,6 +231,10 @@ typedef struct {
     int64_t host_direct_groups; /* ... the tile groups that moved that way (PACK: a pack kernel
                                    from the DMA'd source rectangle; LOCAL / UNPACK: kernels
                                    writing the target rectangle's image, DMA'd back) */
+    /* work items launched by the device-resident path, per kernel (r6): tile_kernel sub-tiles
+       (the large, square, medium and 32 x 32 shapes), skew_kernel sub-tiles, cblock_kernel
+       destination-block groups, tiny_kernel wavefront pieces */
+    int64_t tile_items, skew_items, cblock_items, tiny_items;
 } costa_stats_t;
 int costa_hip_set_profiling(int on);
 int costa_hip_get_stats(costa_stats_t* out, int reset);

@@ -420,3 +420,14 @@ def test_extra_entries_carry_their_events_pass_step(monkeypatch):
     entry = {"ms_per_step": 8.422, "events_pass_ms_per_step": 8.4601,
              "phase_ms_per_step": {"pack": 0.0, "local": 8.4476, "unpack": 0.0}}
     assert max(entry["phase_ms_per_step"].values()) <= entry["events_pass_ms_per_step"]
+
+
+def test_entries_name_the_kernels_that_ran():
+    """the line's cfg 5 entry carries the kernel names that ran, from the
+    library's per-kernel work-item counters (costa_stats_t, r6) over the timed steps"""
+    st = {"tile_items": 0, "skew_items": 0, "cblock_items": 80741 * 20, "tiny_items": 2362 * 20}
+    assert bench.kernels_ran(st, 20, "float") == {"cblock_kernel<float>": 80741, "tiny_kernel<float>": 2362}
+    assert bench.kernels_ran({"tile_items": 4096 * 5}, 5, "double") == {"tile_kernel<double>": 4096}
+    import costa_amd
+    names = [f for f, _ in costa_amd.Stats._fields_]
+    assert names[-4:] == ["tile_items", "skew_items", "cblock_items", "tiny_items"]
