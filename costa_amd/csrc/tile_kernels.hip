@@ -199,11 +199,17 @@ __device__ __forceinline__ void st16(void* p, const raw16& r) {
     }
 }
 
-template <typename T>
+template <typename T, bool NT = true>
 __device__ __forceinline__ void vload(vec<T>& out, const T* p, int n, bool vec_ok) {
     constexpr int V = vec<T>::V;
     if (vec_ok && n >= V) {
-        raw16 r = ld16(p);
+        raw16 r;
+        if constexpr (NT) {
+            r = ld16(p);
+        } else {
+            const u32x4d v = *reinterpret_cast<const u32x4d*>(p);
+            __builtin_memcpy(&r, &v, 16);
+        }
         __builtin_memcpy(&out, &r, 16);
     } else {
 #pragma unroll
@@ -781,7 +787,11 @@ __global__ __launch_bounds__(512) void skew_kernel(const costa_tile_op_t* __rest
 #pragma unroll
     for (int k = 0; k < K::PL; ++k) {
         const int r = c0 + k * K::CPP, s = s0 - G + r;
-        if (r < K::RS && s >= s_lo && s < s_hi && nf_lane > 0) vload(x[k], src + s * lds + lf, nf_lane, vs);
+        // (default cache policy: the G rows above s0 are also the previous sub-tile's, which
+        // reads them from L2 then; non-temporal loads ran fp64 dst-odd 'T' 0.750-0.764 against
+        // 0.780-0.782 ms, fp32 both sides odd 1-1.5 % slower, the rest level: profiles/r6j/)
+        if (r < K::RS && s >= s_lo && s < s_hi && nf_lane > 0)
+            vload<T, false>(x[k], src + s * lds + lf, nf_lane, vs);
     }
 #pragma unroll
     for (int k = 0; k < K::PL; ++k) {
@@ -1133,7 +1143,8 @@ __global__ __launch_bounds__(CB_NT) void cblock_kernel(const costa_tile_op_t* __
             // column (enough for any alignment), slot (k, s) -> the k-th chunk from the one
             // holding the column's first element; elements outside the run are dropped.  An
             // aligned chunk never crosses a page, and holds at least one element of the run.
-            // cfg 5 'N', with the XCD column bands (engine.cpp cblock_groups): 0.436 -> 0.427 ms
+            // cfg 5 'N', with the XCD column bands (engine.cpp cblock_groups): 0.436 -> 0.427 ms,
+            // 0.402 with default-policy chunk loads
             // (CB_UV chunks a lane in flight: 2 / 4 / 8 0.438 / 0.429 / 0.427; 32 KiB groups 0.523;
             // each change alone +1 %; 8 KiB groups 0.484, 128 / 512 threads 0.452 / 0.641:
             // profiles/r6c/, r6d/, r6f/, r6h/).  Transposing groups keep dword loads: a chunk's
@@ -1152,7 +1163,12 @@ __global__ __launch_bounds__(CB_NT) void cblock_kernel(const costa_tile_op_t* __
                         const int mis = int((reinterpret_cast<uintptr_t>(col) >> 2) & 3);
                         const int f = 4 * q.f - mis;  // the chunk's first element, relative to the run
                         if (f < nf) {
-                            x[u] = ld16(col + f);
+                            // default cache policy, not non-temporal: the edge lines a run shares
+                            // with its neighbours (the next column, the group of the next band or
+                            // block-row) stay in L2 for them -- nt chunks read 1.32x the run bytes
+                            // at 0.428 ms, these 1.03x at 0.402 (profiles/r6i/)
+                            const u32x4a v = *reinterpret_cast<const u32x4a*>(col + f);
+                            __builtin_memcpy(&x[u], &v, 16);
                             fb[u] = f;
                             sv[u] = q.s;
                         }
