@@ -99,7 +99,7 @@ class Stats(C.Structure):
                 ("plan_misses", C.c_int64), ("host_groups", C.c_int64),
                 ("device_plans", C.c_int64), ("plan_ms", C.c_double), ("host_direct", C.c_int64),
                 ("host_direct_groups", C.c_int64), ("tile_items", C.c_int64), ("skew_items", C.c_int64),
-                ("cblock_items", C.c_int64), ("tiny_items", C.c_int64)]
+                ("cblock_items", C.c_int64), ("tiny_items", C.c_int64), ("device_lists", C.c_int64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -165,6 +165,8 @@ def lib():
         "costa_hip_plan_export_device": (i, [i, i, C.POINTER(vp), C.POINTER(vp), C.c_char_p, vp, vp,
                                              i, i, C.POINTER(PlanInfo), vp, vp, vp, vp, vp, vp, vp,
                                              vp]),
+        "costa_hip_set_list_builder": (i, [i]),
+        "costa_hip_work_export": (i, [i, vp, i64, i, i, vp, i64, vp, i64, C.POINTER(i64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -516,6 +518,43 @@ def set_planner(mode: int):
     before the first GPU plan of the process, which loads the planner's kernels; default),
     0 = always the host, 2 = the GPU wherever it applies (costa_hip_set_planner)."""
     _check(lib().costa_hip_set_planner(int(mode)))
+
+
+def set_list_builder(mode: int):
+    """Builder of the work lists' destination-block groups on a plan-cache miss: 1 = the GPU for
+    lists of >= 16384 wavefront ops (default), 0 = always the host, 2 = the GPU wherever they apply
+    (costa_hip_set_list_builder)."""
+    _check(lib().costa_hip_set_list_builder(int(mode)))
+
+
+@dataclass
+class WorkLists:
+    ordered: np.ndarray  # TILE_OP_DTYPE: [shaped ops | groups' headers and ops | wavefront pieces]
+    work: np.ndarray     # uint64: sub-tile items, then the groups' header indices
+    meta: dict           # the work_split counts (costa_hip_work_export)
+    on_gpu: bool         # the GPU built the destination-block groups
+
+
+_WORK_META = ("n_large", "n_medium", "n_skew", "n_cblock", "cblock_lds", "cb_map", "tiny_first",
+              "n_tiny", "n_ordered", "n_work", "on_gpu", "flags")
+
+
+def work_export(dtype, ops: np.ndarray, kind: str = "local", device=None) -> WorkLists:
+    """The executor's work lists of one tile-op list (costa_hip_work_export): built on the host, or
+    with ``device`` set with the destination-block groups on that GPU.  No kernel runs."""
+    code = dtype_code(dtype)
+    ops = np.ascontiguousarray(ops, dtype=TILE_OP_DTYPE)
+    k = {"local": 0, "pack": 1, "unpack": 2}[kind]
+    dev = -1 if device is None else int(device)
+    meta = (C.c_int64 * 12)()
+    L = lib()
+    _check(L.costa_hip_work_export(code, ops.ctypes.data, ops.size, k, dev, None, 0, None, 0, meta))
+    o = np.zeros(meta[8], TILE_OP_DTYPE)
+    w = np.zeros(meta[9], np.uint64)
+    _check(L.costa_hip_work_export(code, ops.ctypes.data, ops.size, k, dev, o.ctypes.data, o.size,
+                                   w.ctypes.data, w.size, meta))
+    m = dict(zip(_WORK_META, list(meta)))
+    return WorkLists(o, w, m, bool(m["on_gpu"]))
 
 
 def set_host_staging(mode: int):

@@ -392,6 +392,38 @@ int costa_hip_set_planner(int mode) {
     });
 }
 
+int costa_hip_set_list_builder(int mode) {
+    return guarded([&] {
+        if (mode < 0 || mode > 2) throw costa::engine::error(COSTA_ERR_ARG, "mode must be 0, 1 or 2");
+        costa::engine::set_list_builder_mode(mode);
+    });
+}
+
+int costa_hip_work_export(int dtype, const costa_tile_op_t* ops, int64_t n_ops, int kind, int device,
+                          costa_tile_op_t* ordered, int64_t cap_ordered, uint64_t* work,
+                          int64_t cap_work, int64_t* meta) {
+    auto body = [&] {
+        if (!meta || (n_ops > 0 && !ops) || n_ops < 0) throw costa::engine::error(COSTA_ERR_ARG, "null argument");
+        if (dtype < COSTA_FLOAT || dtype > COSTA_INT32) throw costa::engine::error(COSTA_ERR_ARG, "bad dtype");
+        if (kind < 0 || kind > 2) throw costa::engine::error(COSTA_ERR_ARG, "kind must be 0, 1 or 2");
+        std::vector<costa_tile_op_t> in(ops, ops + n_ops), o;
+        std::vector<uint64_t> w;
+        costa::engine::work_split ws;
+        const bool on_gpu = costa::engine::work_export(
+            costa_dtype_t(dtype), in, costa::engine::list_kind(kind), device, o, w, ws);
+        const int64_t m[12] = {ws.n_large, ws.n_medium, ws.n_skew, ws.n_cblock, ws.cblock_lds, ws.cb_map,
+                               ws.tiny_first, ws.n_tiny, int64_t(o.size()), int64_t(w.size()), on_gpu,
+                               int64_t(ws.tr_shape) | int64_t(ws.sq) << 1 | int64_t(ws.full) << 2 |
+                                   int64_t(ws.med_full) << 3 | int64_t(ws.med_sq) << 4 |
+                                   int64_t(ws.skew_wide) << 5};
+        std::memcpy(meta, m, sizeof(m));
+        if (ordered && cap_ordered >= int64_t(o.size()) && !o.empty())
+            std::memcpy(ordered, o.data(), o.size() * sizeof(o[0]));
+        if (work && cap_work >= int64_t(w.size()) && !w.empty()) std::memcpy(work, w.data(), w.size() * sizeof(w[0]));
+    };
+    return device >= 0 ? gpu_guarded(body) : guarded(body);  // (the host builder touches no GPU)
+}
+
 int costa_hip_set_profiling(int on) {
     costa::engine::set_profiling(on != 0);
     return COSTA_OK;

@@ -529,3 +529,7 @@ std::unique_ptr<plan> make_plan_device(const std::vector<job>& jobs, int rank, i
 
 }  // namespace engine
 }  // namespace costa
+
+// The work lists' destination-block groups on the GPU: in this translation unit so that both share
+// one code object and their rocPRIM kernels (the first GPU plan of a process loads both).
+#include "device_lists.hip"

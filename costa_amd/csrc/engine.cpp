@@ -603,7 +603,7 @@ namespace {
 // (tuning): off.
 int64_t cblock_groups(costa_dtype_t dtype, std::vector<const costa_tile_op_t*>& wave_ops, list_kind kind,
                       std::vector<costa_tile_op_t>& ordered, std::vector<uint64_t>& work, int64_t& lds,
-                      int& map) {
+                      int& map, const std::vector<costa_tile_op_t>& ops, device_section* dev) {
     static const int on = [] {
         const char* s = tuning_env("COSTA_CBLOCK");
         return s ? std::atoi(s) : 1;
@@ -630,6 +630,29 @@ int64_t cblock_groups(costa_dtype_t dtype, std::vector<const costa_tile_op_t*>& 
     // a range of n elements starting off the 16-byte grid spans up to n + V - 1 elements of
     // whole vectors: the workgroup's kCblockChunks vectors a thread must cover that
     const int64_t budget = cblock_max_elems(E) - (16 / E - 1);
+    // on the GPU (device_lists.hip) for long lists: the same groups, order and bytes
+    const int lb_mode = list_builder_mode();
+    if (dev && dev->device >= 0 && (dev->force || lb_mode == 2 || (lb_mode == 1 && wave_ops.size() >= kDeviceGroupsMin))) {
+        std::vector<uint32_t> wave(wave_ops.size());
+        for (size_t i = 0; i < wave_ops.size(); ++i) wave[i] = uint32_t(wave_ops[i] - ops.data());
+        std::vector<char> taken;
+        const int64_t ng = cblock_groups_device(E, budget, vec_bits, bands_env, ops, wave, ordered.size(), *dev,
+                                                taken, lds, map);
+        if (ng >= 0) {
+            if (ng > 0) {
+                dev->at_work = work.size();
+                size_t o = 0;
+                for (size_t i = 0; i < wave_ops.size(); ++i)
+                    if (!taken[i]) wave_ops[o++] = wave_ops[i];
+                wave_ops.resize(o);
+                g_stats.device_lists++;
+            }
+            if (trace)
+                std::fprintf(stderr, "[costa groups] %lld groups built on the GPU in %.2f ms\n", (long long)ng,
+                             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+            return ng;
+        }
+    }
     struct cand {
         uint64_t lo, hi;
         int32_t ldd;
@@ -1054,7 +1077,7 @@ bool granule_split(const std::vector<costa_tile_op_t>& ops, int64_t E, int64_t m
 
 work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops_in,
                       std::vector<costa_tile_op_t>& ordered, std::vector<uint64_t>& work,
-                      list_kind kind) {
+                      list_kind kind, device_section* dev) {
     const bool pack_list = kind == list_pack, local = kind == list_local;
     // Sources off the 16-byte grid: 4-byte elements are read as 16-byte vectors anyway (dword
     // alignment suffices for global_load_dwordx4): fp32 16384^2 'T' with lld 16386 0.405 against
@@ -1378,7 +1401,8 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     // destination-block groups out of the wavefront ops (after the skew items in `work`)
     int64_t cblock_lds = 0;
     int cb_map = cb_round_robin;
-    const int64_t n_cblock = cblock_groups(dtype, wave_ops, kind, ordered, work, cblock_lds, cb_map);
+    const int64_t n_cblock = cblock_groups(dtype, wave_ops, kind, ordered, work, cblock_lds, cb_map, ops, dev);
+    const size_t n_dev = dev ? dev->n_ordered : 0;  // the groups' entries left on the GPU
     lap(1);
     // ops are independent (disjoint destinations), so any order is valid; neighbours in
     // memory run at the same time and share the partially used cache lines at their edges.
@@ -1471,7 +1495,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     w.cblock_lds = cblock_lds;
     w.cb_map = cb_map;
 
-    w.tiny_first = int64_t(ordered.size());
+    w.tiny_first = int64_t(ordered.size() + n_dev);
     w.n_tiny = int64_t(at_piece[nw]);
     const size_t base = ordered.size();
     ordered.resize(base + at_piece[nw]);
@@ -1755,6 +1779,62 @@ void set_planner_mode(int mode) {
 }
 
 namespace {
+int g_list_builder = -1;  // costa_hip_set_list_builder / COSTA_LIST_BUILDER
+}  // namespace
+
+int list_builder_mode() {
+    if (g_list_builder < 0) {
+        const char* s = std::getenv("COSTA_LIST_BUILDER");
+        g_list_builder = s ? std::max(0, std::min(2, std::atoi(s))) : 1;
+    }
+    return g_list_builder;
+}
+
+void set_list_builder_mode(int mode) {
+    std::lock_guard<std::recursive_mutex> lk(g_mutex);
+    g_list_builder = mode;
+}
+
+namespace {
+// a work list into device memory: the host entries around the section the GPU built
+template <typename X>
+void upload_list(dbuf& d, const std::vector<X>& h, const X* sec, size_t at, size_t n, hipStream_t s) {
+    if (!sec || n == 0) return d.upload(h, s);
+    const size_t total = h.size() + n;
+    d.reserve(total * sizeof(X));
+    X* p = static_cast<X*>(d.p);
+    if (at) HIP_CHECK(hipMemcpyAsync(p, h.data(), at * sizeof(X), hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemcpyAsync(p + at, sec, n * sizeof(X), hipMemcpyDeviceToDevice, s));
+    if (h.size() > at)
+        HIP_CHECK(hipMemcpyAsync(p + at + n, h.data() + at, (h.size() - at) * sizeof(X), hipMemcpyHostToDevice, s));
+}
+}  // namespace
+
+bool work_export(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops, list_kind kind, int device,
+                 std::vector<costa_tile_op_t>& ordered, std::vector<uint64_t>& work, work_split& w) {
+    std::lock_guard<std::recursive_mutex> lk(g_mutex);
+    if (device < 0) {
+        w = build_work(dtype, ops, ordered, work, kind);
+        return false;
+    }
+    device_ctx& dc = ctx(device);
+    device_section sec;
+    sec.device = device;
+    sec.stream = dc.main;
+    sec.force = true;
+    w = build_work(dtype, ops, ordered, work, kind, &sec);
+    if (!sec.n_ordered) return false;
+    std::vector<costa_tile_op_t> o(sec.n_ordered);
+    std::vector<uint64_t> k(sec.n_work);
+    HIP_CHECK(hipMemcpyAsync(o.data(), sec.d_ordered, o.size() * sizeof(o[0]), hipMemcpyDeviceToHost, dc.main));
+    HIP_CHECK(hipMemcpyAsync(k.data(), sec.d_work, k.size() * sizeof(k[0]), hipMemcpyDeviceToHost, dc.main));
+    HIP_CHECK(hipStreamSynchronize(dc.main));
+    ordered.insert(ordered.begin() + std::ptrdiff_t(sec.at_ordered), o.begin(), o.end());
+    work.insert(work.begin() + std::ptrdiff_t(sec.at_work), k.begin(), k.end());
+    return true;
+}
+
+namespace {
 // the plan of a cache miss, built on the GPU when the planner mode asks for it and the layouts
 // allow it (make_plan_device), else on the host; both give the same plan
 std::unique_ptr<plan> plan_jobs(const std::vector<job>& jobs, comm* c, hipStream_t s) {
@@ -1950,7 +2030,15 @@ cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
     cp->ax_local = any_axpby(p.local_ops);
     std::vector<costa_tile_op_t> ord_l;
     std::vector<uint64_t> w_l;
-    cp->l_local = build_work(p.dtype, p.local_ops, ord_l, w_l);
+    // the destination-block groups of long lists are built on the GPU and stay there (sec_*)
+    auto section = [&] {
+        device_section d;
+        d.device = c->device;
+        d.stream = dc.main;
+        return d;
+    };
+    device_section sec_l = section();
+    cp->l_local = build_work(p.dtype, p.local_ops, ord_l, w_l, list_local, &sec_l);
     // exchange rounds: pack ops go to the round of their first element (every element a round
     // sends is packed by then), unpack ops to the round of their last (every element they read
     // has arrived)
@@ -1964,23 +2052,26 @@ cached_plan* get_plan(const std::vector<job>& jobs, comm* c, device_ctx& dc) {
     }
     std::vector<std::vector<costa_tile_op_t>> ord_p(static_cast<size_t>(R)), ord_u(static_cast<size_t>(R));
     std::vector<std::vector<uint64_t>> w_p(static_cast<size_t>(R)), w_u(static_cast<size_t>(R));
+    std::vector<device_section> sec_u(static_cast<size_t>(R), section());
     for (int r = 0; r < R; ++r) {
         auto x = std::make_unique<cached_plan::xround>();
         x->tr_unpack = any_transpose(up[size_t(r)]);
         x->ax_unpack = any_axpby(up[size_t(r)]);
         x->l_pack = build_work(p.dtype, pk[size_t(r)], ord_p[size_t(r)], w_p[size_t(r)], list_pack);
-        x->l_unpack = build_work(p.dtype, up[size_t(r)], ord_u[size_t(r)], w_u[size_t(r)], list_unpack);
+        x->l_unpack = build_work(p.dtype, up[size_t(r)], ord_u[size_t(r)], w_u[size_t(r)], list_unpack,
+                                 &sec_u[size_t(r)]);
         cp->rounds.push_back(std::move(x));
     }
     t_work = now() - t0 - t_resid - t_plan;
-    cp->d_local.upload(ord_l, dc.main);
-    cp->w_local.upload(w_l, dc.main);
+    upload_list(cp->d_local, ord_l, sec_l.d_ordered, sec_l.at_ordered, sec_l.n_ordered, dc.main);
+    upload_list(cp->w_local, w_l, sec_l.d_work, sec_l.at_work, sec_l.n_work, dc.main);
     for (int r = 0; r < R; ++r) {
         auto& x = *cp->rounds[size_t(r)];
+        const device_section& su = sec_u[size_t(r)];
         x.d_pack.upload(ord_p[size_t(r)], dc.main);
         x.w_pack.upload(w_p[size_t(r)], dc.main);
-        x.d_unpack.upload(ord_u[size_t(r)], dc.main);
-        x.w_unpack.upload(w_u[size_t(r)], dc.main);
+        upload_list(x.d_unpack, ord_u[size_t(r)], su.d_ordered, su.at_ordered, su.n_ordered, dc.main);
+        upload_list(x.w_unpack, w_u[size_t(r)], su.d_work, su.at_work, su.n_work, dc.main);
     }
     HIP_CHECK(hipStreamSynchronize(dc.main));  // host vectors above are temporaries
     if (trace)

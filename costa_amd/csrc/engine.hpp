@@ -274,9 +274,43 @@ struct work_split {
 // their order), which changes the wavefront ops' order (wave_knobs::sort); local lists (both
 // sides user matrices) cut copy ops finer than pack / unpack lists (tiny_copy_budget)
 enum list_kind { list_local, list_pack, list_unpack };
+// The part of a work list that build_work left on the GPU: the destination-block groups built by
+// device_lists.hip.  `ordered` entries [at_ordered, at_ordered + n_ordered) and `work` entries
+// [at_work, at_work + n_work) are d_ordered / d_work; the host vectors hold all the others, without
+// a gap.  A caller that passes one (device, stream set) lets build_work build the groups there
+// (list_builder_mode; `force`: wherever it applies).
+struct device_section {
+    int device = -1;
+    void* stream = nullptr;  // hipStream_t
+    bool force = false;
+    std::shared_ptr<void> mem;  // owns d_ordered and d_work
+    costa_tile_op_t* d_ordered = nullptr;
+    uint64_t* d_work = nullptr;
+    size_t at_ordered = 0, n_ordered = 0, at_work = 0, n_work = 0;
+};
 work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops,
                       std::vector<costa_tile_op_t>& ordered, std::vector<uint64_t>& work,
-                      list_kind kind = list_local);
+                      list_kind kind = list_local, device_section* dev = nullptr);
+// builder of the destination-block groups on a plan-cache miss (costa_hip_set_list_builder,
+// COSTA_LIST_BUILDER): 0 the host, 1 the GPU for lists of at least kDeviceGroupsMin wavefront ops
+// (default), 2 the GPU wherever it applies
+constexpr size_t kDeviceGroupsMin = 16384;
+int list_builder_mode();
+void set_list_builder_mode(int mode);
+// engine.cpp cblock_groups on the GPU (device_lists.hip): the same groups in the same order, the
+// same bytes.  `wave`: the wavefront ops as indices into `ops`, in list order; base_at: the size of
+// `ordered` so far (header indices count from there).  Fills sec's device part and `taken` (per
+// wavefront op: it joined a group); -> the number of groups, or -1 when the GPU declines (keys
+// wider than 64 bits) and the host builder must run.
+int64_t cblock_groups_device(int64_t E, int64_t budget, uint32_t vec_bits, int bands_env,
+                             const std::vector<costa_tile_op_t>& ops, const std::vector<uint32_t>& wave,
+                             size_t base_at, device_section& sec, std::vector<char>& taken,
+                             int64_t& lds, int& map);
+// one list's work lists, built on the host (device < 0) or with the groups on GPU `device`, copied
+// out whole (costa_hip_work_export); -> whether the GPU built part of them
+bool work_export(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& ops, list_kind kind,
+                 int device, std::vector<costa_tile_op_t>& ordered, std::vector<uint64_t>& work,
+                 work_split& w);
 // launch arguments of one ordered op list
 launch_args make_launch(const work_split& w, const void* d_ordered, const void* d_work,
                         const char* src_base, char* dst_base, const void* d_scalars, bool transpose,

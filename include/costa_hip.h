@@ -235,6 +235,8 @@ typedef struct {
        (the large, square, medium and 32 x 32 shapes), skew_kernel sub-tiles, cblock_kernel
        destination-block groups, tiny_kernel wavefront pieces */
     int64_t tile_items, skew_items, cblock_items, tiny_items;
+    int64_t device_lists; /* work lists whose destination-block groups were built on the GPU
+                             (costa_hip_set_list_builder) */
 } costa_stats_t;
 int costa_hip_set_profiling(int on);
 int costa_hip_get_stats(costa_stats_t* out, int reset);
@@ -271,6 +273,23 @@ int costa_hip_plan_export_device(int device, int n, const costa_layout_t* A, con
                                  costa_tile_op_t* pack_ops, costa_tile_op_t* unpack_ops,
                                  int64_t* send_counts, int64_t* send_displs, int64_t* recv_counts,
                                  int64_t* recv_displs, void* scalars);
+
+/* Builder of the executor's work lists on a plan-cache miss (after the planner): the
+ * destination-block groups of the wavefront ops -- components of ops that tile a destination
+ * range exactly, cut into column bands, in destination / XCD-slice order -- are 1 (default) built
+ * on the GPU for lists of at least 16384 wavefront ops, 0 always on the host, 2 on the GPU wherever
+ * they apply (env COSTA_LIST_BUILDER).  The lists are identical either way. */
+int costa_hip_set_list_builder(int mode);
+/* The executor's work lists of one tile-op list (diagnostics and tests; no kernel runs):
+ * `kind` 0 local, 1 pack (destination = a dense package), 2 unpack; device < 0 builds them on the
+ * host, device >= 0 with the destination-block groups on that GPU.  meta[12] receives n_large,
+ * n_medium, n_skew, n_cblock, cblock_lds, cb_map, tiny_first, n_tiny, n_ordered, n_work, whether the
+ * GPU built part of them, and the flags (bit 0 tr_shape, 1 sq, 2 full, 3 med_full, 4 med_sq,
+ * 5 skew_wide).  `ordered` (cap_ordered ops) and `work` (cap_work entries) are filled when their
+ * capacities suffice (NULL: sizes only). */
+int costa_hip_work_export(int dtype, const costa_tile_op_t* ops, int64_t n_ops, int kind, int device,
+                          costa_tile_op_t* ordered, int64_t cap_ordered, uint64_t* work,
+                          int64_t cap_work, int64_t* meta);
 
 #ifdef __cplusplus
 }

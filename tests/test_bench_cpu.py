@@ -430,4 +430,4 @@ def test_entries_name_the_kernels_that_ran():
     assert bench.kernels_ran({"tile_items": 4096 * 5}, 5, "double") == {"tile_kernel<double>": 4096}
     import costa_amd
     names = [f for f, _ in costa_amd.Stats._fields_]
-    assert names[-4:] == ["tile_items", "skew_items", "cblock_items", "tiny_items"]
+    assert names[-5:] == ["tile_items", "skew_items", "cblock_items", "tiny_items", "device_lists"]
