@@ -222,12 +222,12 @@ inline int64_t cblock_max_elems(int64_t E) { return int64_t(kCblockThreads) * kC
 // XCDs; chunks of kCblockXcdChunk consecutive groups go to one XCD, the 8 XCDs on 8 adjacent
 // chunks; the last partial round of chunks keeps the plain order.  A permutation of [0, nb)
 // (tools/work_check.cpp xcd).  (constexpr: host and device.)
-constexpr int64_t kCblockXcdChunk = 4;
-constexpr int64_t cblock_xcd_order(int64_t b, int64_t nb) {
-    return b / (8 * kCblockXcdChunk) * (8 * kCblockXcdChunk) + 8 * kCblockXcdChunk <= nb
-               ? b / (8 * kCblockXcdChunk) * (8 * kCblockXcdChunk) + (b % 8) * kCblockXcdChunk +
-                     (b / 8) % kCblockXcdChunk
-               : b;
+// r6: 16 (traffic of cfg 5 'T' 1.134x -> 1.050x of its algorithmic bytes; chunks of 4 / 8 / 12 /
+// 16 in-run 0.600 / 0.602 / 0.605 / 0.605 ms, rocprofv3 590.7 / 591.4 / 589.5 / 595.5 us;
+// profiles/r6m/, r6n/)
+constexpr int64_t kCblockXcdChunk = 16;
+constexpr int64_t cblock_xcd_order(int64_t b, int64_t nb, int64_t ch = kCblockXcdChunk) {
+    return b / (8 * ch) * (8 * ch) + 8 * ch <= nb ? b / (8 * ch) * (8 * ch) + (b % 8) * ch + (b / 8) % ch : b;
 }
 // work-list position of workgroup b of nb when XCD x (= b mod 8) walks the x-th of 8 contiguous
 // slices of the list, slice x holding nb / 8 items (one more for the first nb mod 8 slices).  A

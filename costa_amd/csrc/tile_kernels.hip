@@ -1074,20 +1074,22 @@ template <typename T, bool TR, bool AX>
 __global__ __launch_bounds__(CB_NT) void cblock_kernel(const costa_tile_op_t* __restrict__ ops,
                                                        const uint64_t* __restrict__ work,
                                                        const char* src_base, char* dst_base,
-                                                       const T* __restrict__ scalars, int map) {
+                                                       const T* __restrict__ scalars, int map, int chunk) {
     constexpr int V = 16 / int(sizeof(T)), NW = CB_NT / 64;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     T* img = reinterpret_cast<T*>(smem);
     // Transposing lists: workgroups are dealt round-robin over the 8 XCDs; renumbered so that
-    // each XCD takes 4 consecutive groups of the destination order and the 8 XCDs work on 8
-    // adjacent such chunks -- neighbouring groups read the other parts of the same source cache
-    // lines, now in one L2.  cfg 5 'T' 0.634 -> 0.600 ms (chunks of 2 / 16: 0.603 / 0.605; one
-    // contiguous slice per XCD 0.625, its L2 -> memory reads -36 %); the copy ('N') is level or
-    // slower every way (8 slices: +5 %) and keeps the plain order (profiles/r5ab/, r5ac/)
+    // each XCD takes `chunk` (kCblockXcdChunk) consecutive groups of the destination order and
+    // the 8 XCDs work on 8 adjacent such chunks -- neighbouring groups read the other parts of the
+    // same source cache lines, now in one L2.  cfg 5 'T' 0.634 -> 0.600 ms with chunks of 4 (r5;
+    // one contiguous slice per XCD 0.625, its L2 -> memory reads -36 %); r6: 16, the source lines
+    // shared across a chunk boundary a quarter as often -- reads 1.190x -> 1.065x their bytes,
+    // traffic 1.134x -> 1.050x, for +0.7 % in-run (8: 1.107x at +0.2 %, 32 / 64 1.044x / 1.033x
+    // at +1.4 / +2.6 %; profiles/r6m/, r6n/).  The copy ('N') uses the XCD column bands
     // (map == cb_xcd_bands: XCD x walks the x-th slice of the list, one band of target columns;
     // engine.cpp cblock_groups)
     uint64_t g = blockIdx.x;
-    if (map == cb_xcd_chunks) g = uint64_t(cblock_xcd_order(int64_t(blockIdx.x), int64_t(gridDim.x)));
+    if (map == cb_xcd_chunks) g = uint64_t(cblock_xcd_order(int64_t(blockIdx.x), int64_t(gridDim.x), chunk));
     else if (map == cb_xcd_bands) g = uint64_t(xcd_slice_order(int64_t(blockIdx.x), int64_t(gridDim.x)));
     const uint64_t h = work[g];
     const costa_tile_op_t hd = ops[h];
@@ -1251,11 +1253,16 @@ __global__ __launch_bounds__(CB_NT) void cblock_kernel(const costa_tile_op_t* __
 template <typename T, bool TR, bool AX>
 void launch_cblock_v(const launch_args& a, const uint64_t* work, int64_t n, hipStream_t stream) {
     const size_t lds = size_t(a.cblock_lds) * sizeof(T);
+    static const int chunk = [] {  // COSTA_CB_CHUNK (tuning): groups per XCD chunk
+        const char* v = tuning_env("COSTA_CB_CHUNK");
+        return v ? std::max(1, std::atoi(v)) : int(kCblockXcdChunk);
+    }();
     const int64_t max_grid = 1LL << 30;
     for (int64_t off = 0; off < n; off += max_grid) {
         const int64_t m = std::min(max_grid, n - off);
         hipLaunchKernelGGL((cblock_kernel<T, TR, AX>), dim3(unsigned(m)), dim3(CB_NT), lds, stream, a.ops,
-                           work + off, a.src_base, a.dst_base, static_cast<const T*>(a.scalars), a.cb_map);
+                           work + off, a.src_base, a.dst_base, static_cast<const T*>(a.scalars), a.cb_map,
+                           chunk);
     }
 }
 template <typename T>

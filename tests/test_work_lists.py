@@ -56,7 +56,8 @@ def test_work_lists_cfg5(tmp_path):
 TUNING = {"COSTA_TINY_SORT": "0", "COSTA_FORCE_SQ": "1", "COSTA_LARGE_SORT": "0", "COSTA_XCD_BANDS": "0",
           "COSTA_WAVE_POLICY": "1", "COSTA_MERGE": "0", "COSTA_SKEW": "0", "COSTA_TINY_LDS": "1024",
           "COSTA_TINY_COPY": "512", "COSTA_TR_SIDE": "4", "COSTA_MISALIGNED_VEC": "3",
-          "COSTA_SKEW_XCD": "2", "COSTA_CBLOCK": "0", "COSTA_CB_BANDS": "0", "COSTA_COPY_GRANULE": "0"}
+          "COSTA_SKEW_XCD": "2", "COSTA_CBLOCK": "0", "COSTA_CB_BANDS": "0", "COSTA_COPY_GRANULE": "0",
+          "COSTA_CB_CHUNK": "16"}
 
 
 @pytest.mark.skipif(shutil.which("g++") is None, reason="no g++")
