@@ -82,6 +82,33 @@ def main():
     if not np.array_equal(C2.cpu().numpy().view(np.uint64), exp2.view(np.uint64)):
         bad.append(f"{m2}^2 fp64 T alpha beta 80^2 blocks")
     del A2, C2
+    # ragged custom layouts whose C blocks are their own buffers (test_gpu_cblock's geometry): the
+    # unpack lists' destination-block groups, 'N' and 'T' alpha / beta, against the oracle
+    from casegen import Custom
+    rng3 = np.random.default_rng(23)
+
+    def splits(n, lo, hi):
+        sp = [0]
+        while sp[-1] < n:
+            sp.append(min(n, sp[-1] + int(rng3.integers(lo, hi + 1))))
+        return sp
+    for op3, al3, be3 in (("N", 1.0, 0.0), ("T", -0.5, 2.0)):
+        m3, n3 = 1100, 900
+        am, an = (n3, m3) if op3 == "T" else (m3, n3)
+        rs, cs = splits(am, 8, 60), splits(an, 8, 60)
+        CA = Custom(rs, cs, np.zeros((len(rs) - 1, len(cs) - 1), np.int32), gap=1)
+        rs, cs = splits(m3, 30, 220), splits(n3, 30, 220)
+        CC = Custom(rs, cs, np.zeros((len(rs) - 1, len(cs) - 1), np.int32), gap=0)
+        a3 = oracle.gen(oracle.FLOAT, 1, 0, CA.buf_elems(0, 1))
+        c3 = oracle.gen(oracle.FLOAT, 2, 0, CC.buf_elems(0, 1))
+        exp3 = c3.copy()
+        oracle.transform(oracle.FLOAT, op3, al3, be3, CA.geom(1), [a3], CC.geom(1), [exp3])
+        da3, dc3 = dev(a3), dev(c3)
+        costa.transform(CA.make_layout(0, da3.data_ptr(), 1, oracle.FLOAT),
+                        CC.make_layout(0, dc3.data_ptr(), 1, oracle.FLOAT), comm, op3, al3, be3)
+        torch.cuda.synchronize()
+        if dc3.cpu().numpy().tobytes() != exp3.tobytes():
+            bad.append(f"custom {op3} groups")
     # stream-ordered: A changes on torch's stream between queued transforms
     s = torch.cuda.current_stream()
     for k in range(4):
@@ -140,6 +167,7 @@ def main():
     print("HOST", host_groups)
     print("DIRECT", direct_groups)
     st = costa.get_stats()
+    print("LISTS", st["device_lists"])  # work lists whose groups the GPU built
     for b in bad:
         print("FAIL", b)
     print("OK" if not bad else "BAD", n + 1, st["pack_launches"], st["unpack_launches"],

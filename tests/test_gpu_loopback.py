@@ -15,10 +15,13 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("mode,slot,planner", [("1", None, None), ("2", None, None),
-                                               ("2", "1", None), ("1", None, "2")])
+                                               ("2", "1", None), ("1", None, "2"),
+                                               ("1", None, "lists"), ("2", None, "lists")])
 def test_loopback_exchange_matches_golden(mode, slot, planner):
     """slot "1": 1 MiB host pipeline slots (many groups, ops cut into pieces); planner "2": every
-    plan (pack / unpack lists, package geometry) built by the device planner"""
+    plan (pack / unpack lists, package geometry) built by the device planner; "lists": that, and
+    the destination-block groups of every local and unpack list built on the GPU
+    (COSTA_LIST_BUILDER=2)"""
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -28,7 +31,9 @@ def test_loopback_exchange_matches_golden(mode, slot, planner):
         env["COSTA_HOST_SLOT_MIB"] = slot
         env["COSTA_TUNING"] = "1"  # the slot size is a tuning override
     if planner:
-        env["COSTA_PLANNER"] = planner
+        env["COSTA_PLANNER"] = "2"
+    if planner == "lists":
+        env["COSTA_LIST_BUILDER"] = "2"
     r = subprocess.run([sys.executable, child], env=env, capture_output=True, text=True,
                        timeout=600)
     out = r.stdout.strip().splitlines()
@@ -38,6 +43,9 @@ def test_loopback_exchange_matches_golden(mode, slot, planner):
     direct = [l for l in out if l.startswith("DIRECT")]
     # page-locked host cases: pack / unpack groups moved by strided DMA (one rectangle per group)
     assert direct and int(direct[-1].split()[1]) > 0, "no direct (DMA) group ran from page-locked memory"
+    if planner == "lists" and mode == "1":  # (mode 2 splits a block's tiles between two lists)
+        lists = [l for l in out if l.startswith("LISTS")]
+        assert lists and int(lists[-1].split()[1]) > 0, "no work list built on the GPU"
     _, n, packs, unpacks, locals_ = out[-1].split()
     assert int(packs) >= int(n) and int(unpacks) >= int(n), out[-1]  # every case exchanged
     if mode == "1":
