@@ -458,6 +458,26 @@ void xcd_bands(const std::vector<const costa_tile_op_t*>& ops, int64_t E, int k,
     std::stable_sort(perm.begin(), perm.end(), [&](uint32_t x, uint32_t y) { return band[x] < band[y]; });
 }
 
+// (key, item) pairs whose items ascend in list order, sorted by key with equal keys in item
+// order -- what std::sort of the pairs gives -- by a stable LSD radix sort of 16-bit digits over
+// the keys' span (cfg 4's 262 k sub-tiles: a comparison sort cost ~7 ms of a plan-cache miss)
+void sort_pairs_by_key(std::vector<std::pair<uint64_t, uint64_t>>& kv) {
+    const size_t n = kv.size();
+    if (n < 2) return;
+    uint64_t lo = ~uint64_t(0), hi = 0;
+    for (const auto& p : kv) lo = std::min(lo, p.first), hi = std::max(hi, p.first);
+    std::vector<std::pair<uint64_t, uint64_t>> tmp(n);
+    std::vector<uint32_t> at((size_t(1) << 16) + 1);
+    const uint64_t span = hi - lo;
+    for (int sh = 0; sh == 0 || (sh < 64 && (span >> sh) != 0); sh += 16) {
+        std::fill(at.begin(), at.end(), 0u);
+        for (const auto& p : kv) ++at[(((p.first - lo) >> sh) & 0xFFFFu) + 1];
+        for (size_t d = 1; d < at.size(); ++d) at[d] += at[d - 1];
+        for (const auto& p : kv) tmp[at[((p.first - lo) >> sh) & 0xFFFFu]++] = p;
+        kv.swap(tmp);
+    }
+}
+
 // Merges ops that continue each other: the op whose source starts where op a's source ends along
 // s (a.src + a.ns * lds) and whose destination continues a's the same way (one destination
 // stride further for copies, ns elements further for transposes), with the same extent along f,
@@ -474,13 +494,31 @@ void merge_adjacent(std::vector<costa_tile_op_t>& v, int64_t E, std::vector<uint
     }
     if (v.size() < 2) return;
     for (int pass = 0; pass < 2; ++pass) {  // 0: along s, 1: along f
-        std::unordered_map<uint64_t, uint32_t> by_src;
-        by_src.reserve(v.size() * 2);
-        for (size_t i = 0; i < v.size(); ++i) by_src.emplace(v[i].src, uint32_t(i));
-        std::vector<char> gone(v.size(), 0);
+        // the ops in source order (a radix sort of (src, index)), and an open-addressing table
+        // src -> the first op of that source address (std::unordered_map and std::sort cost cfg 3 /
+        // cfg 4's 65 k-op lists ~5 ms of a plan-cache miss)
+        std::vector<std::pair<uint64_t, uint64_t>> kv(v.size());
+        for (size_t i = 0; i < v.size(); ++i) kv[i] = {v[i].src, i};
+        sort_pairs_by_key(kv);
         std::vector<uint32_t> idx(v.size());
-        for (size_t i = 0; i < v.size(); ++i) idx[i] = uint32_t(i);
-        std::sort(idx.begin(), idx.end(), [&](uint32_t x, uint32_t y) { return v[x].src < v[y].src; });
+        for (size_t k = 0; k < v.size(); ++k) idx[k] = uint32_t(kv[k].second);
+        int tb = 4;
+        while ((size_t(1) << tb) < 2 * v.size()) ++tb;
+        const size_t tmask = (size_t(1) << tb) - 1;
+        std::vector<std::pair<uint64_t, uint32_t>> table(tmask + 1, {~uint64_t(0), 0u});
+        auto slot_of = [&](uint64_t a) { return size_t((a * 0x9E3779B97F4A7C15ull) >> (64 - tb)); };
+        for (size_t i = 0; i < v.size(); ++i) {  // ascending index: the first op of a src stays
+            size_t h = slot_of(v[i].src);
+            while (table[h].first != ~uint64_t(0) && table[h].first != v[i].src) h = (h + 1) & tmask;
+            if (table[h].first == ~uint64_t(0)) table[h] = {v[i].src, uint32_t(i)};
+        }
+        auto find_src = [&](uint64_t a) -> int64_t {  // the first op at source address a, or -1
+            for (size_t h = slot_of(a);; h = (h + 1) & tmask) {
+                if (table[h].first == a) return int64_t(table[h].second);
+                if (table[h].first == ~uint64_t(0)) return -1;
+            }
+        };
+        std::vector<char> gone(v.size(), 0);
         for (const uint32_t i : idx) {
             if (gone[i]) continue;
             costa_tile_op_t& a = v[i];
@@ -490,9 +528,9 @@ void merge_adjacent(std::vector<costa_tile_op_t>& v, int64_t E, std::vector<uint
                 const uint64_t next_src = a.src + uint64_t(pass == 0 ? n * a.lds * E : n * E);
                 const uint64_t next_dst =
                     a.dst + uint64_t(pass == 0 ? (tr ? n : n * a.ldd) * E : (tr ? n * a.ldd : n) * E);
-                const auto it = by_src.find(next_src);
-                if (it == by_src.end() || gone[it->second] || it->second == i) break;
-                const costa_tile_op_t& b = v[it->second];
+                const int64_t nx = find_src(next_src);
+                if (nx < 0 || gone[nx] || uint32_t(nx) == i) break;
+                const costa_tile_op_t& b = v[size_t(nx)];
                 const uint32_t vec = COSTA_TILE_VEC_SRC | COSTA_TILE_VEC_DST;
                 const bool same = b.dst == next_dst && (b.flags & ~vec) == (a.flags & ~vec) && b.lds == a.lds &&
                                   b.ldd == a.ldd && (pass == 0 ? b.nf == a.nf : b.ns == a.ns);
@@ -500,8 +538,8 @@ void merge_adjacent(std::vector<costa_tile_op_t>& v, int64_t E, std::vector<uint
                 if (!same || total > (int64_t(1) << 30)) break;
                 (pass == 0 ? a.ns : a.nf) = int32_t(total);
                 if (!a.order) a.order = b.order;  // the merged op keeps the hint of its first tile
-                gone[it->second] = 1;
-                if (root) (*root)[id[it->second]] = id[i];
+                gone[nx] = 1;
+                if (root) (*root)[id[nx]] = id[i];
             }
         }
         size_t o = 0;
@@ -1098,10 +1136,14 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     static const bool trace = std::getenv("COSTA_PLAN_TRACE") != nullptr;
     const auto bw0 = std::chrono::steady_clock::now();
     double bw_t[4] = {0, 0, 0, 0};  // classify + shaped lists, groups, wavefront order, pieces
+    double sub_t[3] = {0, 0, 0};    // ... of the first: merge, vector flags + granule cut, classify
     auto lap = [&](int k) {
         if (!trace) return;
         const double t = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - bw0).count();
         bw_t[k] = t;
+    };
+    auto mark = [&](int k) {
+        if (trace) sub_t[k] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - bw0).count();
     };
     std::vector<costa_tile_op_t> ops_merged;
     const std::vector<costa_tile_op_t>* ops_src = &ops_in;
@@ -1124,6 +1166,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
             ops_src = &ops_merged;
         }
     }
+    mark(0);
     std::vector<costa_tile_op_t> ops_mis;
     bool mis_any = false;  // (the list is copied only when some op gains a flag: cfg 5's 245 k
                            // small ops gain none, and the copy cost a plan-cache miss ~2 ms)
@@ -1154,6 +1197,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
             ops_pre = &ops_gran;
     }
     const std::vector<costa_tile_op_t>& ops = *ops_pre;
+    mark(1);
     const bool tr_shape = any_transpose(ops);
     shape_dims sh;
     tile_shapes(dtype, tr_shape, &sh);
@@ -1272,6 +1316,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         if (cls[li] == 1) --n_med;
         cls[li] = 4;
     }
+    mark(2);
     std::vector<uint32_t> shaped[3];  // [0] large, [1] medium, [2] skew
     std::vector<costa_tile_op_t> skew_ops;
     for (size_t li = 0; li < ops.size(); ++li) {
@@ -1368,7 +1413,7 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
                     }
                 }
             }
-            std::sort(key.begin(), key.end());
+            sort_pairs_by_key(key);
             for (size_t x = 0; x < key.size(); ++x) work[w0 + x] = key[x].second;
         }
         if (c == 2 && skew_group > 1 && work.size() - w0 > 1) {
@@ -1506,9 +1551,11 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     if (trace) {
         lap(3);
         std::fprintf(stderr,
-                     "[costa build_work] %zu ops (%s list): classify + shaped %.2f ms, groups %.2f (%lld), "
+                     "[costa build_work] %zu ops (%s list): classify + shaped %.2f ms (merge %.2f, flags + "
+                     "granules %.2f, classify %.2f, work items %.2f), groups %.2f (%lld), "
                      "wavefront order %.2f, pieces %.2f (%lld)\n",
-                     ops_in.size(), pack_list ? "pack" : local ? "local" : "unpack", bw_t[0], bw_t[1] - bw_t[0],
+                     ops_in.size(), pack_list ? "pack" : local ? "local" : "unpack", bw_t[0], sub_t[0],
+                     sub_t[1] - sub_t[0], sub_t[2] - sub_t[1], bw_t[0] - sub_t[2], bw_t[1] - bw_t[0],
                      (long long)n_cblock, bw_t[2] - bw_t[1], bw_t[3] - bw_t[2], (long long)w.n_tiny);
     }
     return w;
