@@ -788,11 +788,17 @@ def kernels_ran(st: dict, steps: int, tname: str) -> dict:
     (costa_stats_t tile_items / skew_items / cblock_items / tiny_items): tile_kernel sub-tiles,
     skew_kernel sub-tiles, cblock_kernel destination-block groups, tiny_kernel wavefront pieces"""
     out = {}
+    fused = st.get("fused_pieces", 0)  # pieces run in the group kernel's launch (its tail)
+    counts = {"tile_items": st.get("tile_items", 0), "skew_items": st.get("skew_items", 0),
+              "cblock_items": st.get("cblock_items", 0), "tiny_items": st.get("tiny_items", 0) - fused,
+              "fused_pieces": fused}
     for key, name in (("tile_items", "tile_kernel"), ("skew_items", "skew_kernel"),
-                      ("cblock_items", "cblock_kernel"), ("tiny_items", "tiny_kernel")):
-        n = st.get(key, 0) / max(steps, 1)
+                      ("cblock_items", "cblock_kernel"), ("tiny_items", "tiny_kernel"),
+                      ("fused_pieces", "cblock_kernel pieces")):
+        n = counts[key] / max(steps, 1)
         if n:
-            out[f"{name}<{tname}>"] = int(n) if float(n).is_integer() else round(n, 1)
+            label = f"cblock_kernel<{tname}> pieces" if key == "fused_pieces" else f"{name}<{tname}>"
+            out[label] = int(n) if float(n).is_integer() else round(n, 1)
     return out
 
 

@@ -99,7 +99,8 @@ class Stats(C.Structure):
                 ("plan_misses", C.c_int64), ("host_groups", C.c_int64),
                 ("device_plans", C.c_int64), ("plan_ms", C.c_double), ("host_direct", C.c_int64),
                 ("host_direct_groups", C.c_int64), ("tile_items", C.c_int64), ("skew_items", C.c_int64),
-                ("cblock_items", C.c_int64), ("tiny_items", C.c_int64), ("device_lists", C.c_int64)]
+                ("cblock_items", C.c_int64), ("tiny_items", C.c_int64), ("device_lists", C.c_int64),
+                ("fused_pieces", C.c_int64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -2386,11 +2386,13 @@ void transform(const std::vector<job>& jobs, comm* c, void* user_stream, bool as
     }
 
     g_stats.transforms++;
-    auto count_items = [](const work_split& w) {
+    auto count_items = [&](const work_split& w) {
         g_stats.tile_items += w.n_large + w.n_medium;
         g_stats.skew_items += w.n_skew;
         g_stats.cblock_items += w.n_cblock;
         g_stats.tiny_items += w.n_tiny;
+        if (!dtype_is_complex(p.dtype) && pieces_in_group_launch(w.n_cblock, w.n_tiny))
+            g_stats.fused_pieces += w.n_tiny;
     };
     if (cp.l_local.n_items()) {
         g_stats.local_launches++;

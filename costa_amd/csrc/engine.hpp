@@ -209,6 +209,9 @@ struct launch_args {
 bool any_transpose(const std::vector<costa_tile_op_t>& ops);
 bool any_axpby(const std::vector<costa_tile_op_t>& ops);
 void launch_tiles(costa_dtype_t dtype, const launch_args& a, void* stream /* hipStream_t */);
+// the wavefront pieces of a list with destination-block groups run as workgroups after the groups
+// in the group kernel's launch (its tail) instead of a tiny_kernel launch (COSTA_FUSE_PIECES)
+bool pieces_in_group_launch(int64_t n_cblock, int64_t n_tiny);
 // destination columns taller than this are walked in panels of this many bytes of rows (engine.cpp
 // build_work)
 constexpr int64_t kPanelBytes = int64_t(128) << 10;

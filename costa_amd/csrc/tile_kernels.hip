@@ -1074,10 +1074,24 @@ template <typename T, bool TR, bool AX>
 __global__ __launch_bounds__(CB_NT) void cblock_kernel(const costa_tile_op_t* __restrict__ ops,
                                                        const uint64_t* __restrict__ work,
                                                        const char* src_base, char* dst_base,
-                                                       const T* __restrict__ scalars, int map, int chunk) {
+                                                       const T* __restrict__ scalars, int map, int chunk,
+                                                       int64_t n_groups, const costa_tile_op_t* __restrict__ pieces,
+                                                       int64_t n_pieces, int piece_lds) {
     constexpr int V = 16 / int(sizeof(T)), NW = CB_NT / 64;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     T* img = reinterpret_cast<T*>(smem);
+    if (int64_t(blockIdx.x) >= n_groups) {
+        // the list's wavefront pieces (tiny_kernel's work), one a wavefront, as workgroups after
+        // the groups in the same launch: dispatched last, they run in the groups' tail instead of
+        // a launch of their own (launch_cblock: fuse)
+        const int64_t b = xcd_slice_order(int64_t(blockIdx.x) - n_groups, int64_t(gridDim.x) - n_groups);
+        const int wv = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / 64);
+        const int64_t w = b * NW + wv;
+        if (w >= n_pieces) return;
+        tiny_op<T, TR, AX, tiny_copy_bytes<T>()>(pieces[w], int(threadIdx.x) % 64, img + int64_t(wv) * piece_lds,
+                                                 src_base, dst_base, scalars);
+        return;
+    }
     // Transposing lists: workgroups are dealt round-robin over the 8 XCDs; renumbered so that
     // each XCD takes `chunk` (kCblockXcdChunk) consecutive groups of the destination order and
     // the 8 XCDs work on 8 adjacent such chunks -- neighbouring groups read the other parts of the
@@ -1089,8 +1103,8 @@ __global__ __launch_bounds__(CB_NT) void cblock_kernel(const costa_tile_op_t* __
     // (map == cb_xcd_bands: XCD x walks the x-th slice of the list, one band of target columns;
     // engine.cpp cblock_groups)
     uint64_t g = blockIdx.x;
-    if (map == cb_xcd_chunks) g = uint64_t(cblock_xcd_order(int64_t(blockIdx.x), int64_t(gridDim.x), chunk));
-    else if (map == cb_xcd_bands) g = uint64_t(xcd_slice_order(int64_t(blockIdx.x), int64_t(gridDim.x)));
+    if (map == cb_xcd_chunks) g = uint64_t(cblock_xcd_order(int64_t(blockIdx.x), n_groups, chunk));
+    else if (map == cb_xcd_bands) g = uint64_t(xcd_slice_order(int64_t(blockIdx.x), n_groups));
     const uint64_t h = work[g];
     const costa_tile_op_t hd = ops[h];
     const int n_ops = int(hd.src), R = hd.nf, K = hd.ns, P = R | 1;
@@ -1251,31 +1265,37 @@ __global__ __launch_bounds__(CB_NT) void cblock_kernel(const costa_tile_op_t* __
 }
 
 template <typename T, bool TR, bool AX>
-void launch_cblock_v(const launch_args& a, const uint64_t* work, int64_t n, hipStream_t stream) {
-    const size_t lds = size_t(a.cblock_lds) * sizeof(T);
+void launch_cblock_v(const launch_args& a, const uint64_t* work, int64_t n, bool fuse, hipStream_t stream) {
     static const int chunk = [] {  // COSTA_CB_CHUNK (tuning): groups per XCD chunk
         const char* v = tuning_env("COSTA_CB_CHUNK");
         return v ? std::max(1, std::atoi(v)) : int(kCblockXcdChunk);
     }();
     const int64_t max_grid = 1LL << 30;
+    // the wavefront pieces fused into the launch (launch_t decides): CB_NT / 64 a workgroup, each
+    // wavefront its tiny_lds_budget() of the LDS when the list transposes
+    const int64_t pb = fuse ? (a.n_tiny + CB_NT / 64 - 1) / (CB_NT / 64) : 0;
+    const int piece_lds = TR ? int(tiny_lds_budget() / int64_t(sizeof(T))) : 0;
+    size_t lds = size_t(a.cblock_lds) * sizeof(T);
+    if (fuse) lds = std::max(lds, size_t(piece_lds) * sizeof(T) * size_t(CB_NT / 64));
     for (int64_t off = 0; off < n; off += max_grid) {
         const int64_t m = std::min(max_grid, n - off);
-        hipLaunchKernelGGL((cblock_kernel<T, TR, AX>), dim3(unsigned(m)), dim3(CB_NT), lds, stream, a.ops,
+        const int64_t extra = off + m >= n ? pb : 0;  // the pieces ride on the last launch
+        hipLaunchKernelGGL((cblock_kernel<T, TR, AX>), dim3(unsigned(m + extra)), dim3(CB_NT), lds, stream, a.ops,
                            work + off, a.src_base, a.dst_base, static_cast<const T*>(a.scalars), a.cb_map,
-                           chunk);
+                           chunk, m, a.ops + a.tiny_first, extra ? a.n_tiny : int64_t(0), piece_lds);
     }
 }
 template <typename T>
-void launch_cblock(const launch_args& a, const uint64_t* work, int64_t n, hipStream_t stream) {
+void launch_cblock(const launch_args& a, const uint64_t* work, int64_t n, bool fuse, hipStream_t stream) {
     if (n <= 0) return;
     if constexpr (is_cpx<T>::value) {  // real types only (engine.cpp cblock_groups)
         throw error(COSTA_ERR_INTERNAL, "costa: destination-block groups of a complex type");
     } else if (a.any_transpose)
-        a.any_axpby ? launch_cblock_v<T, true, true>(a, work, n, stream)
-                    : launch_cblock_v<T, true, false>(a, work, n, stream);
+        a.any_axpby ? launch_cblock_v<T, true, true>(a, work, n, fuse, stream)
+                    : launch_cblock_v<T, true, false>(a, work, n, fuse, stream);
     else
-        a.any_axpby ? launch_cblock_v<T, false, true>(a, work, n, stream)
-                    : launch_cblock_v<T, false, false>(a, work, n, stream);
+        a.any_axpby ? launch_cblock_v<T, false, true>(a, work, n, fuse, stream)
+                    : launch_cblock_v<T, false, false>(a, work, n, fuse, stream);
 }
 
 // One op per wavefront.  Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md,
@@ -1363,8 +1383,11 @@ void launch_t(const launch_args& a, hipStream_t stream) {
             launch_shape<T, typename shapes<T>::medium_tr>(a, a.work + a.n_large, a.n_medium, stream);
     }
     if (a.n_skew > 0) launch_skew<T>(a, a.work + a.n_large + a.n_medium, a.n_skew, stream);
-    launch_cblock<T>(a, a.work + a.n_large + a.n_medium + a.n_skew, a.n_cblock, stream);
-    launch_tiny<T>(a, stream);
+    // the wavefront pieces ride in the group launch's tail when there is one (COSTA_FUSE_PIECES=0,
+    // tuning: a launch of their own)
+    const bool fuse = !is_cpx<T>::value && pieces_in_group_launch(a.n_cblock, a.n_tiny);
+    launch_cblock<T>(a, a.work + a.n_large + a.n_medium + a.n_skew, a.n_cblock, fuse, stream);
+    if (!fuse) launch_tiny<T>(a, stream);
 }
 
 template <typename T>
@@ -1424,6 +1447,14 @@ void set_lds_limits() {
 }
 
 }  // namespace
+
+bool pieces_in_group_launch(int64_t n_cblock, int64_t n_tiny) {
+    static const bool on = [] {  // COSTA_FUSE_PIECES=0 (tuning): a launch of their own
+        const char* v = tuning_env("COSTA_FUSE_PIECES");
+        return !v || std::atoi(v) != 0;
+    }();
+    return on && n_cblock > 0 && n_tiny > 0 && n_cblock + n_tiny / (CB_NT / 64) + 1 < (int64_t(1) << 30);
+}
 
 void tile_shapes(costa_dtype_t dtype, bool transposing_list, shape_dims* d) {
     const bool t = transposing_list;

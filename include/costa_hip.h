@@ -237,6 +237,8 @@ typedef struct {
     int64_t tile_items, skew_items, cblock_items, tiny_items;
     int64_t device_lists; /* work lists whose destination-block groups were built on the GPU
                              (costa_hip_set_list_builder) */
+    int64_t fused_pieces; /* of tiny_items: wavefront pieces run as workgroups at the end of the
+                             destination-block group launch (no tiny_kernel launch of their own) */
 } costa_stats_t;
 int costa_hip_set_profiling(int on);
 int costa_hip_get_stats(costa_stats_t* out, int reset);

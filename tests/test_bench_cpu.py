@@ -428,6 +428,11 @@ def test_entries_name_the_kernels_that_ran():
     st = {"tile_items": 0, "skew_items": 0, "cblock_items": 80741 * 20, "tiny_items": 2362 * 20}
     assert bench.kernels_ran(st, 20, "float") == {"cblock_kernel<float>": 80741, "tiny_kernel<float>": 2362}
     assert bench.kernels_ran({"tile_items": 4096 * 5}, 5, "double") == {"tile_kernel<double>": 4096}
+    # pieces run at the end of the group launch are named as such, not as a tiny_kernel launch
+    st["fused_pieces"] = 2362 * 20
+    assert bench.kernels_ran(st, 20, "float") == {"cblock_kernel<float>": 80741,
+                                                  "cblock_kernel<float> pieces": 2362}
     import costa_amd
     names = [f for f, _ in costa_amd.Stats._fields_]
-    assert names[-5:] == ["tile_items", "skew_items", "cblock_items", "tiny_items", "device_lists"]
+    assert names[-6:] == ["tile_items", "skew_items", "cblock_items", "tiny_items", "device_lists",
+                          "fused_pieces"]
