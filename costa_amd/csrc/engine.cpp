@@ -639,6 +639,17 @@ namespace {
 // = number of ops, dst = the range, nf = R, ns = K, flags = the transform); `work` gets the
 // header indices in destination order; the grouped ops leave `wave_ops`.  COSTA_CBLOCK=0
 // (tuning): off.
+// the destination-block groups apply to this list (cblock_groups' own conditions, apart from the
+// list's length)
+bool cblock_enabled(costa_dtype_t dtype, list_kind kind) {
+    static const int on = [] {
+        const char* s = tuning_env("COSTA_CBLOCK");
+        return s ? std::atoi(s) : 1;
+    }();
+    const bool real = dtype == COSTA_FLOAT || dtype == COSTA_DOUBLE || dtype == COSTA_INT32;
+    return on && real && kind != list_pack;
+}
+
 int64_t cblock_groups(costa_dtype_t dtype, std::vector<const costa_tile_op_t*>& wave_ops, list_kind kind,
                       std::vector<costa_tile_op_t>& ordered, std::vector<uint64_t>& work, int64_t& lds,
                       int& map, const std::vector<costa_tile_op_t>& ops, device_section* dev) {
@@ -1306,6 +1317,13 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
     // 1.046 / 1.015 -> 0.855 / 0.837 ms, beta != 0 1.444 -> 1.244; fp32 lld + 4 / + 8 / + 24
     // 0.687 / 0.620 / 0.595 -> 0.466 / 0.482 / 0.466; aligned and 64-byte-aligned ld unchanged
     // (profiles/r4l/)
+    // (r6) ...except transposes into a destination range a destination-block group may write: a
+    // custom layout's own block buffer (leading dimension within a group's budget) is written by
+    // its group in whole 16-byte vectors whatever its alignment, so such ops stay on the wavefront
+    // path, where cblock_groups finds them; left out, their block's other ops fail the exactness
+    // test too (cfg 5 'T': 45 skew ops broke 334 groups into 2 672 wavefront pieces)
+    const bool groups_on = cblock_enabled(dtype, kind);
+    const int64_t group_budget = cblock_max_elems(E) - (16 / E - 1);
     for (size_t li = 0; skew_on && k_elems > 0 && li < ops.size(); ++li) {
         const costa_tile_op_t& op = ops[li];
         if (cls[li] == 3 || !(op.flags & COSTA_TILE_TRANSPOSE)) continue;
@@ -1314,6 +1332,10 @@ work_split build_work(costa_dtype_t dtype, const std::vector<costa_tile_op_t>& o
         if (op.dst % uint64_t(E) != 0 || 2 * int64_t(op.nf) * op.ns < k_elems)
             continue;
         if (cls[li] == 1) --n_med;
+        if (groups_on && op.ns <= op.ldd && op.ldd <= group_budget) {
+            cls[li] = 2;
+            continue;
+        }
         cls[li] = 4;
     }
     mark(2);
