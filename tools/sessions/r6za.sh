@@ -1,6 +1,6 @@
 #!/bin/bash
-# r6 final check (re-run after the GPU group builder, the 16-group chunks and the pieces in the
-# group launch), part a: tools/gpu_full.sh without its cfg 3 / 4 / 5 PMC tails (-m gpu, smoke,
+# r6 final check (re-run after the GPU group builder, the 16-group chunks, the pieces in the
+# group launch and the skew ops in groups), part a: tools/gpu_full.sh without its cfg 3 / 4 / 5 PMC tails (-m gpu, smoke,
 # bench N = 1, cfg 5 'N' / 'T' lines, rocprofv3 kernel trace of the bench and its FETCH_SIZE /
 # WRITE_SIZE passes) -> profiles/r6z (tools/save_full.py)
 set -o pipefail
